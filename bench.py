@@ -1,0 +1,323 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident GB/s of the 20-client wide_resnet16_8
+parameter reduction (BASELINE.json metric, configs[1]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+A step is one aggregation of 20 client state_dicts (wide_resnet16_8,
+CIFAR-10 layout: 82 fp32 keys + 16 int64 keys, B = 43,888,744 bytes) into the
+global state — the reference's ``server_aggregate`` arithmetic
+(train_fedavg.py:143-147) — with every input already resident in HBM.
+``value`` = algorithmic bytes (N·B read + B written, SURVEY.md §8 d) / time.
+
+N>1 (launched by torch.distributed.run, one rank per GPU): weak scaling,
+every rank holds 20 client slots; a step is the client-sharded round of
+feddct_amd/dist.py (local partial sums, RCCL all-reduce, /N_total); value =
+all ranks' algorithmic bytes / max-over-ranks time.
+
+Also reported on the same JSON line: the roofline of the reduce kernel
+(HIP-event launch time vs the 8 TB/s HBM3E peak), the CPU baseline (the
+reference loop restated in torch, oracle/torch_mirror.py, on this host's
+cores; rank 0, N=1 only), parity of the output against the reference's
+committed SHA-256 digest, and the host-inclusive rate (pinned H2D + kernel +
+D2H).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from feddct_amd import _lib  # noqa: E402  (loads libfedagg.so or fails loudly)
+from feddct_amd.layout import BucketLayout  # noqa: E402
+from feddct_amd.workload import Reducer, load_manifest, make_clients  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+LAYOUT = "wrn16_8_c10"
+N_CLIENTS = 20
+METRIC = "device-resident GB/s: 20-client wide_resnet16_8 weighted param reduction"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def timed_launches(fn, steps, warmup, sync_group=None):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if sync_group is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if sync_group is not None:
+        dist.barrier()
+    return e0.elapsed_time(e1) / 1e3 / steps, wall / steps
+
+
+def digest_of(layout, out32, out64):
+    import hashlib
+    f = out32.cpu().numpy()
+    i = out64.cpu().numpy()
+    h = hashlib.sha256()
+    for s in layout.slots:
+        src = i if s.kind == "i64" else f
+        h.update(s.key.encode())
+        h.update(np.ascontiguousarray(src[s.offset:s.offset + s.numel]).tobytes())
+    return h.hexdigest()
+
+
+def ulp_dist(a: torch.Tensor, b: torch.Tensor) -> int:
+    ia = a.view(torch.int32).to(torch.int64)
+    ib = b.view(torch.int32).to(torch.int64)
+    ia = torch.where(ia < 0, -(ia & 0x7FFFFFFF), ia)
+    ib = torch.where(ib < 0, -(ib & 0x7FFFFFFF), ib)
+    return int((ia - ib).abs().max().item())
+
+
+def pmc_traffic(n_gpus):
+    """HBM bytes per launch of the reduce kernel from the committed rocprofv3
+    PMC summary (profiles/*pmc*.json written by tools/pmc_summary.py)."""
+    path = os.path.join(ROOT, "profiles", "reduce_pmc.json")
+    if n_gpus != 1 or not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("workload") == f"{LAYOUT}/n{N_CLIENTS}":
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
+    from oracle.torch_mirror import arithmetic_core, reference_loop, time_call
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+
+    class Holder(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            for s in layout.slots:
+                parts = s.key.split(".")
+                mod = self
+                for p in parts[:-1]:
+                    if p not in mod._modules:
+                        mod.add_module(p, torch.nn.Module())
+                    mod = mod._modules[p]
+                t = torch.zeros(s.shape, dtype=s.dtype)
+                if s.dtype == torch.int64:
+                    mod.register_buffer(parts[-1], t)
+                else:
+                    mod.register_parameter(parts[-1], torch.nn.Parameter(t))
+
+    def to_module(f32, i64):
+        m = Holder()
+        fh, ih = f32.cpu(), i64.cpu()
+        sd = m.state_dict()
+        with torch.no_grad():
+            for s in layout.slots:
+                src = ih if s.kind == "i64" else fh
+                sd[s.key].copy_(src[s.offset:s.offset + s.numel].view(s.shape))
+        return m
+
+    mods = [to_module(f, i) for f, i in clients]
+    g = Holder()
+    t_loop, reps = time_call(lambda: reference_loop(g, mods), 5, budget_s * 0.8)
+    states = [m.state_dict() for m in mods]
+    t_core, _ = time_call(lambda: arithmetic_core(states), 3, budget_s * 0.2)
+    nbytes = layout.algorithmic_bytes(len(clients))
+    return {"value": round(nbytes / t_loop / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"full reference loop (K·N state_dict rebuilds + stack/mean + "
+                       f"load_state_dict + broadcast) over the same {len(clients)}-client "
+                       f"{LAYOUT} state, median of {reps} runs, {t_loop * 1e3:.1f} ms/run; "
+                       f"arithmetic-only stack+mean {t_core * 1e3:.1f} ms "
+                       f"({nbytes / t_core / 1e9:.2f} GB/s)"),
+            "loop_ms": round(t_loop * 1e3, 2), "core_ms": round(t_core * 1e3, 2),
+            "cpu": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
+    """Pinned host buckets -> H2D (N·B) -> kernel -> D2H (B), one stream."""
+    host = [(c[0].cpu().pin_memory(), c[1].cpu().pin_memory()) for c in clients]
+    out_h32 = torch.empty_like(out32, device="cpu").pin_memory()
+    out_h64 = torch.empty_like(out64, device="cpu").pin_memory()
+
+    def step():
+        for (h32, h64), (d32, d64) in zip(host, clients):
+            d32.copy_(h32, non_blocking=True)
+            d64.copy_(h64, non_blocking=True)
+        reducer_dev()
+        out_h32.copy_(out32, non_blocking=True)
+        out_h64.copy_(out64, non_blocking=True)
+
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    nbytes = layout.algorithmic_bytes(len(clients))
+    return {"GBps": round(nbytes / t / 1e9, 2), "ms": round(t * 1e3, 3), "source": "pinned"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--chunks", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=25.0)
+    ap.add_argument("--kernel-only", action="store_true",
+                    help="only the timed reduce launches (for rocprofv3 runs)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        group = dist.group.WORLD
+
+    manifest = load_manifest(LAYOUT)
+    layout = BucketLayout.from_manifest(manifest)
+    first = rank * N_CLIENTS
+    clients = make_clients(layout, manifest, range(first, first + N_CLIENTS), dev)
+    out32 = torch.zeros_like(clients[0][0])
+    out64 = torch.zeros_like(clients[0][1])
+    reducer = Reducer(layout, clients, out32, out64)
+    nbytes_rank = layout.algorithmic_bytes(N_CLIENTS)
+    torch.cuda.synchronize()
+
+    extra = {}
+    if world == 1:
+        t_step, wall = timed_launches(reducer, args.steps, args.warmup)
+        t_kernel = t_step
+        if not args.kernel_only:
+            with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+                want = json.load(f)[f"fedavg/{LAYOUT}/n{N_CLIENTS}"]
+            got = digest_of(layout, out32, out64)
+            extra["parity"] = {"vs": "reference server_aggregate SHA-256 (tests/golden)",
+                               "bit_exact": got == want}
+            # streaming-copy ceiling of this box (same 16-B nt load/store path)
+            big = torch.empty(256 * 1024 * 1024, dtype=torch.float32, device=dev)  # 1 GiB
+            big2 = torch.empty_like(big)
+
+            def copy_big():
+                _lib.check(_lib.lib.fa_copy_f32(big.data_ptr(), big2.data_ptr(), big.numel(),
+                                                torch.cuda.current_stream().cuda_stream))
+            tc, _ = timed_launches(copy_big, 20, 3)
+            extra["copy_ceiling_GBps"] = round(2 * big.numel() * 4 / tc / 1e9, 1)
+            del big, big2
+            extra["host_inclusive"] = host_inclusive(layout, clients, reducer, out32, out64)
+            # weighted variant (client-size weights, BASELINE config 4's extension)
+            from oracle.torch_order import weights_from_sizes
+            w = weights_from_sizes(np.arange(1, N_CLIENTS + 1))
+            wred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
+                           weights=w, plan=reducer.plan)
+            tw, _ = timed_launches(wred, max(10, args.steps // 2), 3)
+            extra["weighted_GBps"] = round(nbytes_rank / tw / 1e9, 1)
+            fused = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
+                            flags=_lib.FA_F_BCAST, plan=reducer.plan)
+            tb, _ = timed_launches(fused, max(10, args.steps // 2), 3)
+            extra["round_with_fused_broadcast_us"] = round(tb * 1e6, 1)
+    else:
+        from feddct_amd.dist import ShardedAggregator
+        agg = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
+                                N_CLIENTS * world, out32, out64, nchunks=args.chunks)
+        t_step, wall = timed_launches(agg.step, args.steps, args.warmup, sync_group=group)
+        # kernel-only launch time for the roofline (same kernel, SUM_ONLY)
+        t_kernel, _ = timed_launches(reducer, max(10, args.steps // 2), 3)
+        tt = torch.tensor([t_step], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_step = float(tt.item())
+        if rank == 0 and not args.kernel_only:
+            # accuracy of the re-associated cross-GPU sum vs the exact order
+            allc = make_clients(layout, manifest, range(N_CLIENTS * world), dev)
+            ex32 = torch.zeros_like(out32)
+            ex64 = torch.zeros_like(out64)
+            Reducer(layout, allc, ex32, ex64)()
+            torch.cuda.synchronize()
+            extra["parity"] = {"vs": f"exact single-GPU torch order over {N_CLIENTS * world} clients",
+                               "max_ulp_fp32": ulp_dist(out32, ex32),
+                               "int64_bit_exact": bool(torch.equal(out64, ex64))}
+            del allc
+
+    achieved = nbytes_rank / t_kernel / 1e9
+    traffic = pmc_traffic(world)
+    line = {
+        "metric": METRIC,
+        "value": round(nbytes_rank * world / t_step / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t_step * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (portable integer-hash PRNG, feddct_amd/synth.py; seeds 1000+client)",
+        "config": {"workload": f"FedAvg {N_CLIENTS} clients/GPU x wide_resnet16_8 CIFAR-10 "
+                               "(82 fp32 + 16 int64 keys), unweighted mean (reference semantics)",
+                   "clients_per_gpu": N_CLIENTS, "bytes_per_client": layout.state_bytes(),
+                   "algorithmic_bytes_per_step": nbytes_rank * world,
+                   "parallelism": f"client-shard x{world}" if world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_us": round(t_kernel * 1e6, 2)},
+        "cpu_baseline": None,
+    }
+    line.update(extra)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.kernel_only:
+        try:
+            line["cpu_baseline"] = run_cpu_baseline(layout, manifest, clients, args.cpu_budget)
+        except Exception as e:  # report, never hide
+            line["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

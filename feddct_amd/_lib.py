@@ -1,0 +1,165 @@
+"""ctypes binding of libfedagg.so (include/fedagg.h).
+
+The product path has no CPU fallback: if the HIP library is missing or fails
+to load, importing this module raises.  Build it with
+``python -c "import __graft_entry__ as g; g.build()"`` (or feddct_amd.build).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfedagg.so")
+
+FA_OK = 0
+FA_E_INVAL = -1
+FA_E_RANGE = -2
+FA_E_ALIGN = -3
+FA_E_HIP = -4
+FA_E_NOMEM = -5
+FA_MAX_CLIENTS = 4096
+FA_INLINE_CLIENTS = 128
+FA_F_BCAST = 1
+FA_F_SUM_ONLY = 2
+FA_PLAN_GAPS_ARE_PADDING = 1
+
+EXPORTS = [
+    "fa_version", "fa_last_error", "fa_plan_create", "fa_plan_destroy",
+    "fa_plan_get_info", "fa_plan_build_host", "fa_reduce", "fa_mean_f32", "fa_weighted_f32",
+    "fa_mean_i64_trunc", "fa_div_f32", "fa_div_trunc_i64", "fa_broadcast_f32",
+    "fa_synth_fill_f32", "fa_synth_fill_i64", "fa_copy_f32",
+]
+
+
+class FaSeg(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_int64), ("numel", ctypes.c_int64)]
+
+
+class FaPlanInfo(ctypes.Structure):
+    _fields_ = [("f32_numel", ctypes.c_int64), ("i64_numel", ctypes.c_int64),
+                ("ntiles", ctypes.c_int32), ("ntiles_cascade", ctypes.c_int32),
+                ("ntiles_tail", ctypes.c_int32), ("tile_elems", ctypes.c_int32),
+                ("cascade_elems", ctypes.c_int64), ("tail_elems", ctypes.c_int64)]
+
+
+class FaTileDesc(ctypes.Structure):
+    _fields_ = [("start", ctypes.c_int64), ("count", ctypes.c_int32), ("kind", ctypes.c_int32)]
+
+
+class FedaggError(RuntimeError):
+    pass
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I = ctypes.c_int
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"feddct_amd: HIP library {LIB_PATH} not built (run __graft_entry__.build()); "
+            "there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "fa_version": (ctypes.c_char_p, []),
+        "fa_last_error": (ctypes.c_char_p, []),
+        "fa_plan_create": (_I, [_P, _I, _I64, _P, _I, _I64, _I, ctypes.c_uint,
+                                ctypes.POINTER(_P)]),
+        "fa_plan_destroy": (_I, [_P]),
+        "fa_plan_build_host": (_I, [_P, _I, _I64, _P, _I, _I64, _I, ctypes.c_uint, _P, _I,
+                                    ctypes.POINTER(FaPlanInfo)]),
+        "fa_plan_get_info": (_I, [_P, ctypes.POINTER(FaPlanInfo)]),
+        "fa_reduce": (_I, [_P, _P, _P, _I, _P, _P, _P, ctypes.c_uint, _P]),
+        "fa_mean_f32": (_I, [_P, _I, _I64, _P, _P, _I, _P]),
+        "fa_weighted_f32": (_I, [_P, _P, _I, _I64, _P, _P, _I, _P]),
+        "fa_mean_i64_trunc": (_I, [_P, _I, _I64, _P, _P, _I, _P]),
+        "fa_div_f32": (_I, [_P, ctypes.c_float, _P, _I64, _P]),
+        "fa_div_trunc_i64": (_I, [_P, ctypes.c_float, _P, _I64, _P]),
+        "fa_broadcast_f32": (_I, [_P, _P, _I, _I64, _P]),
+        "fa_synth_fill_f32": (_I, [_P, _I64, _I, _I, ctypes.c_float, ctypes.c_float, _I, _P]),
+        "fa_synth_fill_i64": (_I, [_P, _I64, _I, _I, _I, _P]),
+        "fa_copy_f32": (_I, [_P, _P, _I64, _P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)  # AttributeError = missing export: loud
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != FA_OK:
+        msg = lib.fa_last_error().decode(errors="replace")
+        raise FedaggError(f"{what or 'fedagg'} failed ({rc}): {msg}")
+
+
+def version() -> str:
+    return lib.fa_version().decode()
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    arr = (ctypes.c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr
+
+
+def seg_array(segs: np.ndarray):
+    segs = np.ascontiguousarray(np.asarray(segs, np.int64).reshape(-1, 2))
+    arr = (FaSeg * max(1, len(segs)))()
+    for i, (o, n) in enumerate(segs):
+        arr[i].offset = int(o)
+        arr[i].numel = int(n)
+    return arr, len(segs)
+
+
+def build_tiles_host(segs32, f32_numel, segs64=(), i64_numel=0, tile_elems=0,
+                     flags=FA_PLAN_GAPS_ARE_PADDING):
+    """Tile table of a layout, computed by the library on the host (no GPU):
+    returns (info dict, ndarray of (start, count, kind))."""
+    a32, n32 = seg_array(segs32 if len(segs32) else np.zeros((0, 2), np.int64))
+    a64, n64 = seg_array(segs64 if len(segs64) else np.zeros((0, 2), np.int64))
+    info = FaPlanInfo()
+    check(lib.fa_plan_build_host(a32, n32, int(f32_numel), a64, n64, int(i64_numel),
+                                 int(tile_elems), flags, None, 0, ctypes.byref(info)),
+          "fa_plan_build_host")
+    cap = info.ntiles
+    arr = (FaTileDesc * max(1, cap))()
+    check(lib.fa_plan_build_host(a32, n32, int(f32_numel), a64, n64, int(i64_numel),
+                                 int(tile_elems), flags, arr, cap, ctypes.byref(info)),
+          "fa_plan_build_host")
+    tiles = np.array([(arr[i].start, arr[i].count, arr[i].kind) for i in range(cap)],
+                     np.int64).reshape(-1, 3)
+    return {f: getattr(info, f) for f, _ in FaPlanInfo._fields_}, tiles
+
+
+class Plan:
+    """Owning wrapper of an ``fa_plan`` (device-resident tile table)."""
+
+    def __init__(self, segs32, f32_numel, segs64=(), i64_numel=0, tile_elems=0,
+                 flags=FA_PLAN_GAPS_ARE_PADDING):
+        a32, n32 = seg_array(segs32 if len(segs32) else np.zeros((0, 2), np.int64))
+        a64, n64 = seg_array(segs64 if len(segs64) else np.zeros((0, 2), np.int64))
+        h = ctypes.c_void_p()
+        check(lib.fa_plan_create(a32, n32, int(f32_numel), a64, n64, int(i64_numel),
+                                 int(tile_elems), flags, ctypes.byref(h)), "fa_plan_create")
+        self.handle = h
+        info = FaPlanInfo()
+        check(lib.fa_plan_get_info(h, ctypes.byref(info)), "fa_plan_get_info")
+        self.info = {f: getattr(info, f) for f, _ in FaPlanInfo._fields_}
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                lib.fa_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None

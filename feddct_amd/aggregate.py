@@ -1,0 +1,228 @@
+"""Drop-in ``server_aggregate`` on the MI355X engine.
+
+Mirrors the reference's aggregation call surface and side effects:
+
+* ``server_aggregate(global_model, client_models)`` —
+  train_fedavg.py:138-149 (== train_fedprox.py:143-154): for every key of
+  ``global_model.state_dict()`` the mean over ``client_models`` in list (slot)
+  order, ``.float()`` first; loaded into ``global_model``; then every client
+  reloaded from the global state.
+* ``server_aggregate_split(g_a, g_b, models_a, models_b)`` —
+  train_feddct.py:34-56 (== train_splitfed.py:34-56): two independent such
+  reductions (main-client models, proxy models) and two broadcasts.
+
+Results are bit-identical to the reference's CPU torch arithmetic
+(oracle/torch_order.py; tests/test_gpu_parity.py).  Error behaviour follows the
+reference: ``KeyError`` for a key a client lacks, ``RuntimeError`` for a shape
+mismatch or an empty client list, ``RuntimeError`` from the broadcast for a
+client carrying keys the global model lacks (after the global is updated).
+
+Where the work runs: client state is bound once into flat device buckets
+(arena.py) and the whole state_dict — every fp32 key, every int64 key — is
+reduced by ONE launch of the HIP kernel (csrc/fedagg.hip) that also writes the
+broadcast.  Modules living in host memory (the reference's CPU configuration)
+are bound to pinned host buckets and staged through device buckets
+(host-inclusive path).  There is no CPU arithmetic fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .arena import ModuleArena, get_arena, state_owners
+from .layout import BucketLayout
+
+__all__ = ["server_aggregate", "server_aggregate_split", "aggregate_weighted",
+           "Engine", "engine"]
+
+
+def _require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("feddct_amd: no HIP device visible; the aggregation engine has "
+                           "no CPU fallback")
+
+
+class _Staging:
+    """Device buckets for host-resident client state (host-inclusive path)."""
+
+    def __init__(self, layout: BucketLayout, device: torch.device):
+        self.layout = layout
+        self.device = device
+        self.c32: List[torch.Tensor] = []
+        self.c64: List[torch.Tensor] = []
+        self.out32 = torch.empty(max(layout.f32_numel, 64), dtype=torch.float32, device=device)
+        self.out64 = torch.empty(max(layout.i64_numel, 1), dtype=torch.int64, device=device)
+
+    def ensure(self, n: int):
+        while len(self.c32) < n:
+            self.c32.append(torch.empty_like(self.out32))
+            self.c64.append(torch.empty_like(self.out64))
+
+
+class Engine:
+    """Plan/staging caches for one process (one GPU per process)."""
+
+    def __init__(self):
+        self._plans: Dict[tuple, _lib.Plan] = {}
+        self._staging: Dict[tuple, _Staging] = {}
+        self._layouts: Dict[tuple, BucketLayout] = {}
+
+    # ------------------------------------------------------------ caches --
+    def plan(self, layout: BucketLayout, device: torch.device) -> _lib.Plan:
+        key = (layout.signature, device.index)
+        p = self._plans.get(key)
+        if p is None:
+            with torch.cuda.device(device):
+                p = _lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel)
+            self._plans[key] = p
+        return p
+
+    def layout_of(self, module: torch.nn.Module) -> BucketLayout:
+        a = getattr(module, "_fa_arena", None)
+        if a is not None and a.valid() and len(a.extra_keys) == 0:
+            return a.layout
+        lay = BucketLayout.from_state_dict(module.state_dict())
+        # share one layout object per signature so plans/staging are reused
+        return self._layouts.setdefault(lay.signature, lay)
+
+    def staging(self, layout: BucketLayout, device: torch.device, n: int) -> _Staging:
+        key = (layout.signature, device.index)
+        st = self._staging.get(key)
+        if st is None:
+            st = self._staging[key] = _Staging(layout, device)
+        st.ensure(n)
+        return st
+
+    # ------------------------------------------------------------- core --
+    def reduce_modules(self, global_model: torch.nn.Module,
+                       client_models: Sequence[torch.nn.Module],
+                       weights: Optional[Sequence[float]] = None,
+                       broadcast: bool = True) -> None:
+        n = len(client_models)
+        if n == 0:
+            raise RuntimeError("stack expects a non-empty TensorList")
+        _require_gpu()
+        layout = self.layout_of(global_model)
+        ga = get_arena(global_model, layout)
+        cas = [get_arena(c, layout) for c in client_models]
+        dev = ga.device
+        for c in cas:
+            if c.device != dev:
+                raise RuntimeError(
+                    "Expected all tensors to be on the same device, but found at least two "
+                    f"devices, {dev} and {c.device}!")
+        # A client with keys the global lacks makes the reference's broadcast
+        # raise (train_fedavg.py:149): reduce, load the global, broadcast in
+        # order up to that client, then raise the same way.
+        bad = next((i for i, c in enumerate(cas) if c.extra_keys), None)
+        fuse_bcast = broadcast and bad is None
+        for c in cas:
+            c.pack()
+        if dev.type == "cuda":
+            self._reduce_device(layout, ga, cas, weights, fuse_bcast)
+        else:
+            self._reduce_host(layout, ga, cas, weights, fuse_bcast)
+        ga.unpack()
+        if broadcast and not fuse_bcast:
+            for i, c in enumerate(cas):
+                if i == bad:
+                    raise RuntimeError(
+                        f"Error(s) in loading state_dict for {type(client_models[i]).__name__}:"
+                        "\n\tMissing key(s) in state_dict: "
+                        + ", ".join(f'"{k}"' for k in c.extra_keys) + ". ")
+                c.f32.copy_(ga.f32)
+                c.i64.copy_(ga.i64)
+                c.unpack()
+        elif fuse_bcast:
+            for c in cas:
+                c.unpack()
+
+    def _weights_arg(self, weights, n):
+        if weights is None:
+            return None
+        w = np.asarray(weights, np.float32).reshape(-1)
+        if w.shape[0] != n:
+            raise ValueError(f"{w.shape[0]} weights for {n} clients")
+        return (ctypes.c_float * n)(*[float(x) for x in w])
+
+    def _launch(self, plan, layout, c32, c64, n, weights, out32, out64, flags, device):
+        a32 = _lib.ptr_array(c32)
+        a64 = _lib.ptr_array(c64)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        with torch.cuda.device(device):
+            _lib.check(_lib.lib.fa_reduce(plan.handle, a32, a64, n, weights, out32, out64,
+                                          flags, ctypes.c_void_p(stream)), "fa_reduce")
+
+    def _reduce_device(self, layout, ga: ModuleArena, cas: List[ModuleArena], weights, fuse):
+        n = len(cas)
+        plan = self.plan(layout, ga.device)
+        flags = _lib.FA_F_BCAST if fuse else 0
+        self._launch(plan, layout, [c.ptr32 for c in cas], [c.ptr64 for c in cas], n,
+                     self._weights_arg(weights, n), ga.ptr32, ga.ptr64, flags, ga.device)
+
+    def _reduce_host(self, layout, ga: ModuleArena, cas: List[ModuleArena], weights, fuse):
+        """Host-resident state: pinned H2D of every client bucket, one kernel,
+        D2H of the result into the global and (broadcast) every client."""
+        n = len(cas)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        st = self.staging(layout, dev, n)
+        plan = self.plan(layout, dev)
+        for i, c in enumerate(cas):
+            st.c32[i].copy_(c.f32, non_blocking=True)
+            st.c64[i].copy_(c.i64, non_blocking=True)
+        self._launch(plan, layout, [t.data_ptr() for t in st.c32[:n]],
+                     [t.data_ptr() for t in st.c64[:n]], n, self._weights_arg(weights, n),
+                     st.out32.data_ptr(), st.out64.data_ptr(), 0, dev)
+        ga.f32.copy_(st.out32, non_blocking=True)
+        ga.i64.copy_(st.out64, non_blocking=True)
+        if fuse:
+            for c in cas:
+                c.f32.copy_(st.out32, non_blocking=True)
+                c.i64.copy_(st.out64, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+
+
+_ENGINE: Optional[Engine] = None
+
+
+def engine() -> Engine:
+    global _ENGINE
+    if _ENGINE is None:
+        _ENGINE = Engine()
+    return _ENGINE
+
+
+def server_aggregate(global_model, client_models):
+    """train_fedavg.py:138-149 / train_fedprox.py:143-154, on the MI355X engine."""
+    engine().reduce_modules(global_model, list(client_models))
+
+
+def server_aggregate_split(global_model_a, global_model_b, models_a, models_b):
+    """train_feddct.py:34-56 / train_splitfed.py:34-56: main-client and proxy
+    (or client and server) halves reduced and broadcast independently."""
+    e = engine()
+    e.reduce_modules(global_model_a, list(models_a))
+    e.reduce_modules(global_model_b, list(models_b))
+
+
+def aggregate_weighted(global_model, client_models, weights=None, sizes=None,
+                       broadcast=True):
+    """Client-size-weighted FedAvg (SURVEY.md §8 a9 — an extension: the
+    reference is unweighted).  ``weights`` are fp32 w_i, or ``sizes`` n_i give
+    w_i = fp32(n_i / Σn).  fp32 keys: Σ_i fp32(x_i·w_i) in the torch order;
+    int64 keys keep the reference mean.  Equal weights dispatch to the mean
+    path, because x·(1/N) is not bit-equal to x/N."""
+    if weights is None and sizes is None:
+        raise ValueError("give weights or sizes")
+    if weights is None:
+        s = np.asarray(sizes, np.float64)
+        weights = (s / s.sum()).astype(np.float32)
+    w = np.asarray(weights, np.float32)
+    if np.all(w == w[0]):
+        engine().reduce_modules(global_model, list(client_models), None, broadcast)
+    else:
+        engine().reduce_modules(global_model, list(client_models), w, broadcast)

@@ -1,0 +1,138 @@
+"""Persistent flat parameter storage.
+
+``ModuleArena`` re-points every parameter and persistent buffer of an
+``nn.Module`` at a view of one flat fp32 bucket (+ one int64 bucket), laid
+out by a ``BucketLayout``.  After binding, ``module.state_dict()`` returns
+views into the buckets, so the aggregation kernel reads the clients' live
+weights and writes the global (and, fused, the broadcast) in place: no
+per-round packing, no ``state_dict()`` rebuilds (the K·N rebuilds are what
+dominates the reference's time).
+
+Parameter *objects* are kept (only ``.data`` is swapped), so optimizers that
+hold them keep working.  ``valid()`` detects a module whose tensors were
+replaced since binding (``model.to(...)``, new ``nn.Parameter``), in which
+case the shim re-binds.  This is the MI355X-native analogue of the
+reference's (unused) flatten helpers get_flat_params_from /
+set_flat_params_to (fedml_api/distributed/fedgkt/utils.py:17-32).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import torch
+
+from .layout import KIND_F32, KIND_I64, KIND_PACKF, BucketLayout
+
+
+def state_owners(module: torch.nn.Module) -> Dict[str, Tuple[dict, str]]:
+    """state_dict key → (the dict holding the tensor, name), in state_dict
+    registration order (parameters then persistent buffers per module)."""
+    out = {}
+    for prefix, m in module.named_modules(remove_duplicate=False):
+        pre = prefix + "." if prefix else ""
+        for n, p in m._parameters.items():
+            if p is not None:
+                out[pre + n] = (m._parameters, n)
+        for n, b in m._buffers.items():
+            if b is not None and n not in m._non_persistent_buffers_set:
+                out[pre + n] = (m._buffers, n)
+    return out
+
+
+def alloc_buckets(layout: BucketLayout, device: torch.device, pinned: bool = False):
+    kw = dict(device=device)
+    if device.type == "cpu" and pinned and torch.cuda.is_available():
+        kw = dict(pin_memory=True)
+    f32 = torch.zeros(max(layout.f32_numel, 64), dtype=torch.float32, **kw)
+    i64 = torch.zeros(max(layout.i64_numel, 1), dtype=torch.int64, **kw)
+    return f32, i64
+
+
+class ModuleArena:
+    """A module whose state lives in flat buckets laid out by ``layout``."""
+
+    def __init__(self, module: torch.nn.Module, layout: BucketLayout,
+                 pinned: bool = True):
+        owners = state_owners(module)
+        tensors = {k: owners[k][0][owners[k][1]] for k in owners}
+        missing = [k for k in layout.keys if k not in tensors]
+        if missing:
+            raise KeyError(missing[0])
+        devs = {t.device for t in tensors.values()}
+        if len(devs) != 1:
+            raise RuntimeError(f"module state spans several devices: {sorted(map(str, devs))}")
+        self.device = devs.pop()
+        self.layout = layout
+        for s in layout.slots:
+            t = tensors[s.key]
+            if tuple(t.shape) != s.shape:
+                # what torch.stack raises on the reference path (train_fedavg.py:145)
+                raise RuntimeError(
+                    f"stack expects each tensor to be equal size, but got {list(s.shape)} "
+                    f"(global) and {list(t.shape)} for key {s.key!r}")
+            if t.dtype != s.dtype:
+                raise TypeError(
+                    f"state_dict key {s.key!r}: module dtype {t.dtype} differs from the "
+                    f"global model's {s.dtype} (mixed-dtype client slots are not supported)")
+        # keys the module has beyond the layout: the reference's broadcast
+        # load_state_dict(strict=True) rejects such a client (train_fedavg.py:149)
+        self.extra_keys = [k for k in tensors if k not in layout.by_key]
+        self.f32, self.i64 = alloc_buckets(layout, self.device, pinned)
+        self._checks: List[tuple] = []
+        self._packed: List[tuple] = []
+        with torch.no_grad():
+            for s in layout.slots:
+                d, name = owners[s.key]
+                t = d[name]
+                if s.kind == KIND_PACKF:
+                    self._packed.append((d, name, t, s))
+                    continue
+                bucket = self.i64 if s.kind == KIND_I64 else self.f32
+                view = bucket[s.offset:s.offset + s.numel].view(s.shape)
+                if s.alias_of is None:
+                    view.copy_(t)
+                t.data = view
+                self._checks.append((d, name, t, view.data_ptr()))
+        self.module_ref = module
+
+    def valid(self) -> bool:
+        for d, name, t, ptr in self._checks:
+            if d.get(name) is not t or t.data_ptr() != ptr:
+                return False
+        for d, name, t, _ in self._packed:
+            if d.get(name) is not t:
+                return False
+        return True
+
+    # -- keys stored in another dtype: staged through the f32 bucket -------
+    def pack(self) -> None:
+        """``.float()`` every non-fp32/int64 key into its f32 slot."""
+        for _, _, t, s in self._packed:
+            self.f32[s.offset:s.offset + s.numel].view(s.shape).copy_(t)
+
+    def unpack(self) -> None:
+        """``copy_`` the f32 slot back into the key's own dtype (the
+        load_state_dict semantics of train_fedavg.py:147)."""
+        with torch.no_grad():
+            for _, _, t, s in self._packed:
+                t.copy_(self.f32[s.offset:s.offset + s.numel].view(s.shape))
+
+    @property
+    def ptr32(self) -> int:
+        return self.f32.data_ptr()
+
+    @property
+    def ptr64(self) -> int:
+        return self.i64.data_ptr()
+
+
+def get_arena(module: torch.nn.Module, layout: BucketLayout) -> ModuleArena:
+    """The module's arena for ``layout``, binding (or re-binding) if needed."""
+    a = getattr(module, "_fa_arena", None)
+    if a is not None and a.layout is layout and a.valid():
+        return a
+    if a is not None and a.layout == layout and a.valid():
+        return a
+    a = ModuleArena(module, layout)
+    object.__setattr__(module, "_fa_arena", a)
+    return a

@@ -1,0 +1,865 @@
+// fedagg.hip — MI355X (gfx950) kernels + C ABI for server-side parameter
+// aggregation (the reference's server_aggregate, train_fedavg.py:138-149,
+// train_fedprox.py:143-154, train_feddct.py:34-56, train_splitfed.py:34-56).
+//
+// The work is a bandwidth-bound column reduction: for every element of the
+// flat per-client bucket, sum the N client values in exactly the order torch's
+// CPU SumKernel uses (cascade / ILP-4 / 8-lane inner, see include/fedagg.h and
+// DESIGN.md §2), then divide by N.  Each thread owns its columns and walks the
+// clients serially, so the order costs nothing: there is no cross-lane or LDS
+// reduction over clients (that would re-associate the sum).  The bucket is cut
+// on the host into a tile table; one 256-thread workgroup streams one tile:
+// per client, one coalesced 16-B load per lane per vector (1 KiB per wave
+// instruction), loads for a batch of clients issued before their adds.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared
+// (no fast-math, no FTZ: the sum must be IEEE round-to-nearest-even, no FMA).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fedagg.h"
+
+#define FA_VERSION_STR "fedagg 0.1.0 gfx950"
+
+namespace {
+
+// ---------------------------------------------------------------- errors --
+thread_local std::string g_last_error;
+
+int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t e_ = (expr);                                                  \
+    if (e_ != hipSuccess)                                                    \
+      return set_err(FA_E_HIP, "%s: %s", #expr, hipGetErrorString(e_));     \
+  } while (0)
+
+// ----------------------------------------------------------------- tiles --
+enum TileKind : int32_t {
+  K_F32_VEC = 0,      // cascade order, 16-B vectors, count % 4 == 0
+  K_F32_CASC_S = 1,   // cascade order, one element per thread (unaligned)
+  K_F32_ILP4 = 2,     // tail columns: ILP-4 order
+  K_F32_INNER = 3,    // M == 1: ILP-4 (n < 8) or 8-lane inner (n >= 8)
+  K_I64_CASC = 4,
+  K_I64_ILP4 = 5,
+  K_I64_INNER = 6,
+};
+
+struct Tile {
+  int64_t start;  // first element (bucket index)
+  int32_t count;  // elements
+  int32_t kind;
+};
+static_assert(sizeof(Tile) == 16, "tile is 16 B");
+
+constexpr int kBlock = 256;
+constexpr int kDefaultU = 2;  // float4 vectors per thread per client
+
+constexpr int kInline = FA_INLINE_CLIENTS;
+
+// Client pointer tables travel inline in the kernel arguments for
+// n <= kInline (the common case: no setup copy at all); beyond that they sit
+// in a stream-ordered device allocation (tab32/tab64/tabw).
+struct ReduceArgs {
+  const Tile* tiles;
+  float* out32;
+  int64_t* out64;
+  int n;
+  unsigned flags;
+  const float* const* tab32;
+  const int64_t* const* tab64;
+  const float* tabw;
+  const float* c32[kInline];
+  const int64_t* c64[kInline];
+  float w[kInline];
+};
+
+__device__ __forceinline__ const float* cptr32(const ReduceArgs& a, int i) {
+  return a.n <= kInline ? a.c32[i] : a.tab32[i];
+}
+__device__ __forceinline__ const int64_t* cptr64(const ReduceArgs& a, int i) {
+  return a.n <= kInline ? a.c64[i] : a.tab64[i];
+}
+__device__ __forceinline__ float cw(const ReduceArgs& a, int i) {
+  return a.n <= kInline ? a.w[i] : a.tabw[i];
+}
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// c10::utils::CeilLog2 / ATen multi_row_sum level power
+__host__ __device__ inline int ceil_log2_i(int64_t n) {
+  if (n <= 1) return 0;
+  int r = 0;
+  uint64_t v = (uint64_t)(n - 1);
+  while (v) { ++r; v >>= 1; }
+  return r;
+}
+__host__ __device__ inline int level_power(int64_t n) {
+  int c = ceil_log2_i(n) / 4;
+  return c > 4 ? c : 4;
+}
+
+__device__ __forceinline__ f4 add4(f4 a, f4 b) {
+  return f4{__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y), __fadd_rn(a.z, b.z),
+            __fadd_rn(a.w, b.w)};
+}
+__device__ __forceinline__ f4 mul4s(f4 a, float s) {
+  return f4{__fmul_rn(a.x, s), __fmul_rn(a.y, s), __fmul_rn(a.z, s),
+            __fmul_rn(a.w, s)};
+}
+__device__ __forceinline__ f4 div4s(f4 a, float s) {
+  return f4{__fdiv_rn(a.x, s), __fdiv_rn(a.y, s), __fdiv_rn(a.z, s),
+            __fdiv_rn(a.w, s)};
+}
+
+template <bool NT>
+__device__ __forceinline__ f4 ld4(const float* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+  else return *reinterpret_cast<const f4*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, f4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
+  else *reinterpret_cast<f4*>(p) = v;
+}
+
+// -------------------------------------------------- vectorised cascade ----
+// ATen multi_row_sum over the n clients for 4*U columns per thread.  The
+// loop over clients is uniform (scalar control).  Clients go in batches of B:
+// the batch's B pointers come in as one scalar load, all B*U 16-B loads are
+// issued, then the adds run in client order with the block promotion after
+// every full block of 2^lp rows (lp = 4 for n < 2^20).
+template <int U, bool DEEP>
+struct Acc {
+  f4 l0[U], l1[U], l2[U], l3[U];
+};
+
+template <int U, bool DEEP>
+__device__ __forceinline__ void promote(Acc<U, DEEP>& A, int ii, int lp, int mask) {
+  if ((ii & mask) != 0) return;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    A.l1[u] = add4(A.l1[u], A.l0[u]);
+    A.l0[u] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  if constexpr (DEEP) {
+    if ((ii & (mask << lp)) != 0) return;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      A.l2[u] = add4(A.l2[u], A.l1[u]);
+      A.l1[u] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    if ((ii & (mask << (2 * lp))) != 0) return;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      A.l3[u] = add4(A.l3[u], A.l2[u]);
+      A.l2[u] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// One batch of NB clients starting at b0.  FULL: every lane's U vectors are
+// inside the tile (no per-lane predicate).
+template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, bool NT>
+__device__ __forceinline__ void batch(const ReduceArgs& a, Acc<U, DEEP>& A, int b0,
+                                      const int64_t (&off)[U], const bool (&ok)[U],
+                                      int lp, int mask) {
+  f4 x[NB][U];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const float* p = cptr32(a, b0 + b);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (FULL) x[b][u] = ld4<NT>(p + off[u]);
+      else x[b][u] = ok[u] ? ld4<NT>(p + off[u]) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f4 v = x[b][u];
+      if constexpr (WEIGHTED) v = mul4s(v, cw(a, b0 + b));
+      A.l0[u] = add4(A.l0[u], v);
+    }
+    promote<U, DEEP>(A, b0 + b + 1, lp, mask);
+  }
+}
+
+template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, bool NT>
+__device__ __forceinline__ void tile_vec(const ReduceArgs& a, int64_t start,
+                                         int count) {
+  const int n = a.n;
+  const int lp = level_power(n);
+  const int mask = (1 << lp) - 1;
+  Acc<U, DEEP> A;
+  int64_t off[U];
+  bool ok[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int v = threadIdx.x + u * kBlock;
+    off[u] = start + 4 * (int64_t)v;
+    ok[u] = FULL || 4 * v < count;
+    A.l0[u] = A.l1[u] = A.l2[u] = A.l3[u] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  int b0 = 0;
+  for (; b0 + B <= n; b0 += B)
+    batch<U, B, FULL, DEEP, WEIGHTED, NT>(a, A, b0, off, ok, lp, mask);
+  for (; b0 < n; ++b0)
+    batch<U, 1, FULL, DEEP, WEIGHTED, NT>(a, A, b0, off, ok, lp, mask);
+
+  const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
+  const float fn = (float)n;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!ok[u]) continue;
+    // acc2/acc3 stay +0 unless DEEP; x + (+0) == x for every x a +0-seeded
+    // round-to-nearest sum can produce (never -0), so skipping them is exact.
+    f4 s = add4(A.l0[u], A.l1[u]);
+    if constexpr (DEEP) {
+      s = add4(s, A.l2[u]);
+      s = add4(s, A.l3[u]);
+    }
+    const f4 r = sum_only ? s : div4s(s, fn);
+    st4<NT>(a.out32 + off[u], r);
+    if (a.flags & FA_F_BCAST) {
+      for (int i = 0; i < n; ++i) st4<NT>(const_cast<float*>(cptr32(a, i)) + off[u], r);
+    }
+  }
+}
+
+// ------------------------------------------------------- scalar orders ----
+struct SrcF32 {
+  const ReduceArgs& a;
+  bool weighted;
+  __device__ float operator()(int i, int64_t e) const {
+    float x = cptr32(a, i)[e];
+    return weighted ? __fmul_rn(x, cw(a, i)) : x;
+  }
+};
+struct SrcI64 {
+  const ReduceArgs& a;
+  __device__ float operator()(int i, int64_t e) const {
+    return (float)cptr64(a, i)[e];  // .float(): int64 -> fp32, round to nearest
+  }
+};
+
+// multi_row_sum over rows first, first+stride, ... (count rows), 1 column.
+template <class Src>
+__device__ float cascade_seq(const Src& src, int64_t e, int first, int stride,
+                             int count) {
+  const int lp = level_power(count);
+  const int step = 1 << lp, mask = step - 1;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int i = 0;
+  for (; i + step <= count;) {
+    for (int j = 0; j < step; ++j, ++i) acc[0] = __fadd_rn(acc[0], src(first + i * stride, e));
+    for (int j = 1; j < 4; ++j) {
+      acc[j] = __fadd_rn(acc[j], acc[j - 1]);
+      acc[j - 1] = 0.f;
+      if (i & (mask << (j * lp))) break;
+    }
+  }
+  for (; i < count; ++i) acc[0] = __fadd_rn(acc[0], src(first + i * stride, e));
+  for (int j = 1; j < 4; ++j) acc[0] = __fadd_rn(acc[0], acc[j]);
+  return acc[0];
+}
+
+// ATen row_sum: ILP-4 over rows first + k*stride (count rows).
+template <class Src>
+__device__ float ilp4_seq(const Src& src, int64_t e, int first, int stride,
+                          int count) {
+  const int q = count / 4;
+  float p[4];
+  for (int k = 0; k < 4; ++k) p[k] = cascade_seq(src, e, first + k * stride, 4 * stride, q);
+  for (int i = 4 * q; i < count; ++i) p[0] = __fadd_rn(p[0], src(first + i * stride, e));
+  for (int k = 1; k < 4; ++k) p[0] = __fadd_rn(p[0], p[k]);
+  return p[0];
+}
+
+// ATen vectorized_inner_sum (M == 1, n >= 8): 8 lanes, each an ILP-4 over
+// the n/8 vectors; scalar tail into a fresh +0; then lanes 0..7 in order.
+template <class Src>
+__device__ float inner_seq(const Src& src, int64_t e, int n) {
+  if (n < 8) return ilp4_seq(src, e, 0, 1, n);
+  const int nv = n / 8;
+  float fin = 0.f;
+  for (int k = 8 * nv; k < n; ++k) fin = __fadd_rn(fin, src(k, e));
+  for (int l = 0; l < 8; ++l) fin = __fadd_rn(fin, ilp4_seq(src, e, l, 8, nv));
+  return fin;
+}
+
+template <bool WEIGHTED>
+__device__ void tile_scalar(const ReduceArgs& a, const Tile& t) {
+  const int j = threadIdx.x;
+  if (j >= t.count) return;
+  const int64_t e = t.start + j;
+  const int n = a.n;
+  const float fn = (float)n;
+  if (t.kind <= K_F32_INNER) {
+    SrcF32 src{a, WEIGHTED};
+    float s;
+    if (t.kind == K_F32_CASC_S) s = cascade_seq(src, e, 0, 1, n);
+    else if (t.kind == K_F32_ILP4) s = ilp4_seq(src, e, 0, 1, n);
+    else s = inner_seq(src, e, n);
+    s = __fadd_rn(0.f, s);  // sum_out: out (=+0) += value
+    const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
+    const float r = sum_only ? s : __fdiv_rn(s, fn);
+    a.out32[e] = r;
+    if (a.flags & FA_F_BCAST)
+      for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
+  } else {
+    SrcI64 src{a};
+    float s;
+    if (t.kind == K_I64_CASC) s = cascade_seq(src, e, 0, 1, n);
+    else if (t.kind == K_I64_ILP4) s = ilp4_seq(src, e, 0, 1, n);
+    else s = inner_seq(src, e, n);
+    s = __fadd_rn(0.f, s);
+    // load_state_dict copy_: fp32 -> int64 truncates toward zero
+    const int64_t r = (int64_t)__fdiv_rn(s, fn);
+    a.out64[e] = r;
+    if (a.flags & FA_F_BCAST)
+      for (int i = 0; i < n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
+  }
+}
+
+template <int U, int B, bool DEEP, bool WEIGHTED, bool NT>
+__global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs a) {
+  const Tile t = a.tiles[blockIdx.x];
+  if (t.kind == K_F32_VEC) {
+    if (t.count == 4 * U * kBlock) tile_vec<U, B, true, DEEP, WEIGHTED, NT>(a, t.start, t.count);
+    else tile_vec<U, B, false, DEEP, WEIGHTED, NT>(a, t.start, t.count);
+  } else {
+    tile_scalar<WEIGHTED>(a, t);
+  }
+}
+
+// ------------------------------------------------------ small kernels ----
+__global__ void div_f32_kernel(const float* __restrict__ x, float d, float* __restrict__ out,
+                               int64_t numel) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < numel;
+       j += (int64_t)gridDim.x * blockDim.x)
+    out[j] = __fdiv_rn(x[j], d);
+}
+__global__ void div_trunc_i64_kernel(const float* __restrict__ x, float d,
+                                     int64_t* __restrict__ out, int64_t numel) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < numel;
+       j += (int64_t)gridDim.x * blockDim.x)
+    out[j] = (int64_t)__fdiv_rn(x[j], d);
+}
+
+struct BcastArgs {
+  const float* src;
+  int n;
+  float* dst[FA_MAX_CLIENTS];
+};
+__global__ __launch_bounds__(kBlock) void bcast_kernel(BcastArgs a,
+                                                       int64_t numel) {
+  const int64_t nv = numel / 4;
+  for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nv;
+       v += (int64_t)gridDim.x * kBlock) {
+    const f4 x = ld4<true>(a.src + 4 * v);
+    for (int i = 0; i < a.n; ++i) st4<true>(a.dst[i] + 4 * v, x);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < numel - 4 * nv)
+    for (int i = 0; i < a.n; ++i) a.dst[i][4 * nv + threadIdx.x] = a.src[4 * nv + threadIdx.x];
+}
+
+__global__ __launch_bounds__(kBlock) void copy_kernel(const float* __restrict__ src,
+                                                      float* __restrict__ dst, int64_t numel) {
+  const int64_t nv = numel / 4;
+  for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nv;
+       v += (int64_t)gridDim.x * kBlock)
+    st4<true>(dst + 4 * v, ld4<true>(src + 4 * v));
+  if (blockIdx.x == 0 && threadIdx.x < numel - 4 * nv)
+    dst[4 * nv + threadIdx.x] = src[4 * nv + threadIdx.x];
+}
+
+// ------------------------------------------- synthetic state (synth.py) --
+__device__ __forceinline__ uint64_t hash64(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx * 0xD1B54A32D192ED03ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float sym_unit(uint64_t h) {
+  const int64_t v = (int64_t)(h >> 40) - (1 << 23);
+  return __fmul_rn((float)v, 1.0f / 8388608.0f);
+}
+constexpr uint64_t kBaseSeed = 7, kClientSeed0 = 1000;
+constexpr int kKeyShift = 36;
+
+__global__ void synth_f32_kernel(float* dst, int64_t numel, int key, int client,
+                                 float mu, float sigma, float dsig, int mode) {
+  const uint64_t kb = (uint64_t)key << kKeyShift;
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < numel;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t idx = kb | (uint64_t)j;
+    const uint64_t hc = hash64(kClientSeed0 + client, idx);
+    float x;
+    if (mode == 1) {
+      const int ex = (int)((hc >> 8) % 41ull) - 20;
+      x = __fmul_rn(sym_unit(hc), ldexpf(1.0f, ex));
+    } else {
+      const float base = __fadd_rn(mu, __fmul_rn(sigma, sym_unit(hash64(kBaseSeed, idx))));
+      x = __fadd_rn(base, __fmul_rn(dsig, sym_unit(hc)));
+    }
+    dst[j] = x;
+  }
+}
+__global__ void synth_i64_kernel(int64_t* dst, int64_t numel, int key, int client, int mode) {
+  const uint64_t kb = (uint64_t)key << kKeyShift;
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < numel;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t hc = hash64(kClientSeed0 + client, kb | (uint64_t)j);
+    dst[j] = mode == 1 ? (int64_t)(hc % (1ull << 26)) - (1ll << 25)
+                       : (int64_t)(19 * 5) + (int64_t)(hc % 7ull);
+  }
+}
+
+// ------------------------------------------------------------ host plan --
+int grid_for(int64_t work, int per_block) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > 256 * 16) g = 256 * 16;
+  return (int)g;
+}
+
+}  // namespace
+
+struct fa_plan {
+  int device = 0;
+  Tile* d_tiles = nullptr;
+  fa_plan_info info{};
+  int vec_u = kDefaultU;
+};
+
+namespace {
+
+inline int64_t body_len(int64_t M) {
+  if (M >= 8) return (M / 32) * 32;
+  if (M >= 2) return (M / 4) * 4;
+  return 0;
+}
+
+int check_segs(const fa_seg* s, int ns, int64_t numel, const char* what,
+               std::vector<fa_seg>* sorted) {
+  if (ns < 0 || (ns > 0 && !s)) return set_err(FA_E_INVAL, "%s: bad segment array", what);
+  sorted->assign(s, s + ns);
+  std::stable_sort(sorted->begin(), sorted->end(),
+                   [](const fa_seg& x, const fa_seg& y) { return x.offset < y.offset; });
+  int64_t end = 0;
+  for (const fa_seg& g : *sorted) {
+    if (g.offset < 0 || g.numel < 0 || g.offset + g.numel > numel)
+      return set_err(FA_E_INVAL, "%s: segment [%lld,+%lld) outside bucket of %lld", what,
+                     (long long)g.offset, (long long)g.numel, (long long)numel);
+    if (g.numel > 0 && g.offset < end)
+      return set_err(FA_E_INVAL, "%s: overlapping segments at %lld", what, (long long)g.offset);
+    if (g.numel > 0) end = g.offset + g.numel;
+  }
+  return FA_OK;
+}
+
+void push_scalar(std::vector<Tile>* t, int64_t start, int64_t count, int kind) {
+  for (int64_t c = 0; c < count; c += kBlock)
+    t->push_back(Tile{start + c, (int32_t)std::min<int64_t>(kBlock, count - c), kind});
+}
+
+int build_tiles(const std::vector<fa_seg>& s32, const std::vector<fa_seg>& s64, int tile_elems,
+                unsigned flags, std::vector<Tile>* out, fa_plan_info* info) {
+  std::vector<Tile> vec, tail;
+  // Maximal runs of cascade-order elements, 4-aligned (vectorisable).
+  int64_t run_s = -1, run_e = -1;
+  auto flush = [&]() {
+    if (run_s < 0) return;
+    for (int64_t c = run_s; c < run_e; c += tile_elems)
+      vec.push_back(Tile{c, (int32_t)std::min<int64_t>(tile_elems, run_e - c), K_F32_VEC});
+    info->cascade_elems += run_e - run_s;
+    run_s = run_e = -1;
+  };
+  for (const fa_seg& g : s32) {
+    const int64_t M = g.numel;
+    if (M == 0) continue;
+    if (M == 1) {
+      push_scalar(&tail, g.offset, 1, K_F32_INNER);
+      info->tail_elems += 1;
+      continue;
+    }
+    const int64_t b = body_len(M);
+    if (b > 0) {
+      if (g.offset % 4 == 0) {
+        const bool extend = run_s >= 0 && (run_e == g.offset ||
+                                           ((flags & FA_PLAN_GAPS_ARE_PADDING) && run_e <= g.offset));
+        if (!extend) flush();
+        if (run_s < 0) run_s = g.offset;
+        run_e = g.offset + b;
+      } else {
+        flush();
+        push_scalar(&tail, g.offset, b, K_F32_CASC_S);
+        info->tail_elems += b;
+      }
+    }
+    if (b < M) {
+      flush();  // the tail breaks the run
+      push_scalar(&tail, g.offset + b, M - b, K_F32_ILP4);
+      info->tail_elems += M - b;
+    }
+  }
+  flush();
+  for (const fa_seg& g : s64) {
+    const int64_t M = g.numel;
+    if (M == 0) continue;
+    if (M == 1) { push_scalar(&tail, g.offset, 1, K_I64_INNER); continue; }
+    const int64_t b = body_len(M);
+    if (b) push_scalar(&tail, g.offset, b, K_I64_CASC);
+    if (b < M) push_scalar(&tail, g.offset + b, M - b, K_I64_ILP4);
+  }
+  // Scalar tiles first: their few long-latency workgroups start early and
+  // finish under the vector stream instead of trailing it.
+  out->clear();
+  out->insert(out->end(), tail.begin(), tail.end());
+  out->insert(out->end(), vec.begin(), vec.end());
+  info->ntiles = (int32_t)out->size();
+  info->ntiles_cascade = (int32_t)vec.size();
+  info->ntiles_tail = (int32_t)tail.size();
+  return FA_OK;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+template <int U, int B, bool DEEP, bool W, bool NT>
+hipError_t launch_one(const ReduceArgs& a, int ntiles, hipStream_t st) {
+  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, NT>), dim3(ntiles), dim3(kBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
+template <int U, int B>
+hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, bool nt, hipStream_t st) {
+  if (deep) return w ? launch_one<U, B, true, true, true>(a, ntiles, st)
+                     : launch_one<U, B, true, false, true>(a, ntiles, st);
+  if (w) return nt ? launch_one<U, B, false, true, true>(a, ntiles, st)
+                   : launch_one<U, B, false, true, false>(a, ntiles, st);
+  return nt ? launch_one<U, B, false, false, true>(a, ntiles, st)
+            : launch_one<U, B, false, false, false>(a, ntiles, st);
+}
+
+hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, hipStream_t st) {
+  const bool deep = a.n >= 256;
+  const bool w = a.flags & 0x100u;  // internal: weighted
+  static const int nt_env = env_int("FEDAGG_NT", 1);
+  static const int b_env = env_int("FEDAGG_BATCH", 8);
+  const bool nt = nt_env != 0;
+  switch (vec_u) {
+    case 1: return b_env == 16 ? launch_u<1, 16>(a, ntiles, deep, w, nt, st)
+                               : launch_u<1, 8>(a, ntiles, deep, w, nt, st);
+    case 4: return launch_u<4, 8>(a, ntiles, deep, w, nt, st);
+    default: return b_env == 16 ? launch_u<2, 16>(a, ntiles, deep, w, nt, st)
+                                : launch_u<2, 8>(a, ntiles, deep, w, nt, st);
+  }
+}
+
+// Stateless-API plan cache, keyed by device + layout.
+std::mutex g_cache_mu;
+std::map<std::string, fa_plan*> g_cache;
+
+int cached_plan(const fa_seg* s32, int n32, int64_t numel32, const fa_seg* s64, int n64,
+                int64_t numel64, fa_plan** out) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  std::string key((const char*)&dev, sizeof dev);
+  key.append((const char*)&numel32, sizeof numel32);
+  key.append((const char*)&numel64, sizeof numel64);
+  key.append((const char*)&n32, sizeof n32);
+  if (n32 > 0) key.append((const char*)s32, sizeof(fa_seg) * n32);
+  if (n64 > 0) key.append((const char*)s64, sizeof(fa_seg) * n64);
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  auto it = g_cache.find(key);
+  if (it != g_cache.end()) { *out = it->second; return FA_OK; }
+  fa_plan* p = nullptr;
+  int rc = fa_plan_create(s32, n32, numel32, s64, n64, numel64, 0, 0, &p);
+  if (rc) return rc;
+  g_cache[key] = p;
+  *out = p;
+  return FA_OK;
+}
+
+}  // namespace
+
+// =================================================================== ABI ==
+extern "C" {
+
+const char* fa_version(void) { return FA_VERSION_STR; }
+const char* fa_last_error(void) { return g_last_error.c_str(); }
+
+int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_seg* seg64,
+                   int nseg64, int64_t i64_numel, int tile_elems, unsigned flags,
+                   fa_plan** out) {
+  if (!out) return set_err(FA_E_INVAL, "fa_plan_create: out is NULL");
+  *out = nullptr;
+  if (f32_numel < 0 || i64_numel < 0) return set_err(FA_E_INVAL, "negative bucket size");
+  if (tile_elems == 0) tile_elems = 4 * kBlock * env_int("FEDAGG_U", kDefaultU);
+  if (tile_elems != 4 * kBlock && tile_elems != 8 * kBlock && tile_elems != 16 * kBlock)
+    return set_err(FA_E_INVAL, "tile_elems must be 1024, 2048 or 4096 (got %d)", tile_elems);
+  std::vector<fa_seg> s32, s64;
+  int rc = check_segs(seg32, nseg32, f32_numel, "fp32", &s32);
+  if (rc) return rc;
+  rc = check_segs(seg64, nseg64, i64_numel, "int64", &s64);
+  if (rc) return rc;
+  fa_plan* p = new fa_plan();
+  p->info.f32_numel = f32_numel;
+  p->info.i64_numel = i64_numel;
+  p->info.tile_elems = tile_elems;
+  p->vec_u = tile_elems / (4 * kBlock);
+  std::vector<Tile> tiles;
+  build_tiles(s32, s64, tile_elems, flags, &tiles, &p->info);
+  hipError_t e = hipGetDevice(&p->device);
+  if (e == hipSuccess && !tiles.empty()) {
+    e = hipMalloc(&p->d_tiles, tiles.size() * sizeof(Tile));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_tiles, tiles.data(), tiles.size() * sizeof(Tile), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    if (p->d_tiles) (void)hipFree(p->d_tiles);
+    delete p;
+    return set_err(FA_E_HIP, "fa_plan_create: %s", hipGetErrorString(e));
+  }
+  *out = p;
+  return FA_OK;
+}
+
+int fa_plan_build_host(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_seg* seg64,
+                       int nseg64, int64_t i64_numel, int tile_elems, unsigned flags,
+                       fa_tile_desc* tiles, int cap, fa_plan_info* info) {
+  if (!info) return set_err(FA_E_INVAL, "fa_plan_build_host: info is NULL");
+  if (tile_elems == 0) tile_elems = 4 * kBlock * kDefaultU;
+  if (tile_elems != 4 * kBlock && tile_elems != 8 * kBlock && tile_elems != 16 * kBlock)
+    return set_err(FA_E_INVAL, "tile_elems must be 1024, 2048 or 4096 (got %d)", tile_elems);
+  std::vector<fa_seg> s32, s64;
+  int rc = check_segs(seg32, nseg32, f32_numel, "fp32", &s32);
+  if (rc) return rc;
+  rc = check_segs(seg64, nseg64, i64_numel, "int64", &s64);
+  if (rc) return rc;
+  fa_plan_info in{};
+  in.f32_numel = f32_numel;
+  in.i64_numel = i64_numel;
+  in.tile_elems = tile_elems;
+  std::vector<Tile> t;
+  build_tiles(s32, s64, tile_elems, flags, &t, &in);
+  *info = in;
+  if (tiles) {
+    if (cap < (int)t.size())
+      return set_err(FA_E_RANGE, "fa_plan_build_host: %d tiles, capacity %d", (int)t.size(), cap);
+    for (size_t i = 0; i < t.size(); ++i) tiles[i] = fa_tile_desc{t[i].start, t[i].count, t[i].kind};
+  }
+  return FA_OK;
+}
+
+int fa_plan_destroy(fa_plan* plan) {
+  if (!plan) return FA_OK;
+  if (plan->d_tiles) HIP_TRY(hipFree(plan->d_tiles));
+  delete plan;
+  return FA_OK;
+}
+
+int fa_plan_get_info(const fa_plan* plan, fa_plan_info* info) {
+  if (!plan || !info) return set_err(FA_E_INVAL, "fa_plan_get_info: NULL argument");
+  *info = plan->info;
+  return FA_OK;
+}
+
+int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const* c64, int n,
+              const float* weights, float* out32, int64_t* out64, unsigned flags,
+              void* stream) {
+  if (!plan) return set_err(FA_E_INVAL, "fa_reduce: plan is NULL");
+  if (n < 1) return set_err(FA_E_INVAL, "fa_reduce: need at least one client (n=%d)", n);
+  if (n > FA_MAX_CLIENTS)
+    return set_err(FA_E_RANGE, "fa_reduce: n=%d exceeds FA_MAX_CLIENTS=%d", n, FA_MAX_CLIENTS);
+  if (flags & ~(FA_F_BCAST | FA_F_SUM_ONLY)) return set_err(FA_E_INVAL, "fa_reduce: bad flags");
+  const fa_plan_info& in = plan->info;
+  if (plan->info.ntiles == 0) return FA_OK;
+  ReduceArgs a;
+  memset(&a, 0, sizeof a);
+  a.tiles = plan->d_tiles;
+  a.out32 = out32;
+  a.out64 = out64;
+  a.n = n;
+  a.flags = flags | (weights ? 0x100u : 0u);
+  const bool need32 = in.f32_numel > 0, need64 = in.i64_numel > 0;
+  if (need32) {
+    if (!c32 || !out32) return set_err(FA_E_INVAL, "fa_reduce: fp32 buckets required");
+    if (!aligned16(out32)) return set_err(FA_E_ALIGN, "fa_reduce: out32 not 16-B aligned");
+    for (int i = 0; i < n; ++i) {
+      if (!c32[i]) return set_err(FA_E_INVAL, "fa_reduce: client %d fp32 bucket NULL", i);
+      if (!aligned16(c32[i]))
+        return set_err(FA_E_ALIGN, "fa_reduce: client %d fp32 bucket not 16-B aligned", i);
+    }
+  }
+  if (need64) {
+    if (!c64 || !out64) return set_err(FA_E_INVAL, "fa_reduce: int64 buckets required");
+    for (int i = 0; i < n; ++i)
+      if (!c64[i]) return set_err(FA_E_INVAL, "fa_reduce: client %d int64 bucket NULL", i);
+  }
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev != plan->device)
+    return set_err(FA_E_INVAL, "fa_reduce: plan built on device %d, current device %d",
+                   plan->device, dev);
+  hipStream_t st = (hipStream_t)stream;
+  void* table = nullptr;
+  if (n <= kInline) {
+    for (int i = 0; i < n; ++i) {
+      if (need32) a.c32[i] = c32[i];
+      if (need64) a.c64[i] = c64[i];
+      if (weights) a.w[i] = weights[i];
+    }
+  } else {
+    // [n fp32 ptrs][n int64 ptrs][n weights], stream-ordered alloc + copy
+    std::vector<char> host((size_t)n * 20);
+    const void** h32 = (const void**)host.data();
+    const void** h64 = h32 + n;
+    float* hw = (float*)(h64 + n);
+    for (int i = 0; i < n; ++i) {
+      h32[i] = need32 ? (const void*)c32[i] : nullptr;
+      h64[i] = need64 ? (const void*)c64[i] : nullptr;
+      hw[i] = weights ? weights[i] : 0.f;
+    }
+    HIP_TRY(hipMallocAsync(&table, host.size(), st));
+    HIP_TRY(hipMemcpyAsync(table, host.data(), host.size(), hipMemcpyHostToDevice, st));
+    a.tab32 = (const float* const*)table;
+    a.tab64 = (const int64_t* const*)((const void**)table + n);
+    a.tabw = (const float*)((const void**)table + 2 * n);
+  }
+  hipError_t e = launch_reduce(a, in.ntiles, plan->vec_u, st);
+  if (table) {
+    hipError_t e2 = hipFreeAsync(table, st);
+    if (e == hipSuccess) e = e2;
+  }
+  if (e != hipSuccess) return set_err(FA_E_HIP, "reduce launch: %s", hipGetErrorString(e));
+  return FA_OK;
+}
+
+int fa_mean_f32(const float* const* clients, int n, int64_t numel, float* out,
+                const fa_seg* segs, int nseg, void* stream) {
+  fa_plan* p = nullptr;
+  int rc = cached_plan(segs, nseg, numel, nullptr, 0, 0, &p);
+  if (rc) return rc;
+  return fa_reduce(p, clients, nullptr, n, nullptr, out, nullptr, 0, stream);
+}
+
+int fa_weighted_f32(const float* const* clients, const float* w, int n, int64_t numel,
+                    float* out, const fa_seg* segs, int nseg, void* stream) {
+  if (!w) return set_err(FA_E_INVAL, "fa_weighted_f32: weights NULL");
+  fa_plan* p = nullptr;
+  int rc = cached_plan(segs, nseg, numel, nullptr, 0, 0, &p);
+  if (rc) return rc;
+  return fa_reduce(p, clients, nullptr, n, w, out, nullptr, 0, stream);
+}
+
+int fa_mean_i64_trunc(const int64_t* const* clients, int n, int64_t numel, int64_t* out,
+                      const fa_seg* segs, int nseg, void* stream) {
+  fa_plan* p = nullptr;
+  int rc = cached_plan(nullptr, 0, 0, segs, nseg, numel, &p);
+  if (rc) return rc;
+  return fa_reduce(p, nullptr, clients, n, nullptr, nullptr, out, 0, stream);
+}
+
+int fa_div_f32(const float* x, float d, float* out, int64_t numel, void* stream) {
+  if (numel < 0 || (numel > 0 && (!x || !out))) return set_err(FA_E_INVAL, "fa_div_f32: bad args");
+  if (numel == 0) return FA_OK;
+  hipLaunchKernelGGL(div_f32_kernel, dim3(grid_for(numel, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, x, d, out, numel);
+  HIP_TRY(hipGetLastError());
+  return FA_OK;
+}
+
+int fa_div_trunc_i64(const float* x, float d, int64_t* out, int64_t numel, void* stream) {
+  if (numel < 0 || (numel > 0 && (!x || !out)))
+    return set_err(FA_E_INVAL, "fa_div_trunc_i64: bad args");
+  if (numel == 0) return FA_OK;
+  hipLaunchKernelGGL(div_trunc_i64_kernel, dim3(grid_for(numel, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, x, d, out, numel);
+  HIP_TRY(hipGetLastError());
+  return FA_OK;
+}
+
+int fa_broadcast_f32(const float* src, float* const* dst, int n, int64_t numel, void* stream) {
+  if (n < 0 || n > FA_MAX_CLIENTS) return set_err(FA_E_RANGE, "fa_broadcast_f32: n=%d", n);
+  if (numel < 0 || (numel > 0 && (!src || (n > 0 && !dst))))
+    return set_err(FA_E_INVAL, "fa_broadcast_f32: bad args");
+  if (n == 0 || numel == 0) return FA_OK;
+  BcastArgs a;
+  memset(&a, 0, sizeof a);
+  a.src = src;
+  a.n = n;
+  if (!aligned16(src)) return set_err(FA_E_ALIGN, "fa_broadcast_f32: src not 16-B aligned");
+  for (int i = 0; i < n; ++i) {
+    if (!dst[i] || !aligned16(dst[i]))
+      return set_err(FA_E_ALIGN, "fa_broadcast_f32: dst %d NULL or unaligned", i);
+    a.dst[i] = dst[i];
+  }
+  hipLaunchKernelGGL(bcast_kernel, dim3(grid_for(numel / 4 + 1, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, a, numel);
+  HIP_TRY(hipGetLastError());
+  return FA_OK;
+}
+
+int fa_synth_fill_f32(float* dst, int64_t numel, int key_index, int client, float mu,
+                      float sigma, int mode, void* stream) {
+  if (numel < 0 || (numel > 0 && !dst)) return set_err(FA_E_INVAL, "fa_synth_fill_f32: bad args");
+  if (numel == 0) return FA_OK;
+  // the generator's third constant, rounded exactly as synth.key_consts does
+  volatile float s = sigma, c = 0.01f;
+  const float dsig = s * c;
+  hipLaunchKernelGGL(synth_f32_kernel, dim3(grid_for(numel, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, dst, numel, key_index, client, mu, sigma, dsig, mode);
+  HIP_TRY(hipGetLastError());
+  return FA_OK;
+}
+
+int fa_synth_fill_i64(int64_t* dst, int64_t numel, int key_index, int client, int mode,
+                      void* stream) {
+  if (numel < 0 || (numel > 0 && !dst)) return set_err(FA_E_INVAL, "fa_synth_fill_i64: bad args");
+  if (numel == 0) return FA_OK;
+  hipLaunchKernelGGL(synth_i64_kernel, dim3(grid_for(numel, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, dst, numel, key_index, client, mode);
+  HIP_TRY(hipGetLastError());
+  return FA_OK;
+}
+
+int fa_copy_f32(const float* src, float* dst, int64_t numel, void* stream) {
+  if (numel < 0 || (numel > 0 && (!src || !dst))) return set_err(FA_E_INVAL, "fa_copy_f32: bad args");
+  if (numel == 0) return FA_OK;
+  if (!aligned16(src) || !aligned16(dst)) return set_err(FA_E_ALIGN, "fa_copy_f32: unaligned");
+  hipLaunchKernelGGL(copy_kernel, dim3(grid_for(numel / 4 + 1, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, src, dst, numel);
+  HIP_TRY(hipGetLastError());
+  return FA_OK;
+}
+
+}  // extern "C"

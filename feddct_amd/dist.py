@@ -1,0 +1,142 @@
+"""Client-sharded aggregation across the GPUs of one node.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).
+Rank r holds a contiguous shard of the client slots.  A round is:
+
+1. local partial: the HIP kernel sums the rank's clients for every fp32 key
+   in the torch order, without the /N (FA_F_SUM_ONLY);
+2. exchange: ``all_reduce(SUM)`` of the partial bucket over RCCL — every rank
+   needs the global model afterwards to reload its own client slots, so the
+   "final reduce" of the north_star is an all-reduce; the bucket is cut into
+   chunks at key boundaries and chunk c's all-reduce (RCCL's own stream) runs
+   while the kernel sums chunk c+1;
+3. finish: ``/ N_total`` (IEEE division, fa_div_f32).
+
+int64 keys (a few bytes) are exchanged raw — an all-gather of every rank's
+int64 buckets — and reduced exactly over all N_total clients by the same
+kernel, so they match the single-process reference bit-for-bit.
+
+The fp32 result is the exact torch-order sum within each shard, but the
+cross-rank all-reduce re-associates it: it is NOT bit-identical to the
+single-process reference (bench.py reports the max ULP distance).  The exact
+element-sharded mode (§8 e2) is listed under "next" in DESIGN.md.
+
+The arithmetic backends are pluggable so the orchestration is testable on
+CPU with gloo (tests/test_dist_gloo.py injects oracle backends); the product
+backend is ``HipBackend``.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .layout import BucketLayout
+
+
+def shard_range(n_total: int, world: int, rank: int):
+    """Contiguous client-slot shard of ``rank`` (slot order is preserved)."""
+    base, rem = divmod(n_total, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def chunk_segments(layout: BucketLayout, nchunks: int):
+    """Split the fp32 segments into <= nchunks consecutive groups of roughly
+    equal bytes.  Returns [(segs ndarray, lo, hi)] with [lo, hi) the bucket
+    range the group spans (gaps are layout padding)."""
+    segs = layout.segs32
+    if len(segs) == 0:
+        return []
+    total = int(segs[:, 1].sum())
+    target = max(1, total // max(1, nchunks))
+    groups, cur, acc = [], [], 0
+    for o, m in segs:
+        cur.append((o, m))
+        acc += m
+        if acc >= target and len(groups) < nchunks - 1:
+            groups.append(cur)
+            cur, acc = [], 0
+    if cur:
+        groups.append(cur)
+    out = []
+    for i, g in enumerate(groups):
+        arr = np.array(g, np.int64)
+        lo = int(arr[0, 0])
+        hi = int(groups[i + 1][0][0]) if i + 1 < len(groups) else layout.f32_numel
+        out.append((arr, lo, hi))
+    return out
+
+
+class HipBackend:
+    """fa_reduce / fa_div_f32 on the current device and stream."""
+
+    def __init__(self, layout: BucketLayout, chunks, n_local: int, n_total: int):
+        from . import _lib
+        self._lib = _lib
+        self.plans = [_lib.Plan(s, layout.f32_numel) for s, _, _ in chunks]
+        self.plan64 = (_lib.Plan(np.zeros((0, 2), np.int64), 0, layout.segs64, layout.i64_numel)
+                       if layout.i64_numel else None)
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def partial_sum(self, chunk_index, clients32: Sequence[torch.Tensor], out: torch.Tensor):
+        L = self._lib
+        a = L.ptr_array([t.data_ptr() for t in clients32])
+        L.check(L.lib.fa_reduce(self.plans[chunk_index].handle, a, None, len(clients32), None,
+                                out.data_ptr(), None, L.FA_F_SUM_ONLY, self._stream()),
+                "fa_reduce(partial)")
+
+    def divide(self, x: torch.Tensor, d: float, out: torch.Tensor):
+        L = self._lib
+        L.check(L.lib.fa_div_f32(x.data_ptr(), float(d), out.data_ptr(), x.numel(),
+                                 self._stream()), "fa_div_f32")
+
+    def reduce_i64(self, clients64: Sequence[torch.Tensor], out: torch.Tensor):
+        if self.plan64 is None:
+            return
+        L = self._lib
+        a = L.ptr_array([t.data_ptr() for t in clients64])
+        L.check(L.lib.fa_reduce(self.plan64.handle, None, a, len(clients64), None, None,
+                                out.data_ptr(), 0, self._stream()), "fa_reduce(i64)")
+
+
+class ShardedAggregator:
+    """The cross-GPU round over pre-bound buckets (bench.py's N>1 step)."""
+
+    def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
+                 local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
+                 out64: torch.Tensor, nchunks: int = 4, backend=None, group=None):
+        self.layout = layout
+        self.local32, self.local64 = local32, local64
+        self.n_total = n_total
+        self.out32, self.out64 = out32, out64
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.chunks = chunk_segments(layout, nchunks)
+        self.backend = backend or HipBackend(layout, self.chunks, len(local32), n_total)
+        self.partial = torch.zeros_like(out32)
+        n_loc = len(local64)
+        self.gather64 = torch.zeros((self.world * n_loc, max(1, layout.i64_numel)),
+                                    dtype=torch.int64, device=out64.device)
+        self.stack64 = torch.stack(local64, 0) if local64 else None
+
+    def step(self) -> None:
+        works = []
+        for c, (_, lo, hi) in enumerate(self.chunks):
+            self.backend.partial_sum(c, self.local32, self.partial)
+            works.append(dist.all_reduce(self.partial[lo:hi], op=dist.ReduceOp.SUM,
+                                         group=self.group, async_op=True))
+        if self.layout.i64_numel:
+            self.stack64.copy_(torch.stack(self.local64, 0))
+            works.append(dist.all_gather_into_tensor(self.gather64, self.stack64,
+                                                     group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+        self.backend.divide(self.partial, float(self.n_total), self.out32)
+        if self.layout.i64_numel:
+            self.backend.reduce_i64(list(self.gather64.unbind(0)), self.out64)

@@ -1,0 +1,167 @@
+/*
+ * fedagg.h — C ABI of libfedagg.so, the MI355X (gfx950) server-side
+ * parameter-aggregation engine.
+ *
+ * Drop-in boundary.  The reference has no native plugin/FFI API: its hot path
+ * is the Python function
+ *
+ *     server_aggregate(global_model, client_models)
+ *         train_fedavg.py:138-149  ==  train_fedprox.py:143-154
+ *     server_aggregate(g_main, g_proxy, mains, proxies)
+ *         train_feddct.py:34-56    ==  train_splitfed.py:34-56
+ *
+ * whose arithmetic is, per state_dict key k (train_fedavg.py:145-146),
+ *
+ *     torch.stack([client_models[i].state_dict()[k].float() for i], 0).mean(0)
+ *
+ * followed by load_state_dict into the global model (:147) and a broadcast of
+ * the global state back into every client (:148-149).  The Python shim
+ * feddct_amd.aggregate.server_aggregate keeps those signatures and side
+ * effects and binds this ABI through ctypes; every entry
+ * point below replaces one piece of that expression:
+ *
+ *   fa_reduce            stack(...).mean(0) for every key at once, over flat
+ *                        per-client buckets (all fp32 keys + all int64 keys),
+ *                        optionally fused with the :148-149 broadcast.
+ *   fa_mean_f32          the same for fp32 keys only, stateless form.
+ *   fa_weighted_f32      client-size-weighted extension.
+ *   fa_mean_i64_trunc    int64 keys: .float() -> mean -> copy_ into int64
+ *                        (truncation toward zero), train_fedavg.py:146-147.
+ *
+ * Summation order.  Results are bit-identical to torch's CPU
+ * stack(...).mean(0) (ATen SumKernel cascade_sum, single-thread order; see
+ * DESIGN.md §2): columns of a tensor with numel M are summed over the N
+ * clients by the 4-level cascade (block 16) for the first (M/32)*32 columns
+ * (M>=8) or (M/4)*4 columns (2<=M<8), by the ILP-4 interleaved order for the
+ * remaining tail columns, and by the 8-lane inner order when M==1; the sum
+ * starts from +0 and is divided by N with IEEE true division.
+ *
+ * Conventions
+ *   - All buffers are caller-owned DEVICE pointers (PyTorch-ROCm tensors via
+ *     data_ptr(), zero-copy).  The library never allocates or frees caller
+ *     memory; plans own a small device-resident tile table.
+ *   - Offsets and counts are in ELEMENTS of the bucket's dtype.
+ *   - Return 0 on success or a negative FA_E* code; fa_last_error() returns a
+ *     thread-local message for the last failure on the calling thread.
+ *   - Calls are stream-ordered on the caller's stream (hipStream_t passed as
+ *     void*, 0 = null stream) and never synchronise; reentrant.
+ */
+#ifndef FEDAGG_H
+#define FEDAGG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA_OK 0
+#define FA_E_INVAL (-1)   /* bad argument (null pointer, n<1, overlap ...)   */
+#define FA_E_RANGE (-2)   /* n exceeds FA_MAX_CLIENTS, size overflow          */
+#define FA_E_ALIGN (-3)   /* a vectorised bucket pointer is not 16-B aligned */
+#define FA_E_HIP (-4)     /* HIP runtime error (message in fa_last_error)     */
+#define FA_E_NOMEM (-5)
+
+/* Max clients per call.  Up to FA_INLINE_CLIENTS the client pointer tables
+ * travel in the kernel arguments; above, in a stream-ordered device table. */
+#define FA_MAX_CLIENTS 4096
+#define FA_INLINE_CLIENTS 128
+
+/* fa_reduce flags */
+#define FA_F_BCAST 1u    /* also write the result into every client bucket  */
+#define FA_F_SUM_ONLY 2u /* fp32 keys: write the ordered sum, skip the /N   */
+
+/* Plan-build flags */
+#define FA_PLAN_GAPS_ARE_PADDING 1u /* bytes between segments may be written */
+
+/* One tensor (state_dict key) inside a flat bucket: [offset, offset+numel). */
+typedef struct fa_seg {
+  int64_t offset;
+  int64_t numel;
+} fa_seg;
+
+typedef struct fa_plan fa_plan; /* opaque: layout -> device tile table */
+
+typedef struct fa_plan_info {
+  int64_t f32_numel;      /* bucket length covered by the plan             */
+  int64_t i64_numel;
+  int32_t ntiles;         /* total work tiles (one workgroup each)          */
+  int32_t ntiles_cascade; /* vectorised cascade tiles                       */
+  int32_t ntiles_tail;    /* ILP-4 tail / M==1 / int64 tiles                */
+  int32_t tile_elems;     /* fp32 elements per cascade tile                 */
+  int64_t cascade_elems;  /* elements summed by the vectorised cascade      */
+  int64_t tail_elems;     /* elements summed in the scalar orders           */
+} fa_plan_info;
+
+const char *fa_version(void);
+const char *fa_last_error(void);
+
+/* Build a plan for a bucket layout.  seg32 / seg64 describe the fp32 and
+ * int64 keys (either may be empty).  tile_elems: fp32 elements per
+ * vectorised tile (0 = default).  Allocates + uploads the tile table (sync). */
+int fa_plan_create(const fa_seg *seg32, int nseg32, int64_t f32_numel,
+                   const fa_seg *seg64, int nseg64, int64_t i64_numel,
+                   int tile_elems, unsigned flags, fa_plan **out);
+int fa_plan_destroy(fa_plan *plan);
+
+/* Host-only tile table of a layout (no device, no allocation): for tests and
+ * inspection.  kind: 0 fp32 cascade (16-B vectors), 1 fp32 cascade (scalar),
+ * 2 fp32 ILP-4 tail, 3 fp32 M==1, 4/5/6 int64 cascade/ILP-4/M==1.  With
+ * tiles==NULL only info is filled. */
+typedef struct fa_tile_desc {
+  int64_t start;
+  int32_t count;
+  int32_t kind;
+} fa_tile_desc;
+int fa_plan_build_host(const fa_seg *seg32, int nseg32, int64_t f32_numel,
+                       const fa_seg *seg64, int nseg64, int64_t i64_numel,
+                       int tile_elems, unsigned flags, fa_tile_desc *tiles,
+                       int cap, fa_plan_info *info);
+int fa_plan_get_info(const fa_plan *plan, fa_plan_info *info);
+
+/* The hot path: every key of N client buckets -> global bucket, one launch.
+ *   c32[i] / c64[i]  : client i's fp32 / int64 bucket (slot order 0..n-1)
+ *   weights          : NULL -> mean (sum / n);  else fp32 w[i], result =
+ *                      ordered sum of fp32(x_i * w_i) (no division)
+ *   out32 / out64    : global buckets (may alias a client bucket)
+ *   flags            : FA_F_BCAST | FA_F_SUM_ONLY
+ * int64 keys always take the mean + truncation path (weights ignored). */
+int fa_reduce(const fa_plan *plan, const float *const *c32,
+              const int64_t *const *c64, int n, const float *weights,
+              float *out32, int64_t *out64, unsigned flags, void *stream);
+
+/* Stateless fp32 mean over segments (plan cached internally by layout). */
+int fa_mean_f32(const float *const *clients, int n, int64_t numel, float *out,
+                const fa_seg *segs, int nseg, void *stream);
+/* Stateless weighted sum: out = sum_i fp32(x_i * w_i) in torch order. */
+int fa_weighted_f32(const float *const *clients, const float *w, int n,
+                    int64_t numel, float *out, const fa_seg *segs, int nseg,
+                    void *stream);
+/* int64 keys, each segment its own tensor; numel elements total. */
+int fa_mean_i64_trunc(const int64_t *const *clients, int n, int64_t numel,
+                      int64_t *out, const fa_seg *segs, int nseg,
+                      void *stream);
+
+/* Elementwise out[j] = x[j] / d (IEEE true division), fp32; and the int64
+ * finish of a cross-GPU partial sum: out64[j] = trunc(x[j] / d). */
+int fa_div_f32(const float *x, float d, float *out, int64_t numel,
+               void *stream);
+int fa_div_trunc_i64(const float *x, float d, int64_t *out, int64_t numel,
+                     void *stream);
+/* Copy a bucket into n destinations (the standalone broadcast). */
+int fa_broadcast_f32(const float *src, float *const *dst, int n,
+                     int64_t numel, void *stream);
+
+/* Synthetic client state (feddct_amd/synth.py restated bit-exactly). */
+int fa_synth_fill_f32(float *dst, int64_t numel, int key_index, int client,
+                      float mu, float sigma, int mode, void *stream);
+int fa_synth_fill_i64(int64_t *dst, int64_t numel, int key_index, int client,
+                      int mode, void *stream);
+
+/* Streaming copy (bandwidth ceiling calibration for the roofline). */
+int fa_copy_f32(const float *src, float *dst, int64_t numel, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEDAGG_H */

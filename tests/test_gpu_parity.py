@@ -1,0 +1,395 @@
+"""GPU parity: the HIP kernels (through the C ABI and through the drop-in
+shim) against the oracle and the reference's own outputs.  Bit-exact for
+every fp32 and int64 key (NaN positions must match; payloads are free)."""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, load_manifest
+from feddct_amd import synth
+from feddct_amd.layout import BucketLayout
+from helpers import StateModule, bits_equal, buckets_to_state, states_to_buckets
+from oracle import torch_order as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from feddct_amd import _lib
+    torch.cuda.set_device(DEV)
+    return _lib
+
+
+def _reduce(lib, layout, buckets, weights=None, flags=0, tile_elems=0, out_pad=None):
+    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
+                    tile_elems=tile_elems)
+    n = len(buckets)
+    out32 = torch.full_like(buckets[0][0], np.nan if out_pad is None else out_pad)
+    out64 = torch.full_like(buckets[0][1], -7)
+    w = None if weights is None else (ctypes.c_float * n)(*[float(x) for x in weights])
+    stream = torch.cuda.current_stream().cuda_stream
+    lib.check(lib.lib.fa_reduce(plan.handle, lib.ptr_array([b[0].data_ptr() for b in buckets]),
+                                lib.ptr_array([b[1].data_ptr() for b in buckets]), n, w,
+                                out32.data_ptr(), out64.data_ptr(), flags,
+                                ctypes.c_void_p(stream)), "fa_reduce")
+    torch.cuda.synchronize()
+    return out32, out64
+
+
+def _rand_manifest(rng, sizes):
+    keys = [{"key": f"k{j}", "shape": [int(m)] if m != 0 else [], "dtype": "float32"}
+            for j, m in enumerate(sizes)]
+    keys.append({"key": "nbt", "shape": [], "dtype": "int64"})
+    return {"keys": keys}
+
+
+SIZES = [0, 2, 3, 4, 5, 7, 8, 9, 16, 31, 32, 33, 63, 64, 65, 100, 432, 1000, 2047, 2048, 2049,
+         4097, 5120, 9000]
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 7, 8, 9, 15, 16, 17, 20, 24, 31, 32, 33, 48, 64,
+                               100, 127, 128, 129, 255, 256, 300])
+@pytest.mark.parametrize("mode", [synth.MODE_REALISTIC, synth.MODE_ADVERSARIAL])
+def test_reduce_matches_oracle(lib, n, mode):
+    man = _rand_manifest(np.random.default_rng(n), SIZES)
+    layout = BucketLayout.from_manifest(man)
+    states = [synth.gen_state(man, i, mode) for i in range(n)]
+    out32, out64 = _reduce(lib, layout, states_to_buckets(layout, states, DEV))
+    got = buckets_to_state(layout, out32, out64)
+    for (k, want), (k2, g) in zip(O.aggregate_state(states), got):
+        assert k == k2 and bits_equal(g, want), (n, mode, k)
+
+
+@pytest.mark.parametrize("tile_elems", [1024, 2048, 4096])
+def test_tile_sizes_bit_exact(lib, tile_elems):
+    n = 20
+    man = _rand_manifest(None, [8192 + 32, 4096, 12345, 1])
+    layout = BucketLayout.from_manifest(man)
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    out32, out64 = _reduce(lib, layout, states_to_buckets(layout, states, DEV),
+                           tile_elems=tile_elems)
+    for (k, want), (_, g) in zip(O.aggregate_state(states),
+                                 buckets_to_state(layout, out32, out64)):
+        assert bits_equal(g, want), k
+
+
+def test_special_values_and_subnormals(lib):
+    n, M = 17, 300
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((n, M)).astype(np.float32)
+    x[:, 0] = -0.0
+    x[:, 1] = np.float32(1e-45) * rng.integers(-5, 5, n)   # subnormals
+    x[3, 2] = np.inf
+    x[5, 3] = np.nan
+    x[:, 4] = np.float32(3e38)                             # overflow to inf
+    x[:, 5] = np.float32(1e-40)
+    man = {"keys": [{"key": "t", "shape": [M], "dtype": "float32"}]}
+    layout = BucketLayout.from_manifest(man)
+    states = [[("t", x[i])] for i in range(n)]
+    out32, _ = _reduce(lib, layout, states_to_buckets(layout, states, DEV))
+    got = buckets_to_state(layout, out32, torch.zeros(1, dtype=torch.int64))[0][1]
+    want = O.torch_mean0(x)
+    assert bits_equal(got, want)
+    ref = torch.from_numpy(x).mean(0).numpy()
+    assert bits_equal(got, ref)
+    assert got.view(np.uint32)[0] == 0
+
+
+def test_weighted_matches_oracle(lib):
+    n = 20
+    man = _rand_manifest(None, SIZES)
+    layout = BucketLayout.from_manifest(man)
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    w = O.weights_from_sizes(np.arange(1, n + 1) * 37)
+    out32, out64 = _reduce(lib, layout, states_to_buckets(layout, states, DEV), weights=w)
+    got = dict(buckets_to_state(layout, out32, out64))
+    for j, (k, _) in enumerate(states[0]):
+        x = np.stack([s[j][1] for s in states])
+        want = O.mean_i64_trunc(x) if x.dtype == np.int64 else O.weighted_sum0(x, w)
+        assert bits_equal(got[k], want), k
+
+
+def test_sum_only_and_bcast_flags(lib):
+    from feddct_amd._lib import FA_F_BCAST, FA_F_SUM_ONLY
+    n = 9
+    man = _rand_manifest(None, [100, 4096, 7, 1])
+    layout = BucketLayout.from_manifest(man)
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    bk = states_to_buckets(layout, states, DEV)
+    out32, _ = _reduce(lib, layout, bk, flags=FA_F_SUM_ONLY)
+    got = dict(buckets_to_state(layout, out32, torch.zeros(1, dtype=torch.int64)))
+    for j, (k, _) in enumerate(states[0]):
+        x = np.stack([s[j][1] for s in states])
+        if x.dtype == np.float32:
+            assert bits_equal(got[k], O.torch_sum0(x)), k
+    bk = states_to_buckets(layout, states, DEV)
+    out32, out64 = _reduce(lib, layout, bk, flags=FA_F_BCAST)
+    want = buckets_to_state(layout, out32, out64)
+    for f32, i64 in bk:
+        for (k, a), (_, b) in zip(buckets_to_state(layout, f32, i64), want):
+            assert bits_equal(a, b), k
+
+
+def test_int64_adversarial(lib):
+    man = {"keys": [{"key": f"i{j}", "shape": s, "dtype": "int64"}
+                    for j, s in enumerate([[], [1], [3], [9], [40], [300]])]}
+    layout = BucketLayout.from_manifest(man)
+    for n in (1, 2, 7, 8, 9, 20, 33):
+        states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+        out32, out64 = _reduce(lib, layout, states_to_buckets(layout, states, DEV))
+        for (k, want), (_, g) in zip(O.aggregate_state(states),
+                                     buckets_to_state(layout, out32, out64)):
+            assert bits_equal(g, want), (n, k)
+
+
+def test_synth_fill_matches_numpy(lib):
+    stream = torch.cuda.current_stream().cuda_stream
+    for mode in (0, 1):
+        for key, name, shape in [(0, "a.weight", (64, 3, 3, 3)), (5, "b.running_var", (777,)),
+                                 (9, "fc.weight", (10, 640))]:
+            mu, sigma = synth.key_params(name, shape, "float32")
+            numel = int(np.prod(shape))
+            t = torch.empty(numel, dtype=torch.float32, device=DEV)
+            lib.check(lib.lib.fa_synth_fill_f32(t.data_ptr(), numel, key, 3, mu, sigma, mode,
+                                                ctypes.c_void_p(stream)))
+            want = synth.gen_f32(key, numel, 3, mu, sigma, mode)
+            assert bits_equal(t.cpu().numpy(), want), (mode, name)
+        t = torch.empty(50, dtype=torch.int64, device=DEV)
+        lib.check(lib.lib.fa_synth_fill_i64(t.data_ptr(), 50, 7, 2, mode, ctypes.c_void_p(stream)))
+        assert np.array_equal(t.cpu().numpy(), synth.gen_i64(7, 50, 2, mode))
+
+
+def test_stateless_abi(lib):
+    n, M = 6, 3000
+    x = np.random.default_rng(1).standard_normal((n, M)).astype(np.float32)
+    segs = np.array([[0, 1000], [1024, 1976]], np.int64)
+    bufs = [torch.from_numpy(np.concatenate([x[i, :1000], np.zeros(24, np.float32), x[i, 1000:2976]])).to(DEV)
+            for i in range(n)]
+    out = torch.zeros(3000, device=DEV)
+    arr, ns = lib.seg_array(segs)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    lib.check(lib.lib.fa_mean_f32(lib.ptr_array([b.data_ptr() for b in bufs]), n, 3000,
+                                  out.data_ptr(), arr, ns, stream))
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    assert bits_equal(o[:1000], O.torch_mean0(x[:, :1000]))
+    assert bits_equal(o[1024:3000], O.torch_mean0(x[:, 1000:2976]))
+    assert (o[1000:1024] == 0).all(), "stateless plan must not write gaps"
+    w = O.weights_from_sizes([3, 1, 4, 1, 5, 9])
+    lib.check(lib.lib.fa_weighted_f32(lib.ptr_array([b.data_ptr() for b in bufs]),
+                                      (ctypes.c_float * n)(*map(float, w)), n, 3000,
+                                      out.data_ptr(), arr, ns, stream))
+    torch.cuda.synchronize()
+    assert bits_equal(out.cpu().numpy()[:1000], O.weighted_sum0(x[:, :1000], w))
+    iv = [torch.tensor([i * 1000003 - 5, 7 * i], dtype=torch.int64, device=DEV) for i in range(n)]
+    o64 = torch.zeros(2, dtype=torch.int64, device=DEV)
+    a64, n64 = lib.seg_array(np.array([[0, 1], [1, 1]], np.int64))
+    lib.check(lib.lib.fa_mean_i64_trunc(lib.ptr_array([t.data_ptr() for t in iv]), n, 2,
+                                        o64.data_ptr(), a64, n64, stream))
+    torch.cuda.synchronize()
+    xs = np.stack([t.cpu().numpy() for t in iv])
+    assert o64.cpu().tolist() == [int(O.mean_i64_trunc(xs[:, 0])), int(O.mean_i64_trunc(xs[:, 1]))]
+
+
+def test_errors(lib):
+    from feddct_amd._lib import FedaggError
+    layout = BucketLayout.from_manifest(_rand_manifest(None, [100]))
+    with pytest.raises(FedaggError, match="FA_MAX_CLIENTS|exceeds"):
+        bk = states_to_buckets(layout, [synth.gen_state({"keys": [
+            {"key": "k0", "shape": [100], "dtype": "float32"},
+            {"key": "nbt", "shape": [], "dtype": "int64"}]}, 0)], DEV)
+        _reduce(lib, layout, bk * 4097)
+    misaligned = torch.zeros(200, device=DEV)[1:]
+    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel)
+    rc = lib.lib.fa_reduce(plan.handle, lib.ptr_array([misaligned.data_ptr()]),
+                           lib.ptr_array([misaligned.data_ptr()]), 1, None,
+                           misaligned.data_ptr(), misaligned.data_ptr(), 0, None)
+    assert rc == lib.FA_E_ALIGN
+
+
+# ----------------------------------------------------------- drop-in shim --
+def _modules(man, states):
+    return [StateModule(man).load_numpy(s).to(DEV) for s in states]
+
+
+@pytest.mark.parametrize("variant", ["fedavg", "fedprox"])
+@pytest.mark.parametrize("mode", [synth.MODE_REALISTIC, synth.MODE_ADVERSARIAL])
+def test_shim_matches_reference_goldens(golden, variant, mode):
+    import importlib
+    sa = importlib.import_module(f"feddct_amd.{variant}").server_aggregate
+    man = golden["manifest"]["small"]
+    gold = golden["gold"]
+    for n in golden["manifest"]["ns"]:
+        states = [synth.gen_state(man, i, mode) for i in range(n)]
+        g = StateModule(man).to(DEV)
+        clients = _modules(man, states)
+        sa(g, clients)
+        torch.cuda.synchronize()
+        gsd = g.state_dict()
+        for e in man["keys"]:
+            k = e["key"]
+            ref = gold[f"{variant}/m{mode}/n{n}/{k}"]
+            assert bits_equal(gsd[k].cpu().numpy(), ref), (variant, n, k)
+            for c in clients:
+                assert bits_equal(c.state_dict()[k].cpu().numpy(), ref), "broadcast"
+
+
+@pytest.mark.parametrize("variant", ["feddct", "splitfed"])
+def test_shim_split_matches_reference_goldens(golden, variant):
+    import importlib
+    sa = importlib.import_module(f"feddct_amd.{variant}").server_aggregate
+    mm, pm = golden["manifest"]["main"], golden["manifest"]["proxy"]
+    gold = golden["gold"]
+    for n in (5, 24):
+        ms = _modules(mm, [synth.gen_state(mm, i, synth.MODE_ADVERSARIAL) for i in range(n)])
+        ps = _modules(pm, [synth.gen_state(pm, 100 + i, synth.MODE_ADVERSARIAL) for i in range(n)])
+        gm, gp = StateModule(mm).to(DEV), StateModule(pm).to(DEV)
+        sa(gm, gp, ms, ps)
+        torch.cuda.synchronize()
+        for part, g, cl in (("main", gm, ms), ("proxy", gp, ps)):
+            for k, v in g.state_dict().items():
+                ref = gold[f"{variant}/n{n}/{part}/{k}"]
+                assert bits_equal(v.cpu().numpy(), ref), (part, k)
+                assert bits_equal(cl[-1].state_dict()[k].cpu().numpy(), ref)
+
+
+def test_shim_host_resident_modules(golden):
+    """The reference's CPU configuration (BASELINE config 1): modules in host
+    memory, staged through the GPU and written back."""
+    from feddct_amd.fedavg import server_aggregate
+    man = golden["manifest"]["small"]
+    gold = golden["gold"]
+    n = 20
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    g = StateModule(man)
+    clients = [StateModule(man).load_numpy(s) for s in states]
+    server_aggregate(g, clients)
+    for k, v in g.state_dict().items():
+        assert v.device.type == "cpu"
+        assert bits_equal(v.numpy(), gold[f"fedavg/m1/n{n}/{k}"]), k
+        assert bits_equal(clients[7].state_dict()[k].numpy(), gold[f"fedavg/m1/n{n}/{k}"])
+
+
+def test_shim_second_round_and_rebind():
+    """Arena binding persists across rounds; training-style in-place updates
+    are seen; replacing a parameter triggers a re-bind."""
+    from feddct_amd.fedavg import server_aggregate
+    man = {"keys": [{"key": "w", "shape": [1000], "dtype": "float32"},
+                    {"key": "n", "shape": [], "dtype": "int64"}]}
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(4)]
+    g = StateModule(man).to(DEV)
+    clients = _modules(man, states)
+    server_aggregate(g, clients)
+    with torch.no_grad():
+        for i, c in enumerate(clients):
+            c.w.mul_(float(i + 1))
+            c.n.add_(i)
+    clients[2].w = torch.nn.Parameter(clients[2].w.detach().clone() + 1)  # new object
+    snap = [[(k, v.detach().cpu().numpy().copy()) for k, v in c.state_dict().items()]
+            for c in clients]
+    server_aggregate(g, clients)
+    torch.cuda.synchronize()
+    for (k, want) in O.aggregate_state(snap):
+        assert bits_equal(g.state_dict()[k].cpu().numpy(), want), k
+        assert bits_equal(clients[2].state_dict()[k].cpu().numpy(), want), k
+
+
+def test_shim_errors_like_reference():
+    from feddct_amd.fedavg import server_aggregate
+    man = {"keys": [{"key": "w", "shape": [10], "dtype": "float32"}]}
+    g = StateModule(man).to(DEV)
+    with pytest.raises(RuntimeError):
+        server_aggregate(g, [])
+    other = StateModule({"keys": [{"key": "v", "shape": [10], "dtype": "float32"}]}).to(DEV)
+    with pytest.raises(KeyError):
+        server_aggregate(g, [StateModule(man).to(DEV), other])
+    bad = StateModule({"keys": [{"key": "w", "shape": [11], "dtype": "float32"}]}).to(DEV)
+    with pytest.raises(RuntimeError):
+        server_aggregate(g, [StateModule(man).to(DEV), bad])
+    extra = StateModule({"keys": man["keys"] + [{"key": "z", "shape": [2], "dtype": "float32"}]})
+    extra = extra.to(DEV)
+    c0 = StateModule(man).to(DEV)
+    with torch.no_grad():
+        c0.w.fill_(2.0)
+        extra.w.fill_(4.0)
+    with pytest.raises(RuntimeError, match="Missing key"):
+        server_aggregate(g, [c0, extra])
+    assert torch.all(g.w == 3.0) and torch.all(c0.w == 3.0)  # global + earlier clients updated
+
+
+def test_shim_mixed_dtypes_packed():
+    """Non-fp32 floating keys and int32/bool buffers take the packed path
+    (.float() -> mean -> copy_ back), as load_state_dict would."""
+    from feddct_amd.fedavg import server_aggregate
+    man = {"keys": [{"key": "h", "shape": [70], "dtype": "float16"},
+                    {"key": "d", "shape": [33], "dtype": "float64"},
+                    {"key": "b", "shape": [5], "dtype": "bool"},
+                    {"key": "i", "shape": [4], "dtype": "int32"},
+                    {"key": "f", "shape": [40], "dtype": "float32"}]}
+    rng = np.random.default_rng(0)
+    n = 5
+    cpu_mods = []
+    for i in range(n):
+        m = StateModule(man)
+        with torch.no_grad():
+            m.h.copy_(torch.from_numpy(rng.standard_normal(70).astype(np.float16)))
+            m.d.copy_(torch.from_numpy(rng.standard_normal(33)))
+            m.b.copy_(torch.from_numpy(rng.integers(0, 2, 5).astype(bool)))
+            m.i.copy_(torch.from_numpy(rng.integers(-99, 99, 4).astype(np.int32)))
+            m.f.copy_(torch.from_numpy(rng.standard_normal(40).astype(np.float32)))
+        cpu_mods.append(m)
+    want = {}
+    for k in ("h", "d", "b", "i", "f"):
+        ref = torch.stack([m.state_dict()[k].float() for m in cpu_mods], 0).mean(0)
+        t = cpu_mods[0].state_dict()[k].clone()
+        t.copy_(ref)
+        want[k] = t
+    g = StateModule(man).to(DEV)
+    clients = [m.to(DEV) for m in cpu_mods]
+    server_aggregate(g, clients)
+    torch.cuda.synchronize()
+    for k, v in want.items():
+        assert torch.equal(g.state_dict()[k].cpu(), v), k
+        assert torch.equal(clients[3].state_dict()[k].cpu(), v), k
+
+
+# ------------------------------------------------------ full-size digests --
+def _full_case(lib, lay_name, n, device=DEV):
+    man = load_manifest(lay_name)
+    layout = BucketLayout.from_manifest(man)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    bk = []
+    for i in range(n):
+        f32 = torch.zeros(layout.f32_numel, dtype=torch.float32, device=device)
+        i64 = torch.zeros(max(1, layout.i64_numel), dtype=torch.int64, device=device)
+        for j, e in enumerate(man["keys"]):
+            s = layout.by_key[e["key"]]
+            if s.kind == "i64":
+                lib.check(lib.lib.fa_synth_fill_i64(i64[s.offset:].data_ptr(), s.numel, j, i, 0,
+                                                    stream))
+            else:
+                mu, sigma = synth.key_params(e["key"], tuple(e["shape"]), e["dtype"])
+                lib.check(lib.lib.fa_synth_fill_f32(f32[s.offset:].data_ptr(), s.numel, j, i,
+                                                    mu, sigma, 0, stream))
+        bk.append((f32, i64))
+    out32, out64 = _reduce(lib, layout, bk)
+    return O.state_digest(buckets_to_state(layout, out32, out64))
+
+
+@pytest.mark.parametrize("case", ["fedavg/wrn16_8_c10/n2", "fedavg/wrn16_8_c10/n20",
+                                  "fedprox/wrn16_8_c100/n20",
+                                  "feddct/wrnsl16_8_sf4_c10_main/n5",
+                                  "feddct/wrnsl16_8_sf4_c10_proxy/n5",
+                                  "feddct/wrnsl16_8_sf4_c100_main/n24",
+                                  "feddct/wrnsl16_8_sf4_c100_proxy/n24"])
+def test_full_size_digest_vs_reference(lib, golden, case):
+    _, lay, nn = case.split("/")
+    assert _full_case(lib, lay, int(nn[1:])) == golden["digests"][case]
