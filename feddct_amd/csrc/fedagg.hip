@@ -95,13 +95,20 @@ struct ReduceArgs {
   float w[kInline];
 };
 
-__device__ __forceinline__ const float* cptr32(const ReduceArgs& a, int i) {
+// The kernel reads its arguments through this constant-address-space view of
+// the kernarg segment.  Binding a by-value struct parameter to a reference
+// instead makes the compiler copy the whole 2.6 KB struct into per-lane
+// scratch (measured: 7x slower); the kernarg view keeps every pointer fetch a
+// scalar load.
+typedef __attribute__((address_space(4))) const ReduceArgs KArgs;
+
+__device__ __forceinline__ const float* cptr32(KArgs& a, int i) {
   return a.n <= kInline ? a.c32[i] : a.tab32[i];
 }
-__device__ __forceinline__ const int64_t* cptr64(const ReduceArgs& a, int i) {
+__device__ __forceinline__ const int64_t* cptr64(KArgs& a, int i) {
   return a.n <= kInline ? a.c64[i] : a.tab64[i];
 }
-__device__ __forceinline__ float cw(const ReduceArgs& a, int i) {
+__device__ __forceinline__ float cw(KArgs& a, int i) {
   return a.n <= kInline ? a.w[i] : a.tabw[i];
 }
 
@@ -182,7 +189,7 @@ __device__ __forceinline__ void promote(Acc<U, DEEP>& A, int ii, int lp, int mas
 // One batch of NB clients starting at b0.  FULL: every lane's U vectors are
 // inside the tile (no per-lane predicate).
 template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, bool NT>
-__device__ __forceinline__ void batch(const ReduceArgs& a, Acc<U, DEEP>& A, int b0,
+__device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0,
                                       const int64_t (&off)[U], const bool (&ok)[U],
                                       int lp, int mask) {
   f4 x[NB][U];
@@ -208,7 +215,7 @@ __device__ __forceinline__ void batch(const ReduceArgs& a, Acc<U, DEEP>& A, int 
 }
 
 template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, bool NT>
-__device__ __forceinline__ void tile_vec(const ReduceArgs& a, int64_t start,
+__device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
                                          int count) {
   const int n = a.n;
   const int lp = level_power(n);
@@ -251,7 +258,7 @@ __device__ __forceinline__ void tile_vec(const ReduceArgs& a, int64_t start,
 
 // ------------------------------------------------------- scalar orders ----
 struct SrcF32 {
-  const ReduceArgs& a;
+  KArgs& a;
   bool weighted;
   __device__ float operator()(int i, int64_t e) const {
     float x = cptr32(a, i)[e];
@@ -259,7 +266,7 @@ struct SrcF32 {
   }
 };
 struct SrcI64 {
-  const ReduceArgs& a;
+  KArgs& a;
   __device__ float operator()(int i, int64_t e) const {
     return (float)cptr64(a, i)[e];  // .float(): int64 -> fp32, round to nearest
   }
@@ -311,7 +318,7 @@ __device__ float inner_seq(const Src& src, int64_t e, int n) {
 }
 
 template <bool WEIGHTED>
-__device__ void tile_scalar(const ReduceArgs& a, const Tile& t) {
+__device__ void tile_scalar(KArgs& a, const Tile& t) {
   const int j = threadIdx.x;
   if (j >= t.count) return;
   const int64_t e = t.start + j;
@@ -345,7 +352,9 @@ __device__ void tile_scalar(const ReduceArgs& a, const Tile& t) {
 }
 
 template <int U, int B, bool DEEP, bool WEIGHTED, bool NT>
-__global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs a) {
+__global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs args) {
+  (void)args;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const Tile t = a.tiles[blockIdx.x];
   if (t.kind == K_F32_VEC) {
     if (t.count == 4 * U * kBlock) tile_vec<U, B, true, DEEP, WEIGHTED, NT>(a, t.start, t.count);
@@ -453,6 +462,7 @@ struct fa_plan {
   Tile* d_tiles = nullptr;
   fa_plan_info info{};
   int vec_u = kDefaultU;
+  unsigned flags = 0;
 };
 
 namespace {
@@ -554,10 +564,6 @@ hipError_t launch_one(const ReduceArgs& a, int ntiles, hipStream_t st) {
   return hipGetLastError();
 }
 
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
 
 template <int U, int B>
 hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, bool nt, hipStream_t st) {
@@ -569,12 +575,12 @@ hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, bool nt,
             : launch_one<U, B, false, false, false>(a, ntiles, st);
 }
 
-hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, hipStream_t st) {
+hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pflags,
+                         hipStream_t st) {
   const bool deep = a.n >= 256;
   const bool w = a.flags & 0x100u;  // internal: weighted
-  static const int nt_env = env_int("FEDAGG_NT", 1);
-  static const int b_env = env_int("FEDAGG_BATCH", 8);
-  const bool nt = nt_env != 0;
+  const bool nt = !(pflags & FA_PLAN_TUNE_NO_NT);
+  const int b_env = (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : 8;
   switch (vec_u) {
     case 1: return b_env == 16 ? launch_u<1, 16>(a, ntiles, deep, w, nt, st)
                                : launch_u<1, 8>(a, ntiles, deep, w, nt, st);
@@ -623,7 +629,7 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   if (!out) return set_err(FA_E_INVAL, "fa_plan_create: out is NULL");
   *out = nullptr;
   if (f32_numel < 0 || i64_numel < 0) return set_err(FA_E_INVAL, "negative bucket size");
-  if (tile_elems == 0) tile_elems = 4 * kBlock * env_int("FEDAGG_U", kDefaultU);
+  if (tile_elems == 0) tile_elems = 4 * kBlock * kDefaultU;
   if (tile_elems != 4 * kBlock && tile_elems != 8 * kBlock && tile_elems != 16 * kBlock)
     return set_err(FA_E_INVAL, "tile_elems must be 1024, 2048 or 4096 (got %d)", tile_elems);
   std::vector<fa_seg> s32, s64;
@@ -636,6 +642,7 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   p->info.i64_numel = i64_numel;
   p->info.tile_elems = tile_elems;
   p->vec_u = tile_elems / (4 * kBlock);
+  p->flags = flags;
   std::vector<Tile> tiles;
   build_tiles(s32, s64, tile_elems, flags, &tiles, &p->info);
   hipError_t e = hipGetDevice(&p->device);
@@ -755,7 +762,7 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
     a.tab64 = (const int64_t* const*)((const void**)table + n);
     a.tabw = (const float*)((const void**)table + 2 * n);
   }
-  hipError_t e = launch_reduce(a, in.ntiles, plan->vec_u, st);
+  hipError_t e = launch_reduce(a, in.ntiles, plan->vec_u, plan->flags, st);
   if (table) {
     hipError_t e2 = hipFreeAsync(table, st);
     if (e == hipSuccess) e = e2;
