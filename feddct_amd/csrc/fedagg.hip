@@ -580,7 +580,7 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   const bool deep = a.n >= 256;
   const bool w = a.flags & 0x100u;  // internal: weighted
   const bool nt = !(pflags & FA_PLAN_TUNE_NO_NT);
-  const int b_env = (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : 8;
+  const int b_env = (pflags & FA_PLAN_TUNE_BATCH8) ? 8 : 16;
   switch (vec_u) {
     case 1: return b_env == 16 ? launch_u<1, 16>(a, ntiles, deep, w, nt, st)
                                : launch_u<1, 8>(a, ntiles, deep, w, nt, st);
