@@ -201,6 +201,10 @@ def main():
     ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI); gloo only to rehearse ranks on one GPU")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal: every rank on cuda:0 (with --dist-backend gloo)")
     ap.add_argument("--kernel-only", action="store_true",
                     help="only the timed reduce launches (for rocprofv3 runs)")
     args = ap.parse_args()
@@ -210,11 +214,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if args.same_device:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     group = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
         group = dist.group.WORLD
 
     manifest = load_manifest(LAYOUT)

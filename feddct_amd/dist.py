@@ -120,10 +120,18 @@ class ShardedAggregator:
         self.chunks = chunk_segments(layout, nchunks)
         self.backend = backend or HipBackend(layout, self.chunks, len(local32), n_total)
         self.partial = torch.zeros_like(out32)
-        n_loc = len(local64)
-        self.gather64 = torch.zeros((self.world * n_loc, max(1, layout.i64_numel)),
-                                    dtype=torch.int64, device=out64.device)
-        self.stack64 = torch.stack(local64, 0) if local64 else None
+        # int64 keys: every rank's buckets gathered raw; shards may be uneven,
+        # so each rank sends max-shard rows and only the real ones are used
+        nmax = -(-n_total // self.world)
+        width = max(1, layout.i64_numel)
+        self.gather64 = torch.zeros((self.world * nmax, width), dtype=torch.int64,
+                                    device=out64.device)
+        self.stack64 = torch.zeros((nmax, width), dtype=torch.int64, device=out64.device)
+        rows = []
+        for r in range(self.world):
+            lo, hi = shard_range(n_total, self.world, r)
+            rows += [r * nmax + j for j in range(hi - lo)]
+        self.rows64 = rows
 
     def step(self) -> None:
         works = []
@@ -132,11 +140,12 @@ class ShardedAggregator:
             works.append(dist.all_reduce(self.partial[lo:hi], op=dist.ReduceOp.SUM,
                                          group=self.group, async_op=True))
         if self.layout.i64_numel:
-            self.stack64.copy_(torch.stack(self.local64, 0))
+            for j, t in enumerate(self.local64):
+                self.stack64[j].copy_(t)
             works.append(dist.all_gather_into_tensor(self.gather64, self.stack64,
                                                      group=self.group, async_op=True))
         for w in works:
             w.wait()
         self.backend.divide(self.partial, float(self.n_total), self.out32)
         if self.layout.i64_numel:
-            self.backend.reduce_i64(list(self.gather64.unbind(0)), self.out64)
+            self.backend.reduce_i64([self.gather64[r] for r in self.rows64], self.out64)

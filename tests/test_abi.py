@@ -1,0 +1,94 @@
+"""C-ABI library: loads, exports every symbol include/fedagg.h declares, and
+the host-side paths (argument checks, tile planning) behave without a GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, load_manifest
+from feddct_amd import _lib
+from feddct_amd.layout import BucketLayout
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "fedagg.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fa_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_every_declared_symbol_is_exported():
+    fns = header_functions()
+    assert len(fns) >= 15
+    so = ctypes.CDLL(_lib.LIB_PATH)
+    for f in fns:
+        assert hasattr(so, f), f"{f} declared in include/fedagg.h but not exported"
+    assert set(fns) == set(_lib.EXPORTS), "python binding table out of sync with the header"
+
+
+def test_version_and_error_paths():
+    assert "gfx950" in _lib.version()
+    L = _lib.lib
+    assert L.fa_plan_create(None, 0, 0, None, 0, 0, 0, 0, None) == _lib.FA_E_INVAL
+    assert b"NULL" in L.fa_last_error()
+    segs, n = _lib.seg_array(np.array([[0, 10], [5, 10]], np.int64))
+    h = ctypes.c_void_p()
+    assert L.fa_plan_create(segs, n, 20, None, 0, 0, 0, 0, ctypes.byref(h)) == _lib.FA_E_INVAL
+    assert b"overlap" in L.fa_last_error()
+    segs, n = _lib.seg_array(np.array([[0, 30]], np.int64))
+    assert L.fa_plan_create(segs, n, 20, None, 0, 0, 0, 0, ctypes.byref(h)) == _lib.FA_E_INVAL
+    assert L.fa_plan_create(segs, n, 64, None, 0, 0, 3000, 0, ctypes.byref(h)) == _lib.FA_E_INVAL
+    assert L.fa_reduce(None, None, None, 1, None, None, None, 0, None) == _lib.FA_E_INVAL
+    assert L.fa_div_f32(None, 2.0, None, 0, None) == _lib.FA_OK
+    assert L.fa_div_f32(None, 2.0, None, 5, None) == _lib.FA_E_INVAL
+    assert L.fa_broadcast_f32(None, None, 5000, 10, None) == _lib.FA_E_RANGE
+    with pytest.raises(_lib.FedaggError, match="overlap"):
+        _lib.build_tiles_host(np.array([[0, 10], [5, 10]]), 20)
+
+
+def _expected_kind(M, col):
+    """Which torch order an element uses (oracle column rule)."""
+    if M == 1:
+        return "inner"
+    b = (M // 32) * 32 if M >= 8 else (M // 4) * 4
+    return "cascade" if col < b else "ilp4"
+
+
+KIND_NAME = {0: "cascade", 1: "cascade", 2: "ilp4", 3: "inner", 4: "cascade", 5: "ilp4", 6: "inner"}
+
+
+@pytest.mark.parametrize("lay", ["wrn16_8_c10", "wrnsl16_8_sf4_c100_main",
+                                 "wrnsl16_8_sf4_c100_proxy"])
+@pytest.mark.parametrize("tile", [1024, 2048, 4096])
+def test_tiles_partition_every_key_with_the_right_order(lay, tile):
+    L = BucketLayout.from_manifest(load_manifest(lay))
+    info, tiles = _lib.build_tiles_host(L.segs32, L.f32_numel, L.segs64, L.i64_numel, tile)
+    assert info["ntiles"] == len(tiles)
+    cover32 = np.full(L.f32_numel, "", dtype=object)
+    cover64 = np.full(max(1, L.i64_numel), "", dtype=object)
+    for start, count, kind in tiles:
+        assert 1 <= count <= (tile if kind == 0 else 256)
+        tgt = cover64 if kind >= 4 else cover32
+        assert (tgt[start:start + count] == "").all(), "tiles overlap"
+        tgt[start:start + count] = KIND_NAME[kind]
+        if kind == 0:
+            assert start % 4 == 0 and count % 4 == 0
+    for o, M in L.segs32:
+        for col in range(M):
+            assert cover32[o + col] == _expected_kind(M, col), (lay, o, M, col)
+    for o, M in L.segs64:
+        for col in range(M):
+            assert cover64[o + col] == _expected_kind(M, col)
+
+
+def test_stateless_plans_never_cover_gaps():
+    segs = np.array([[0, 100], [128, 64], [200, 33]], np.int64)
+    info, tiles = _lib.build_tiles_host(segs, 256, flags=0)
+    covered = np.zeros(256, bool)
+    for s, c, k in tiles:
+        covered[s:s + c] = True
+    want = np.zeros(256, bool)
+    for o, m in segs:
+        want[o:o + m] = True
+    assert np.array_equal(covered, want)

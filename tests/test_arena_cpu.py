@@ -1,0 +1,102 @@
+"""Arena binding and the shim's host-side checks (no GPU needed)."""
+import numpy as np
+import pytest
+import torch
+
+from feddct_amd.arena import ModuleArena, get_arena, state_owners
+from feddct_amd.layout import BucketLayout
+
+
+def net():
+    return torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8),
+                               torch.nn.Linear(5, 2))
+
+
+def test_binding_keeps_values_and_parameter_objects():
+    m = net()
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    params = list(m.parameters())
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    L = BucketLayout.from_state_dict(m.state_dict())
+    a = ModuleArena(m, L)
+    assert a.valid()
+    assert [id(p) for p in m.parameters()] == [id(p) for p in params]
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k])
+        s = L.by_key[k]
+        bucket = a.i64 if s.kind == "i64" else a.f32
+        assert v.data_ptr() == bucket[s.offset:].data_ptr()
+    # training writes land in the bucket
+    loss = m[2](torch.randn(4, 5)).sum()
+    loss.backward()
+    opt.step()
+    s = L.by_key["2.weight"]
+    assert torch.equal(a.f32[s.offset:s.offset + s.numel].view(s.shape), m[2].weight.detach())
+
+
+def test_rebind_detection():
+    m = net()
+    L = BucketLayout.from_state_dict(m.state_dict())
+    a = get_arena(m, L)
+    assert get_arena(m, L) is a
+    m[0].weight = torch.nn.Parameter(torch.zeros_like(m[0].weight))
+    assert not a.valid()
+    b = get_arena(m, L)
+    assert b is not a and b.valid()
+    assert torch.equal(m[0].weight.detach(), torch.zeros_like(m[0].weight))
+
+
+def test_arena_errors_like_reference():
+    m = net()
+    L = BucketLayout.from_state_dict(m.state_dict())
+    other = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3))
+    with pytest.raises(KeyError):
+        ModuleArena(other, L)
+    wrong = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 5), torch.nn.BatchNorm2d(8),
+                                torch.nn.Linear(5, 2))
+    w0 = wrong[0].weight.data_ptr()
+    with pytest.raises(RuntimeError, match="equal size"):
+        ModuleArena(wrong, L)
+    assert wrong[0].weight.data_ptr() == w0, "a failed bind must not touch the module"
+    half = net().half()
+    with pytest.raises(TypeError):
+        ModuleArena(half, L)
+    bigger = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8),
+                                 torch.nn.Linear(5, 2), torch.nn.Linear(2, 2))
+    a = ModuleArena(bigger, L)
+    assert a.extra_keys == ["3.weight", "3.bias"]
+
+
+def test_state_owners_order_matches_state_dict():
+    m = net()
+    assert list(state_owners(m).keys()) == list(m.state_dict().keys())
+
+
+def test_pack_unpack_roundtrip_dtypes():
+    m = torch.nn.Module()
+    m.register_buffer("h", torch.tensor([1.5, -2.25], dtype=torch.float16))
+    m.register_buffer("b", torch.tensor([True, False]))
+    m.register_buffer("i", torch.tensor([7, -3], dtype=torch.int32))
+    L = BucketLayout.from_state_dict(m.state_dict())
+    a = ModuleArena(m, L)
+    a.pack()
+    for k in ("h", "b", "i"):
+        s = L.by_key[k]
+        assert torch.equal(a.f32[s.offset:s.offset + s.numel], m.state_dict()[k].float())
+    s = L.by_key["i"]
+    a.f32[s.offset:s.offset + s.numel] = torch.tensor([2.9, -2.9])
+    a.unpack()
+    assert m.i.tolist() == [2, -2]  # copy_ float -> int truncates
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+def test_no_cpu_fallback():
+    from feddct_amd.aggregate import server_aggregate
+    with pytest.raises(RuntimeError, match="no CPU fallback|no HIP device"):
+        server_aggregate(net(), [net(), net()])
+
+
+def test_empty_client_list_like_torch_stack():
+    from feddct_amd.aggregate import server_aggregate
+    with pytest.raises(RuntimeError, match="non-empty"):
+        server_aggregate(net(), [])

@@ -1,0 +1,130 @@
+"""Multi-GPU orchestration (feddct_amd/dist.py) rehearsed on CPU with gloo,
+world_size 2 and 3: the arithmetic backends are the oracle, the exchange is
+real torch.distributed.  Checks chunking at key boundaries, the cross-rank
+sum, the /N_total finish and the exact int64 path."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from feddct_amd import synth
+from feddct_amd.dist import ShardedAggregator, chunk_segments, shard_range
+from feddct_amd.layout import BucketLayout
+from oracle import torch_order as O
+
+MAN = {"keys": [{"key": f"k{j}", "shape": [m], "dtype": "float32"}
+                for j, m in enumerate([100, 4096, 33, 2048, 7, 1, 5000])]
+       + [{"key": "nbt", "shape": [], "dtype": "int64"},
+          {"key": "nbt2", "shape": [], "dtype": "int64"}]}
+
+
+class OracleBackend:
+    def __init__(self, layout, chunks):
+        self.layout, self.chunks = layout, chunks
+
+    def partial_sum(self, c, clients32, out):
+        segs, _, _ = self.chunks[c]
+        for o, m in segs:
+            x = np.stack([t[o:o + m].numpy() for t in clients32])
+            out[o:o + m] = torch.from_numpy(O.torch_sum0(x))
+
+    def divide(self, x, d, out):
+        out.copy_(torch.from_numpy((x.numpy() / np.float32(d)).astype(np.float32)))
+
+    def reduce_i64(self, clients64, out):
+        for o, m in self.layout.segs64:
+            x = np.stack([t[o:o + m].numpy() for t in clients64])
+            out[o:o + m] = torch.from_numpy(O.mean_i64_trunc(x))
+
+
+def _bucket(layout, state):
+    f32 = torch.zeros(layout.f32_numel)
+    i64 = torch.zeros(max(1, layout.i64_numel), dtype=torch.int64)
+    for k, v in state:
+        s = layout.by_key[k]
+        tgt = i64 if s.kind == "i64" else f32
+        tgt[s.offset:s.offset + s.numel] = torch.from_numpy(np.array(v, copy=True)).reshape(-1)
+    return f32, i64
+
+
+def _worker(rank, world, port, n_total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    layout = BucketLayout.from_manifest(MAN)
+    lo, hi = shard_range(n_total, world, rank)
+    bk = [_bucket(layout, synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL)) for c in range(lo, hi)]
+    out32 = torch.zeros(layout.f32_numel)
+    out64 = torch.zeros(max(1, layout.i64_numel), dtype=torch.int64)
+    chunks = chunk_segments(layout, 3)
+    agg = ShardedAggregator(layout, [b[0] for b in bk], [b[1] for b in bk], n_total, out32,
+                            out64, nchunks=3, backend=OracleBackend(layout, chunks))
+    agg.step()
+    # what each rank contributed, to rebuild the expected cross-rank sum
+    part = torch.zeros(layout.f32_numel)
+    for c in range(len(chunks)):
+        OracleBackend(layout, chunks).partial_sum(c, [b[0] for b in bk], part)
+    parts = [torch.zeros_like(part) for _ in range(world)]
+    dist.all_gather(parts, part)
+    if rank == 0:
+        q.put((out32.numpy().copy(), out64.numpy().copy(), [p.numpy() for p in parts]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,n_total", [(2, 20), (3, 7)])
+def test_sharded_round_gloo(world, n_total):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out32, out64, parts = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    layout = BucketLayout.from_manifest(MAN)
+    states = [synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL) for c in range(n_total)]
+    exact = dict(O.aggregate_state(states))
+    # int64 keys: raw all-gather + exact reduction == single-process reference
+    for k in ("nbt", "nbt2"):
+        s = layout.by_key[k]
+        assert out64[s.offset] == exact[k][()]
+    # fp32: exact within shards, summed across ranks, then /N_total
+    tot = parts[0].copy()
+    for p in parts[1:]:
+        tot = (tot + p).astype(np.float32)
+    want = (tot / np.float32(n_total)).astype(np.float32)
+    for o, m in layout.segs32:
+        if world == 2:  # a two-term sum is order-free: the exchange is exactly p0 + p1
+            assert np.array_equal(out32[o:o + m].view(np.uint32), want[o:o + m].view(np.uint32))
+        # and within the re-association error bound of the exact order:
+        # |err| <= 2 N eps mean|x_i| (N-term fp32 summation, both orders)
+        key = layout.slots[[s.offset for s in layout.slots].index(o)].key
+        mag = np.mean(np.abs(np.stack([dict(st)[key].reshape(-1) for st in states])), 0)
+        err = np.abs(out32[o:o + m].astype(np.float64) - exact[key].reshape(-1))
+        assert (err <= 2 * n_total * 2.0 ** -24 * mag + 1e-38).all()
+
+
+def test_shard_range_and_chunks():
+    assert [shard_range(20, 8, r) for r in range(8)] == [(0, 3), (3, 6), (6, 9), (9, 12),
+                                                          (12, 14), (14, 16), (16, 18), (18, 20)]
+    layout = BucketLayout.from_manifest(MAN)
+    ch = chunk_segments(layout, 3)
+    assert 1 <= len(ch) <= 3
+    assert ch[0][1] == 0 and ch[-1][2] == layout.f32_numel
+    for (a, _, hi), (b, lo, _) in zip(ch, ch[1:]):
+        assert hi == lo
+    assert sum(len(c[0]) for c in ch) == len(layout.segs32)
