@@ -273,8 +273,11 @@ def main():
         agg = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
                                 N_CLIENTS * world, out32, out64, nchunks=args.chunks)
         t_step, wall = timed_launches(agg.step, args.steps, args.warmup, sync_group=group)
-        # kernel-only launch time for the roofline (same kernel, SUM_ONLY)
-        t_kernel, _ = timed_launches(reducer, max(10, args.steps // 2), 3)
+        # kernel-only launch time for the roofline: the same reduce over this
+        # rank's clients into scratch outputs (out32/out64 hold the round's result)
+        kred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
+                       flags=_lib.FA_F_SUM_ONLY, plan=reducer.plan)
+        t_kernel, _ = timed_launches(kred, max(10, args.steps // 2), 3)
         tt = torch.tensor([t_step], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_step = float(tt.item())
