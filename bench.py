@@ -193,6 +193,55 @@ def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
     return {"GBps": round(nbytes / t / 1e9, 2), "ms": round(t * 1e3, 3), "source": "pinned"}
 
 
+def _holder_class(layout):
+    class Holder(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            for s in layout.slots:
+                parts = s.key.split(".")
+                mod = self
+                for p in parts[:-1]:
+                    if p not in mod._modules:
+                        mod.add_module(p, torch.nn.Module())
+                    mod = mod._modules[p]
+                t = torch.zeros(s.shape, dtype=s.dtype)
+                if s.dtype == torch.int64:
+                    mod.register_buffer(parts[-1], t)
+                else:
+                    mod.register_parameter(parts[-1], torch.nn.Parameter(t))
+    return Holder
+
+
+def dropin_timing(layout, clients, dev, reps=20):
+    """Wall time of the drop-in ``server_aggregate(global, clients)`` on
+    nn.Modules with the wrn16_8 state_dict (arena validation + one fused
+    reduce/broadcast launch + stream sync), as the round loop would call it."""
+    from feddct_amd.aggregate import server_aggregate
+    Holder = _holder_class(layout)
+    mods = []
+    for f32, i64 in clients:
+        m = Holder().to(dev)
+        sd = m.state_dict()
+        with torch.no_grad():
+            for s in layout.slots:
+                src = i64 if s.kind == "i64" else f32
+                sd[s.key].copy_(src[s.offset:s.offset + s.numel].view(s.shape))
+        mods.append(m)
+    g = Holder().to(dev)
+    server_aggregate(g, mods)  # first call binds the arenas
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        server_aggregate(g, mods)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    t = ts[len(ts) // 2]
+    return {"server_aggregate_ms": round(t * 1e3, 3),
+            "note": "median wall incl. Python shim, arena checks, fused reduce+broadcast, sync"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,6 +317,7 @@ def main():
                             flags=_lib.FA_F_BCAST, plan=reducer.plan)
             tb, _ = timed_launches(fused, max(10, args.steps // 2), 3)
             extra["round_with_fused_broadcast_us"] = round(tb * 1e6, 1)
+            extra["dropin"] = dropin_timing(layout, clients, dev)
     else:
         from feddct_amd.dist import ShardedAggregator
         agg = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
