@@ -114,21 +114,7 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
 
-    class Holder(torch.nn.Module):
-        def __init__(self):
-            super().__init__()
-            for s in layout.slots:
-                parts = s.key.split(".")
-                mod = self
-                for p in parts[:-1]:
-                    if p not in mod._modules:
-                        mod.add_module(p, torch.nn.Module())
-                    mod = mod._modules[p]
-                t = torch.zeros(s.shape, dtype=s.dtype)
-                if s.dtype == torch.int64:
-                    mod.register_buffer(parts[-1], t)
-                else:
-                    mod.register_parameter(parts[-1], torch.nn.Parameter(t))
+    Holder = _holder_class(layout)
 
     def to_module(f32, i64):
         m = Holder()
@@ -169,28 +155,53 @@ def _cpu_model():
 
 
 def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
-    """Pinned host buckets -> H2D (N·B) -> kernel -> D2H (B), one stream."""
+    """Client buckets in pinned host memory, result back to host.
+    serial:    H2D of N·B, one kernel, D2H of B, one stream;
+    pipelined: feddct_amd/pipeline.py (8 column chunks, H2D / reduce / D2H
+               overlapped on two copy streams), result to the global only,
+               and with the broadcast (D2H into all N client buckets too)."""
+    from feddct_amd.pipeline import HostPipeline
+    n = len(clients)
     host = [(c[0].cpu().pin_memory(), c[1].cpu().pin_memory()) for c in clients]
     out_h32 = torch.empty_like(out32, device="cpu").pin_memory()
     out_h64 = torch.empty_like(out64, device="cpu").pin_memory()
+    nbytes = layout.algorithmic_bytes(n)
 
-    def step():
+    def serial():
         for (h32, h64), (d32, d64) in zip(host, clients):
             d32.copy_(h32, non_blocking=True)
             d64.copy_(h64, non_blocking=True)
         reducer_dev()
         out_h32.copy_(out32, non_blocking=True)
         out_h64.copy_(out64, non_blocking=True)
+        torch.cuda.synchronize()
 
-    step()
+    pipe = HostPipeline(layout, n, out32.device)
+    h32 = [h[0] for h in host]
+    h64 = [h[1] for h in host]
+
+    def piped():
+        pipe.run(h32, h64, out_h32, out_h64)
+
+    def piped_bcast():
+        pipe.run(h32, h64, out_h32, out_h64, h32, h64)
+
+    res = {"source": "pinned", "algorithmic_bytes": nbytes}
+    # the pipelined result is the same bits as the device-resident one
+    reducer_dev()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        step()
-    torch.cuda.synchronize()
-    t = (time.perf_counter() - t0) / reps
-    nbytes = layout.algorithmic_bytes(len(clients))
-    return {"GBps": round(nbytes / t / 1e9, 2), "ms": round(t * 1e3, 3), "source": "pinned"}
+    piped()
+    res["pipelined_bit_exact"] = bool(torch.equal(out_h32, out32.cpu()) and
+                                      torch.equal(out_h64, out64.cpu()))
+    for name, fn in (("serial", serial), ("pipelined", piped),
+                     ("pipelined_with_broadcast", piped_bcast)):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        t = (time.perf_counter() - t0) / reps
+        res[name] = {"ms": round(t * 1e3, 3), "GBps": round(nbytes / t / 1e9, 2)}
+    return res
 
 
 def _holder_class(layout):

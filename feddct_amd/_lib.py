@@ -30,7 +30,7 @@ FA_PLAN_TUNE_BATCH8 = 4
 
 EXPORTS = [
     "fa_version", "fa_last_error", "fa_plan_create", "fa_plan_destroy",
-    "fa_plan_get_info", "fa_plan_build_host", "fa_reduce", "fa_mean_f32", "fa_weighted_f32",
+    "fa_plan_get_info", "fa_plan_build_host", "fa_plan_create_from_tiles", "fa_reduce", "fa_mean_f32", "fa_weighted_f32",
     "fa_mean_i64_trunc", "fa_div_f32", "fa_div_trunc_i64", "fa_broadcast_f32",
     "fa_synth_fill_f32", "fa_synth_fill_i64", "fa_copy_f32",
 ]
@@ -75,6 +75,8 @@ def _load():
         "fa_plan_build_host": (_I, [_P, _I, _I64, _P, _I, _I64, _I, ctypes.c_uint, _P, _I,
                                     ctypes.POINTER(FaPlanInfo)]),
         "fa_plan_get_info": (_I, [_P, ctypes.POINTER(FaPlanInfo)]),
+        "fa_plan_create_from_tiles": (_I, [_P, _I, _I64, _I64, _I, ctypes.c_uint,
+                                           ctypes.POINTER(_P)]),
         "fa_reduce": (_I, [_P, _P, _P, _I, _P, _P, _P, ctypes.c_uint, _P]),
         "fa_mean_f32": (_I, [_P, _I, _I64, _P, _P, _I, _P]),
         "fa_weighted_f32": (_I, [_P, _P, _I, _I64, _P, _P, _I, _P]),
@@ -143,15 +145,25 @@ def build_tiles_host(segs32, f32_numel, segs64=(), i64_numel=0, tile_elems=0,
 
 
 class Plan:
-    """Owning wrapper of an ``fa_plan`` (device-resident tile table)."""
+    """Owning wrapper of an ``fa_plan`` (device-resident tile table); built
+    from a layout's segments, or from an explicit tile subset (``tiles``)."""
 
     def __init__(self, segs32, f32_numel, segs64=(), i64_numel=0, tile_elems=0,
-                 flags=FA_PLAN_GAPS_ARE_PADDING):
-        a32, n32 = seg_array(segs32 if len(segs32) else np.zeros((0, 2), np.int64))
-        a64, n64 = seg_array(segs64 if len(segs64) else np.zeros((0, 2), np.int64))
+                 flags=FA_PLAN_GAPS_ARE_PADDING, tiles=None):
         h = ctypes.c_void_p()
-        check(lib.fa_plan_create(a32, n32, int(f32_numel), a64, n64, int(i64_numel),
-                                 int(tile_elems), flags, ctypes.byref(h)), "fa_plan_create")
+        if tiles is not None:
+            tiles = np.asarray(tiles, np.int64).reshape(-1, 3)
+            arr = (FaTileDesc * max(1, len(tiles)))()
+            for i, (s, c, k) in enumerate(tiles):
+                arr[i].start, arr[i].count, arr[i].kind = int(s), int(c), int(k)
+            check(lib.fa_plan_create_from_tiles(arr, len(tiles), int(f32_numel), int(i64_numel),
+                                                int(tile_elems), flags, ctypes.byref(h)),
+                  "fa_plan_create_from_tiles")
+        else:
+            a32, n32 = seg_array(segs32 if len(segs32) else np.zeros((0, 2), np.int64))
+            a64, n64 = seg_array(segs64 if len(segs64) else np.zeros((0, 2), np.int64))
+            check(lib.fa_plan_create(a32, n32, int(f32_numel), a64, n64, int(i64_numel),
+                                     int(tile_elems), flags, ctypes.byref(h)), "fa_plan_create")
         self.handle = h
         info = FaPlanInfo()
         check(lib.fa_plan_get_info(h, ctypes.byref(info)), "fa_plan_get_info")

@@ -46,30 +46,13 @@ def _require_gpu():
                            "no CPU fallback")
 
 
-class _Staging:
-    """Device buckets for host-resident client state (host-inclusive path)."""
-
-    def __init__(self, layout: BucketLayout, device: torch.device):
-        self.layout = layout
-        self.device = device
-        self.c32: List[torch.Tensor] = []
-        self.c64: List[torch.Tensor] = []
-        self.out32 = torch.empty(max(layout.f32_numel, 64), dtype=torch.float32, device=device)
-        self.out64 = torch.empty(max(layout.i64_numel, 1), dtype=torch.int64, device=device)
-
-    def ensure(self, n: int):
-        while len(self.c32) < n:
-            self.c32.append(torch.empty_like(self.out32))
-            self.c64.append(torch.empty_like(self.out64))
-
-
 class Engine:
     """Plan/staging caches for one process (one GPU per process)."""
 
     def __init__(self):
         self._plans: Dict[tuple, _lib.Plan] = {}
-        self._staging: Dict[tuple, _Staging] = {}
         self._layouts: Dict[tuple, BucketLayout] = {}
+        self._pipes: Dict[tuple, object] = {}
 
     # ------------------------------------------------------------ caches --
     def plan(self, layout: BucketLayout, device: torch.device) -> _lib.Plan:
@@ -88,14 +71,6 @@ class Engine:
         lay = BucketLayout.from_state_dict(module.state_dict())
         # share one layout object per signature so plans/staging are reused
         return self._layouts.setdefault(lay.signature, lay)
-
-    def staging(self, layout: BucketLayout, device: torch.device, n: int) -> _Staging:
-        key = (layout.signature, device.index)
-        st = self._staging.get(key)
-        if st is None:
-            st = self._staging[key] = _Staging(layout, device)
-        st.ensure(n)
-        return st
 
     # ------------------------------------------------------------- core --
     def reduce_modules(self, global_model: torch.nn.Module,
@@ -165,25 +140,20 @@ class Engine:
                      self._weights_arg(weights, n), ga.ptr32, ga.ptr64, flags, ga.device)
 
     def _reduce_host(self, layout, ga: ModuleArena, cas: List[ModuleArena], weights, fuse):
-        """Host-resident state: pinned H2D of every client bucket, one kernel,
-        D2H of the result into the global and (broadcast) every client."""
+        """Host-resident state (the reference's CPU configuration): the
+        chunked H2D / reduce / D2H pipeline (pipeline.py) over the modules'
+        pinned arenas; the broadcast is part of the D2H stream."""
+        from .pipeline import HostPipeline
         n = len(cas)
         dev = torch.device("cuda", torch.cuda.current_device())
-        st = self.staging(layout, dev, n)
-        plan = self.plan(layout, dev)
-        for i, c in enumerate(cas):
-            st.c32[i].copy_(c.f32, non_blocking=True)
-            st.c64[i].copy_(c.i64, non_blocking=True)
-        self._launch(plan, layout, [t.data_ptr() for t in st.c32[:n]],
-                     [t.data_ptr() for t in st.c64[:n]], n, self._weights_arg(weights, n),
-                     st.out32.data_ptr(), st.out64.data_ptr(), 0, dev)
-        ga.f32.copy_(st.out32, non_blocking=True)
-        ga.i64.copy_(st.out64, non_blocking=True)
-        if fuse:
-            for c in cas:
-                c.f32.copy_(st.out32, non_blocking=True)
-                c.i64.copy_(st.out64, non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
+        key = (layout.signature, dev.index, n)
+        pipe = self._pipes.get(key)
+        if pipe is None:
+            pipe = self._pipes[key] = HostPipeline(layout, n, dev)
+        bc32 = [c.f32 for c in cas] if fuse else []
+        bc64 = [c.i64 for c in cas] if fuse else []
+        pipe.run([c.f32 for c in cas], [c.i64 for c in cas], ga.f32, ga.i64, bc32, bc64,
+                 weights=None if weights is None else np.asarray(weights, np.float32))
 
 
 _ENGINE: Optional[Engine] = None

@@ -687,6 +687,67 @@ int fa_plan_build_host(const fa_seg* seg32, int nseg32, int64_t f32_numel, const
   return FA_OK;
 }
 
+int fa_plan_create_from_tiles(const fa_tile_desc* tiles, int ntiles, int64_t f32_numel,
+                              int64_t i64_numel, int tile_elems, unsigned flags,
+                              fa_plan** out) {
+  if (!out) return set_err(FA_E_INVAL, "fa_plan_create_from_tiles: out is NULL");
+  *out = nullptr;
+  if (ntiles < 0 || (ntiles > 0 && !tiles))
+    return set_err(FA_E_INVAL, "fa_plan_create_from_tiles: bad tile array");
+  if (tile_elems == 0) tile_elems = 4 * kBlock * kDefaultU;
+  if (tile_elems != 4 * kBlock && tile_elems != 8 * kBlock && tile_elems != 16 * kBlock)
+    return set_err(FA_E_INVAL, "tile_elems must be 1024, 2048 or 4096 (got %d)", tile_elems);
+  std::vector<Tile> t(ntiles);
+  fa_plan_info in{};
+  in.f32_numel = f32_numel;
+  in.i64_numel = i64_numel;
+  in.tile_elems = tile_elems;
+  std::vector<Tile> vec, sc;
+  for (int i = 0; i < ntiles; ++i) {
+    const fa_tile_desc& d = tiles[i];
+    const bool is64 = d.kind >= K_I64_CASC;
+    const int64_t lim = is64 ? i64_numel : f32_numel;
+    if (d.kind < K_F32_VEC || d.kind > K_I64_INNER || d.count < 1 || d.start < 0 ||
+        d.start + d.count > lim)
+      return set_err(FA_E_INVAL, "tile %d: kind %d [%lld,+%d) invalid", i, d.kind,
+                     (long long)d.start, d.count);
+    if (d.kind == K_F32_VEC) {
+      if (d.start % 4 || d.count % 4 || d.count > tile_elems)
+        return set_err(FA_E_INVAL, "tile %d: vector tile must be 4-aligned and <= %d", i,
+                       tile_elems);
+      vec.push_back(Tile{d.start, d.count, d.kind});
+      in.cascade_elems += d.count;
+    } else {
+      if (d.count > kBlock) return set_err(FA_E_INVAL, "tile %d: scalar tile > %d", i, kBlock);
+      sc.push_back(Tile{d.start, d.count, d.kind});
+      if (!is64) in.tail_elems += d.count;
+    }
+  }
+  t.clear();
+  t.insert(t.end(), sc.begin(), sc.end());
+  t.insert(t.end(), vec.begin(), vec.end());
+  in.ntiles = (int32_t)t.size();
+  in.ntiles_cascade = (int32_t)vec.size();
+  in.ntiles_tail = (int32_t)sc.size();
+  fa_plan* p = new fa_plan();
+  p->info = in;
+  p->vec_u = tile_elems / (4 * kBlock);
+  p->flags = flags;
+  hipError_t e = hipGetDevice(&p->device);
+  if (e == hipSuccess && !t.empty()) {
+    e = hipMalloc(&p->d_tiles, t.size() * sizeof(Tile));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_tiles, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    if (p->d_tiles) (void)hipFree(p->d_tiles);
+    delete p;
+    return set_err(FA_E_HIP, "fa_plan_create_from_tiles: %s", hipGetErrorString(e));
+  }
+  *out = p;
+  return FA_OK;
+}
+
 int fa_plan_destroy(fa_plan* plan) {
   if (!plan) return FA_OK;
   if (plan->d_tiles) HIP_TRY(hipFree(plan->d_tiles));

@@ -1,0 +1,102 @@
+"""Host-ingress / egress pipeline for one GPU.
+
+Client updates arrive in (pinned) host memory and the global model goes back
+out: the round is PCIe-bound, not HBM-bound.  The bucket is cut into column
+chunks (partition.range_plans); per chunk
+
+    copy stream A : H2D of the chunk of every client bucket
+    compute       : waits for A's event, reduces the chunk (exact order)
+    copy stream B : waits for the kernel, D2H of the chunk of the result
+                    into the global's host bucket and every broadcast target
+
+so chunk c+1's upload, chunk c's reduction and chunk c-1's download overlap
+(PCIe Gen5 is full duplex; the kernel is <1 % of the round).  Results are
+bit-identical to the one-shot path: each chunk is a tile subset.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _lib
+from .layout import BucketLayout
+from .partition import range_plans
+
+
+class HostPipeline:
+    def __init__(self, layout: BucketLayout, n: int, device: torch.device, nchunks: int = 8,
+                 tile_elems: int = 0):
+        self.layout = layout
+        self.device = device
+        with torch.cuda.device(device):
+            self.ranges, self.plan64 = range_plans(layout, nchunks, tile_elems)
+            self.dev32 = [torch.empty(max(layout.f32_numel, 64), dtype=torch.float32,
+                                      device=device) for _ in range(n)]
+            self.dev64 = [torch.empty(max(layout.i64_numel, 1), dtype=torch.int64,
+                                      device=device) for _ in range(n)]
+            self.out32 = torch.empty_like(self.dev32[0])
+            self.out64 = torch.empty_like(self.dev64[0])
+            self.s_in = torch.cuda.Stream(device)
+            self.s_out = torch.cuda.Stream(device)
+        self.n = n
+        self.a32 = _lib.ptr_array([t.data_ptr() for t in self.dev32])
+        self.a64 = _lib.ptr_array([t.data_ptr() for t in self.dev64])
+
+    def run(self, host32: Sequence[torch.Tensor], host64: Sequence[torch.Tensor],
+            out_host32: torch.Tensor, out_host64: torch.Tensor,
+            bcast32: Sequence[torch.Tensor] = (), bcast64: Sequence[torch.Tensor] = (),
+            weights=None) -> None:
+        """One round.  ``host*`` are the clients' host buckets (slot order),
+        ``out_host*`` the global's, ``bcast*`` extra host buckets that receive
+        the result (the broadcast).  Returns after the result is in host
+        memory."""
+        n = len(host32)
+        if n != self.n:
+            raise ValueError(f"pipeline built for {self.n} clients, got {n}")
+        compute = torch.cuda.current_stream(self.device)
+        w = None if weights is None else (ctypes.c_float * n)(*map(float, weights))
+        # buffers of the previous round are free once its work is done
+        self.s_in.wait_stream(compute)
+        self.s_in.wait_stream(self.s_out)
+        compute.wait_stream(self.s_out)
+        ev_in = []
+        with torch.cuda.stream(self.s_in):
+            if self.plan64 is not None:
+                for i in range(n):
+                    self.dev64[i].copy_(host64[i], non_blocking=True)
+            for lo, hi, _ in self.ranges:
+                if hi > lo:
+                    for i in range(n):
+                        self.dev32[i][lo:hi].copy_(host32[i][lo:hi], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.s_in)
+                ev_in.append(ev)
+        stream = ctypes.c_void_p(compute.cuda_stream)
+        for c, (lo, hi, plan) in enumerate(self.ranges):
+            compute.wait_event(ev_in[c])
+            if plan is not None:
+                _lib.check(_lib.lib.fa_reduce(plan.handle, self.a32, self.a64, n, w,
+                                              self.out32.data_ptr(), self.out64.data_ptr(), 0,
+                                              stream), "fa_reduce(chunk)")
+            ev = torch.cuda.Event()
+            ev.record(compute)
+            self.s_out.wait_event(ev)
+            if hi > lo:
+                with torch.cuda.stream(self.s_out):
+                    out_host32[lo:hi].copy_(self.out32[lo:hi], non_blocking=True)
+                    for t in bcast32:
+                        t[lo:hi].copy_(self.out32[lo:hi], non_blocking=True)
+        if self.plan64 is not None:
+            _lib.check(_lib.lib.fa_reduce(self.plan64.handle, self.a32, self.a64, n, None,
+                                          self.out32.data_ptr(), self.out64.data_ptr(), 0,
+                                          stream), "fa_reduce(int64)")
+            ev = torch.cuda.Event()
+            ev.record(compute)
+            self.s_out.wait_event(ev)
+            with torch.cuda.stream(self.s_out):
+                out_host64.copy_(self.out64, non_blocking=True)
+                for t in bcast64:
+                    t.copy_(self.out64, non_blocking=True)
+        self.s_out.synchronize()

@@ -121,6 +121,14 @@ int fa_plan_build_host(const fa_seg *seg32, int nseg32, int64_t f32_numel,
                        int cap, fa_plan_info *info);
 int fa_plan_get_info(const fa_plan *plan, fa_plan_info *info);
 
+/* A plan over an explicit subset of a layout's tiles (as returned by
+ * fa_plan_build_host): the unit of column-striped work — a GPU's stripe in the
+ * exact multi-GPU mode, a chunk of the host-ingress pipeline.  Every tile keeps
+ * the order its column needs, so any tile subset reduces bit-exactly. */
+int fa_plan_create_from_tiles(const fa_tile_desc *tiles, int ntiles,
+                              int64_t f32_numel, int64_t i64_numel,
+                              int tile_elems, unsigned flags, fa_plan **out);
+
 /* The hot path: every key of N client buckets -> global bucket, one launch.
  *   c32[i] / c64[i]  : client i's fp32 / int64 bucket (slot order 0..n-1)
  *   weights          : NULL -> mean (sum / n);  else fp32 w[i], result =

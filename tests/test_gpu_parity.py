@@ -393,3 +393,55 @@ def _full_case(lib, lay_name, n, device=DEV):
 def test_full_size_digest_vs_reference(lib, golden, case):
     _, lay, nn = case.split("/")
     assert _full_case(lib, lay, int(nn[1:])) == golden["digests"][case]
+
+
+# ------------------------------------------- partitions and host pipeline --
+@pytest.mark.parametrize("parts", [1, 3, 8, 64])
+def test_range_plans_union_is_bit_exact(lib, parts):
+    from feddct_amd.partition import range_plans
+    man = load_manifest("wrnsl16_8_sf4_c10_proxy")
+    layout = BucketLayout.from_manifest(man)
+    from feddct_amd.workload import make_clients
+    n = 7
+    cl = make_clients(layout, man, range(n), DEV, synth.MODE_ADVERSARIAL)
+    full32, full64 = _reduce(lib, layout, cl)
+    ranges, p64 = range_plans(layout, parts)
+    out32 = torch.full_like(full32, np.nan)
+    out64 = torch.full_like(full64, -1)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    a32 = lib.ptr_array([c[0].data_ptr() for c in cl])
+    a64 = lib.ptr_array([c[1].data_ptr() for c in cl])
+    for lo, hi, plan in ranges:
+        if plan is not None:
+            lib.check(lib.lib.fa_reduce(plan.handle, a32, a64, n, None, out32.data_ptr(),
+                                        out64.data_ptr(), 0, stream))
+    lib.check(lib.lib.fa_reduce(p64.handle, a32, a64, n, None, out32.data_ptr(),
+                                out64.data_ptr(), 0, stream))
+    torch.cuda.synchronize()
+    for s in layout.slots:
+        if s.kind == "i64":
+            assert torch.equal(out64[s.offset:s.offset + s.numel], full64[s.offset:s.offset + s.numel])
+        else:
+            a = out32[s.offset:s.offset + s.numel].cpu().numpy()
+            b = full32[s.offset:s.offset + s.numel].cpu().numpy()
+            assert bits_equal(a, b), s.key
+
+
+def test_host_pipeline_bit_exact_with_broadcast(lib):
+    from feddct_amd.pipeline import HostPipeline
+    from feddct_amd.workload import make_clients
+    man = load_manifest("wrn16_8_c10")
+    layout = BucketLayout.from_manifest(man)
+    n = 5
+    cl = make_clients(layout, man, range(n), DEV)
+    full32, full64 = _reduce(lib, layout, cl)
+    h32 = [c[0].cpu().pin_memory() for c in cl]
+    h64 = [c[1].cpu().pin_memory() for c in cl]
+    o32 = torch.zeros_like(h32[0]).pin_memory()
+    o64 = torch.zeros_like(h64[0]).pin_memory()
+    pipe = HostPipeline(layout, n, DEV, nchunks=6)
+    for _ in range(2):  # second round reuses the device buffers
+        pipe.run(h32, h64, o32, o64)
+        assert torch.equal(o32, full32.cpu()) and torch.equal(o64, full64.cpu())
+    pipe.run(h32, h64, o32, o64, h32[1:3], h64[1:3])
+    assert torch.equal(h32[2], full32.cpu()) and torch.equal(h64[1], full64.cpu())
