@@ -11,6 +11,12 @@ import os
 
 import numpy as np
 
+# torch first: libfedagg.so must bind to the SAME HIP runtime as PyTorch-ROCm
+# (torch ships its own libamdhip64.so.7).  Loaded the other way round the
+# process ends up with two runtimes and torch's stream handles / device
+# pointers are not valid in ours ("no ROCm-capable device").
+import torch  # noqa: F401  (load order)
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfedagg.so")
 
