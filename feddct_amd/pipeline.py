@@ -36,8 +36,8 @@ class HostPipeline:
                                       device=device) for _ in range(n)]
             self.dev64 = [torch.empty(max(layout.i64_numel, 1), dtype=torch.int64,
                                       device=device) for _ in range(n)]
-            self.out32 = torch.empty_like(self.dev32[0])
-            self.out64 = torch.empty_like(self.dev64[0])
+            self.out32 = torch.zeros_like(self.dev32[0])
+            self.out64 = torch.zeros_like(self.dev64[0])
             self.s_in = torch.cuda.Stream(device)
             self.s_out = torch.cuda.Stream(device)
         self.n = n

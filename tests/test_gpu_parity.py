@@ -440,8 +440,13 @@ def test_host_pipeline_bit_exact_with_broadcast(lib):
     o32 = torch.zeros_like(h32[0]).pin_memory()
     o64 = torch.zeros_like(h64[0]).pin_memory()
     pipe = HostPipeline(layout, n, DEV, nchunks=6)
+    want = buckets_to_state(layout, full32, full64)
+
+    def same(b32, b64):
+        return all(bits_equal(a, b) for (_, a), (_, b) in
+                   zip(buckets_to_state(layout, b32, b64), want))
     for _ in range(2):  # second round reuses the device buffers
         pipe.run(h32, h64, o32, o64)
-        assert torch.equal(o32, full32.cpu()) and torch.equal(o64, full64.cpu())
+        assert same(o32, o64)
     pipe.run(h32, h64, o32, o64, h32[1:3], h64[1:3])
-    assert torch.equal(h32[2], full32.cpu()) and torch.equal(h64[1], full64.cpu())
+    assert same(h32[2], h64[2]) and same(h32[1], h64[1]) and same(o32, o64)
