@@ -260,6 +260,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-exact", action="store_true",
+                    help="N>1: skip timing the column-striped exact mode")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI); gloo only to rehearse ranks on one GPU")
@@ -342,6 +344,23 @@ def main():
         tt = torch.tensor([t_step], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_step = float(tt.item())
+        # the exact (column-striped) mode on the same client placement
+        striped = None
+        if not args.kernel_only and not args.no_exact:
+            from feddct_amd.dist import StripedAggregator
+            s32 = torch.zeros_like(out32)
+            s64 = torch.zeros_like(out64)
+            sagg = StripedAggregator(layout, N_CLIENTS * world, s32, s64, group=group)
+            lc32 = [c[0] for c in clients]
+            lc64 = [c[1] for c in clients]
+            ts, _ = timed_launches(lambda: sagg.step_device(lc32, lc64),
+                                   max(3, args.steps // 10), 2, sync_group=group)
+            tt = torch.tensor([ts], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            ts = float(tt.item())
+            striped = {"mode": "column-striped exact (grouped P2P stripe exchange over RCCL)",
+                       "ms_per_step": round(ts * 1e3, 3),
+                       "GBps": round(nbytes_rank * world / ts / 1e9, 2)}
         if rank == 0 and not args.kernel_only:
             # accuracy of the re-associated cross-GPU sum vs the exact order
             allc = make_clients(layout, manifest, range(N_CLIENTS * world), dev)
@@ -352,6 +371,9 @@ def main():
             extra["parity"] = {"vs": f"exact single-GPU torch order over {N_CLIENTS * world} clients",
                                "max_ulp_fp32": ulp_dist(out32, ex32),
                                "int64_bit_exact": bool(torch.equal(out64, ex64))}
+            if striped is not None:
+                striped["bit_exact"] = bool(torch.equal(s32, ex32) and torch.equal(s64, ex64))
+                extra["exact_mode"] = striped
             del allc
 
     achieved = nbytes_rank / t_kernel / 1e9

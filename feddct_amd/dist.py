@@ -149,3 +149,160 @@ class ShardedAggregator:
         self.backend.divide(self.partial, float(self.n_total), self.out32)
         if self.layout.i64_numel:
             self.backend.reduce_i64([self.gather64[r] for r in self.rows64], self.out64)
+
+
+# --------------------------------------------------------------------------
+# Exact mode: element (column) stripes.
+# --------------------------------------------------------------------------
+class HipStripeBackend:
+    """Stripe reduction with the HIP kernel over a tile-subset plan."""
+
+    def __init__(self, layout: BucketLayout, stripe_tiles, tiles64):
+        from . import _lib
+        self._lib = _lib
+        te = 0
+        self.plan = (_lib.Plan(None, layout.f32_numel, None, layout.i64_numel, te,
+                               tiles=stripe_tiles) if len(stripe_tiles) else None)
+        self.plan64 = (_lib.Plan(None, layout.f32_numel, None, layout.i64_numel, te,
+                                 tiles=tiles64) if len(tiles64) else None)
+
+    def reduce_stripe(self, sources, out32: torch.Tensor):
+        """``sources[k] = (tensor, base)``: client slot k's element e lives at
+        ``tensor[e - base]`` for e in this rank's stripe."""
+        if self.plan is None:
+            return
+        L = self._lib
+        ptrs = [t.data_ptr() - 4 * base for t, base in sources]
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        L.check(L.lib.fa_reduce(self.plan.handle, L.ptr_array(ptrs), None, len(ptrs), None,
+                                out32.data_ptr(), None, 0, s), "fa_reduce(stripe)")
+
+    def reduce_i64(self, clients64, out64: torch.Tensor):
+        if self.plan64 is None:
+            return
+        L = self._lib
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        L.check(L.lib.fa_reduce(self.plan64.handle, None,
+                                L.ptr_array([t.data_ptr() for t in clients64]), len(clients64),
+                                None, None, out64.data_ptr(), 0, s), "fa_reduce(i64)")
+
+
+class StripedAggregator:
+    """Bit-exact cross-GPU round: rank r owns the column stripe
+    [lo_r, hi_r) of the bucket (cut at vector-tile starts, partition.py), gets
+    every client's values for those columns, reduces them in the exact torch
+    order and the stripes are exchanged so every rank ends with the full
+    global state.  Two ingress forms:
+
+    * ``step_device(local32, local64)`` — client slots device-resident and
+      sharded by rank (as in ShardedAggregator): the stripes travel
+      rank-to-rank as grouped P2P send/recv over RCCL (n·B·(W-1)/W per rank:
+      the price of exactness on device-resident inputs);
+    * ``step_host(stripes32, clients64)`` — client updates in host memory:
+      each GPU uploads only ITS stripe of every client (no xGMI traffic for
+      inputs; ingress bandwidth scales with the GPUs' PCIe links).
+
+    The result is the same bits as the single-GPU reduction (tested).
+    """
+
+    def __init__(self, layout: BucketLayout, n_total: int, out32: torch.Tensor,
+                 out64: torch.Tensor, group=None, backend=None):
+        from .partition import i64_tiles, layout_tiles, split_tiles
+        self.layout = layout
+        self.n_total = n_total
+        self.out32, self.out64 = out32, out64
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        info, tiles = layout_tiles(layout)
+        parts = split_tiles(tiles, self.world, layout.f32_numel)
+        self.ranges = [(lo, hi) for lo, hi, _ in parts]
+        self.lo, self.hi = self.ranges[self.rank]
+        self.backend = backend or HipStripeBackend(layout, parts[self.rank][2], i64_tiles(tiles))
+        L = self.hi - self.lo
+        self.lpad = (L + 3) // 4 * 4
+        dev = out32.device
+        self.recv = torch.zeros((n_total, max(self.lpad, 4)), dtype=torch.float32, device=dev)
+        nmax = -(-n_total // self.world)
+        width = max(1, layout.i64_numel)
+        self.gather64 = torch.zeros((self.world * nmax, width), dtype=torch.int64, device=dev)
+        self.stack64 = torch.zeros((nmax, width), dtype=torch.int64, device=dev)
+        self.rows64 = []
+        self.shards = [shard_range(n_total, self.world, r) for r in range(self.world)]
+        for r, (a, b) in enumerate(self.shards):
+            self.rows64 += [r * nmax + j for j in range(b - a)]
+
+    def _peer(self, r):
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def _gather_stripes(self, ops):
+        """Every rank's stripe of out32 to every other rank (P2P into views)."""
+        me = self.rank
+        for r in range(self.world):
+            if r == me:
+                continue
+            lo, hi = self.ranges[r]
+            if self.hi > self.lo:
+                ops.append(dist.P2POp(dist.isend, self.out32[self.lo:self.hi], self._peer(r),
+                                      self.group))
+            if hi > lo:
+                ops.append(dist.P2POp(dist.irecv, self.out32[lo:hi], self._peer(r), self.group))
+
+    def _run(self, ops):
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+
+    def _i64(self, local64):
+        if not self.layout.i64_numel:
+            return
+        for j, t in enumerate(local64):
+            self.stack64[j].copy_(t)
+        dist.all_gather_into_tensor(self.gather64, self.stack64, group=self.group)
+        self.backend.reduce_i64([self.gather64[r] for r in self.rows64], self.out64)
+
+    def step_device(self, local32: List[torch.Tensor], local64: List[torch.Tensor]) -> None:
+        me = self.rank
+        a, b = self.shards[me]
+        assert len(local32) == b - a
+        ops = []
+        for r in range(self.world):
+            if r == me:
+                continue
+            lo, hi = self.ranges[r]
+            if hi > lo:
+                for t in local32:
+                    ops.append(dist.P2POp(dist.isend, t[lo:hi], self._peer(r), self.group))
+            qa, qb = self.shards[r]
+            if self.hi > self.lo:
+                for k in range(qa, qb):
+                    ops.append(dist.P2POp(dist.irecv, self.recv[k, :self.hi - self.lo],
+                                          self._peer(r), self.group))
+        self._run(ops)
+        sources = []
+        for k in range(self.n_total):
+            if a <= k < b:
+                sources.append((local32[k - a], 0))
+            else:
+                sources.append((self.recv[k], self.lo))
+        self.backend.reduce_stripe(sources, self.out32)
+        self._i64(local64)
+        ops = []
+        self._gather_stripes(ops)
+        self._run(ops)
+
+    def step_host(self, stripes32: Sequence[torch.Tensor], clients64: Sequence[torch.Tensor],
+                  local64: Optional[List[torch.Tensor]] = None) -> None:
+        """``stripes32[k]``: client slot k's values for THIS rank's columns
+        [lo, hi) (host, pinned), ``clients64[k]``: its int64 bucket."""
+        L = self.hi - self.lo
+        for k, t in enumerate(stripes32):
+            self.recv[k, :L].copy_(t, non_blocking=True)
+        self.backend.reduce_stripe([(self.recv[k], self.lo) for k in range(self.n_total)],
+                                   self.out32)
+        if self.layout.i64_numel:
+            g = torch.stack([t.to(self.out64.device, non_blocking=True) for t in clients64])
+            self.backend.reduce_i64(list(g.unbind(0)), self.out64)
+        ops = []
+        self._gather_stripes(ops)
+        self._run(ops)

@@ -128,3 +128,86 @@ def test_shard_range_and_chunks():
     for (a, _, hi), (b, lo, _) in zip(ch, ch[1:]):
         assert hi == lo
     assert sum(len(c[0]) for c in ch) == len(layout.segs32)
+
+
+# ------------------------------------------------ exact striped mode (e2) --
+class OracleStripeBackend:
+    """Per-column oracle over whatever columns a stripe holds: the order a
+    column needs depends only on its position inside its tensor."""
+
+    def __init__(self, layout, lo, hi):
+        self.layout, self.lo, self.hi = layout, lo, hi
+
+    def reduce_stripe(self, sources, out32):
+        n = len(sources)
+        for o, M in self.layout.segs32:
+            a, b = max(o, self.lo), min(o + M, self.hi)
+            if a >= b:
+                continue
+            x = np.stack([t[a - base:b - base].numpy() for t, base in sources])
+            body = O.body_len(M)
+            res = np.empty(b - a, np.float32)
+            for j, e in enumerate(range(a, b)):
+                col = [x[i, j:j + 1] for i in range(n)]
+                if M == 1:
+                    s = O.ilp4(col)[0] if n < 8 else O.inner8(x[:, j])
+                elif e - o < body:
+                    s = O.cascade(col)[0]
+                else:
+                    s = O.ilp4(col)[0]
+                res[j] = np.float32(np.float32(0) + np.float32(s)) / np.float32(n)
+            out32[a:b] = torch.from_numpy(res)
+
+    def reduce_i64(self, clients64, out):
+        for o, m in self.layout.segs64:
+            x = np.stack([t[o:o + m].numpy() for t in clients64])
+            out[o:o + m] = torch.from_numpy(O.mean_i64_trunc(x))
+
+
+def _striped_worker(rank, world, port, n_total, host, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from feddct_amd.dist import StripedAggregator
+    from feddct_amd.partition import layout_tiles, split_tiles
+    layout = BucketLayout.from_manifest(MAN)
+    out32 = torch.full((layout.f32_numel,), float("nan"))
+    out64 = torch.zeros(max(1, layout.i64_numel), dtype=torch.int64)
+    info, tiles = layout_tiles(layout)
+    lo, hi, _ = split_tiles(tiles, world, layout.f32_numel)[rank]
+    agg = StripedAggregator(layout, n_total, out32, out64,
+                            backend=OracleStripeBackend(layout, lo, hi))
+    if host:
+        allb = [_bucket(layout, synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL))
+                for c in range(n_total)]
+        agg.step_host([b[0][lo:hi].clone() for b in allb], [b[1] for b in allb])
+    else:
+        a, b = shard_range(n_total, world, rank)
+        bk = [_bucket(layout, synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL)) for c in range(a, b)]
+        agg.step_device([x[0] for x in bk], [x[1] for x in bk])
+    q.put((rank, out32.numpy().copy(), out64.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total,host", [(2, 20, False), (3, 7, False), (2, 9, True)])
+def test_striped_round_is_exact_gloo(world, n_total, host):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_striped_worker, args=(r, world, port, n_total, host, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    layout = BucketLayout.from_manifest(MAN)
+    states = [synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL) for c in range(n_total)]
+    exact = dict(O.aggregate_state(states))
+    for _, o32, o64 in res:  # every rank holds the full, exact global state
+        for s in layout.slots:
+            src = o64 if s.kind == "i64" else o32
+            got = src[s.offset:s.offset + s.numel].reshape(s.shape)
+            want = exact[s.key]
+            assert got.tobytes() == np.asarray(want).tobytes(), s.key
