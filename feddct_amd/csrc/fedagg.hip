@@ -463,7 +463,18 @@ struct fa_plan {
   fa_plan_info info{};
   int vec_u = kDefaultU;
   unsigned flags = 0;
+  bool has32 = false;  // the tile table touches the fp32 bucket
+  bool has64 = false;  // ... the int64 bucket
 };
+
+namespace {
+void set_kinds(fa_plan* p, const std::vector<Tile>& t) {
+  for (const Tile& x : t) {
+    if (x.kind >= K_I64_CASC) p->has64 = true;
+    else p->has32 = true;
+  }
+}
+}  // namespace
 
 namespace {
 
@@ -645,6 +656,7 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   p->flags = flags;
   std::vector<Tile> tiles;
   build_tiles(s32, s64, tile_elems, flags, &tiles, &p->info);
+  set_kinds(p, tiles);
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess && !tiles.empty()) {
     e = hipMalloc(&p->d_tiles, tiles.size() * sizeof(Tile));
@@ -733,6 +745,7 @@ int fa_plan_create_from_tiles(const fa_tile_desc* tiles, int ntiles, int64_t f32
   p->info = in;
   p->vec_u = tile_elems / (4 * kBlock);
   p->flags = flags;
+  set_kinds(p, t);
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess && !t.empty()) {
     e = hipMalloc(&p->d_tiles, t.size() * sizeof(Tile));
@@ -778,7 +791,7 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
   a.out64 = out64;
   a.n = n;
   a.flags = flags | (weights ? 0x100u : 0u);
-  const bool need32 = in.f32_numel > 0, need64 = in.i64_numel > 0;
+  const bool need32 = plan->has32, need64 = plan->has64;
   if (need32) {
     if (!c32 || !out32) return set_err(FA_E_INVAL, "fa_reduce: fp32 buckets required");
     if (!aligned16(out32)) return set_err(FA_E_ALIGN, "fa_reduce: out32 not 16-B aligned");
