@@ -6,7 +6,9 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "fedagg.hip")
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("fedagg.hip", "prox.hip")]
+DEPS = SRCS + [os.path.join(HERE, "csrc", "common.h"),
+               os.path.join(HERE, "..", "include", "fedagg.h")]
 OUT = os.path.join(HERE, "libfedagg.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -19,10 +21,9 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
 
 def build(force: bool = False, extra=()) -> str:
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= max(
-            os.path.getmtime(SRC),
-            os.path.getmtime(os.path.join(HERE, "..", "include", "fedagg.h"))):
+            os.path.getmtime(d) for d in DEPS):
         return OUT
-    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", SRC]
+    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", *SRCS]
     subprocess.run(cmd, check=True)
     os.replace(OUT + ".tmp", OUT)
     return OUT

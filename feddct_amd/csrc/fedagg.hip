@@ -28,17 +28,16 @@
 #include <string>
 #include <vector>
 
-#include "../../include/fedagg.h"
+#include "common.h"
 
 #define FA_VERSION_STR "fedagg 0.1.0 gfx950"
 
-namespace {
-
 // ---------------------------------------------------------------- errors --
+namespace {
 thread_local std::string g_last_error;
+}  // namespace
 
-int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-int set_err(int code, const char* fmt, ...) {
+int fa::set_err(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -48,12 +47,9 @@ int set_err(int code, const char* fmt, ...) {
   return code;
 }
 
-#define HIP_TRY(expr)                                                        \
-  do {                                                                       \
-    hipError_t e_ = (expr);                                                  \
-    if (e_ != hipSuccess)                                                    \
-      return set_err(FA_E_HIP, "%s: %s", #expr, hipGetErrorString(e_));     \
-  } while (0)
+namespace {
+using fa::set_err;
+#define HIP_TRY(expr) FA_HIP_TRY(expr)
 
 // ----------------------------------------------------------------- tiles --
 enum TileKind : int32_t {

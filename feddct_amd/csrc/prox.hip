@@ -1,0 +1,213 @@
+// prox.hip — FedProx proximal term on flat buckets.
+//
+// The reference adds, every training step of every FedProx client
+// (train_fedprox.py:113-116),
+//
+//     proximal_term = 0.0
+//     for w, w_t in zip(client_model.parameters(), global_model.parameters()):
+//         proximal_term += (w - w_t).norm(2)
+//     total_loss = total_loss + (mu / 2) * proximal_term
+//
+// i.e. one norm kernel launch (+ its backward) per parameter tensor.  Here
+// the client's and the global's parameters are views of flat buckets
+// (arena.py), so the whole term is two launches forward and one backward:
+//
+//   prox_partials : one workgroup per chunk (<= 4096 floats of ONE tensor),
+//                   sum of (a-b)^2 with 16-B loads, wave + LDS reduction;
+//   prox_finish   : one workgroup: per tensor the chunk partials in fixed
+//                   order -> sqrt -> norms[k]; sum of norms -> total
+//                   (deterministic: no atomics);
+//   prox_grad     : d/dw ||w - w_t|| = (w - w_t)/||w - w_t|| (0 where the
+//                   norm is 0, as torch's norm backward), scaled by the
+//                   incoming gradient; the global side gets the negation.
+//
+// HBM-bound: forward reads 2 B per element pair, backward reads 2 and writes
+// 1-2.  fp32 throughout (the reference runs it in fp32 on the GPU, whose
+// reduction order is not torch-CPU-defined): results agree with torch to
+// fp32 rounding, not bitwise.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kBlk = 256;
+constexpr int kChunk = 4096;  // floats per workgroup (4 float4 per lane)
+
+struct NormChunk {
+  int64_t start;
+  int32_t count;
+  int32_t seg;
+};
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* lds) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) lds[w] = v;
+  __syncthreads();
+  float r = 0.f;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r += lds[i];
+  __syncthreads();
+  return r;  // valid in thread 0
+}
+
+__global__ __launch_bounds__(kBlk) void prox_partials(const NormChunk* __restrict__ chunks,
+                                                      const float* __restrict__ a,
+                                                      const float* __restrict__ b,
+                                                      float* __restrict__ partials) {
+  __shared__ float lds[kBlk / 64];
+  const NormChunk c = chunks[blockIdx.x];
+  float acc = 0.f;
+  const int nv = c.count / 4;
+  const bool al = (c.start % 4) == 0;
+  if (al) {
+    const f4* pa = reinterpret_cast<const f4*>(a + c.start);
+    const f4* pb = reinterpret_cast<const f4*>(b + c.start);
+    for (int v = threadIdx.x; v < nv; v += kBlk) {
+      const f4 d = pa[v] - pb[v];
+      acc += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
+    }
+  }
+  for (int j = (al ? 4 * nv : 0) + threadIdx.x; j < c.count; j += kBlk) {
+    const float d = a[c.start + j] - b[c.start + j];
+    acc += d * d;
+  }
+  const float s = block_sum(acc, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kBlk) void prox_finish(const int* __restrict__ seg_first,
+                                                    int nseg, const float* __restrict__ partials,
+                                                    float* __restrict__ norms,
+                                                    float* __restrict__ total) {
+  __shared__ float lds[kBlk / 64];
+  float acc = 0.f;
+  for (int k = threadIdx.x; k < nseg; k += kBlk) {
+    float sq = 0.f;
+    for (int c = seg_first[k]; c < seg_first[k + 1]; ++c) sq += partials[c];
+    const float nk = sqrtf(sq);
+    norms[k] = nk;
+    acc += nk;
+  }
+  const float s = block_sum(acc, lds);
+  if (threadIdx.x == 0) *total = s;
+}
+
+__global__ __launch_bounds__(kBlk) void prox_grad(const NormChunk* __restrict__ chunks,
+                                                  const float* __restrict__ a,
+                                                  const float* __restrict__ b,
+                                                  const float* __restrict__ norms,
+                                                  const float* __restrict__ gout, float alpha,
+                                                  float* __restrict__ ga, float* __restrict__ gb) {
+  const NormChunk c = chunks[blockIdx.x];
+  const float nk = norms[c.seg];
+  const float g = nk > 0.f ? (*gout) * alpha / nk : 0.f;
+  for (int j = threadIdx.x; j < c.count; j += kBlk) {
+    const int64_t e = c.start + j;
+    const float d = g * (a[e] - b[e]);
+    ga[e] = d;
+    if (gb) gb[e] = -d;
+  }
+}
+
+}  // namespace
+
+struct fa_norm_plan {
+  int device = 0;
+  int nseg = 0;
+  int nchunks = 0;
+  int64_t numel = 0;
+  NormChunk* d_chunks = nullptr;
+  int* d_seg_first = nullptr;
+  float* d_partials = nullptr;
+};
+
+extern "C" {
+
+int fa_norm_plan_create(const fa_seg* segs, int nseg, int64_t numel, fa_norm_plan** out) {
+  if (!out) return fa::set_err(FA_E_INVAL, "fa_norm_plan_create: out is NULL");
+  *out = nullptr;
+  if (nseg < 0 || (nseg > 0 && !segs) || numel < 0)
+    return fa::set_err(FA_E_INVAL, "fa_norm_plan_create: bad segments");
+  std::vector<NormChunk> ch;
+  std::vector<int> first(nseg + 1, 0);
+  for (int k = 0; k < nseg; ++k) {
+    first[k] = (int)ch.size();
+    if (segs[k].offset < 0 || segs[k].numel < 0 || segs[k].offset + segs[k].numel > numel)
+      return fa::set_err(FA_E_INVAL, "fa_norm_plan_create: segment %d outside bucket", k);
+    for (int64_t c = 0; c < segs[k].numel; c += kChunk)
+      ch.push_back(NormChunk{segs[k].offset + c, (int32_t)std::min<int64_t>(kChunk, segs[k].numel - c), k});
+  }
+  first[nseg] = (int)ch.size();
+  fa_norm_plan* p = new fa_norm_plan();
+  p->nseg = nseg;
+  p->nchunks = (int)ch.size();
+  p->numel = numel;
+  hipError_t e = hipGetDevice(&p->device);
+  if (e == hipSuccess && !ch.empty()) e = hipMalloc(&p->d_chunks, ch.size() * sizeof(NormChunk));
+  if (e == hipSuccess) e = hipMalloc(&p->d_seg_first, first.size() * sizeof(int));
+  if (e == hipSuccess && !ch.empty()) e = hipMalloc(&p->d_partials, ch.size() * sizeof(float));
+  if (e == hipSuccess && !ch.empty())
+    e = hipMemcpy(p->d_chunks, ch.data(), ch.size() * sizeof(NormChunk), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(p->d_seg_first, first.data(), first.size() * sizeof(int), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(p->d_chunks);
+    (void)hipFree(p->d_seg_first);
+    (void)hipFree(p->d_partials);
+    delete p;
+    return fa::set_err(FA_E_HIP, "fa_norm_plan_create: %s", hipGetErrorString(e));
+  }
+  *out = p;
+  return FA_OK;
+}
+
+int fa_norm_plan_destroy(fa_norm_plan* p) {
+  if (!p) return FA_OK;
+  FA_HIP_TRY(hipFree(p->d_chunks));
+  FA_HIP_TRY(hipFree(p->d_seg_first));
+  FA_HIP_TRY(hipFree(p->d_partials));
+  delete p;
+  return FA_OK;
+}
+
+int fa_prox_norms(const fa_norm_plan* p, const float* a, const float* b, float* norms,
+                  float* total, void* stream) {
+  if (!p || !a || !b || !norms || !total) return fa::set_err(FA_E_INVAL, "fa_prox_norms: NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  if (p->nchunks > 0) {
+    hipLaunchKernelGGL(prox_partials, dim3(p->nchunks), dim3(kBlk), 0, st, p->d_chunks, a, b,
+                       p->d_partials);
+    FA_HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(prox_finish, dim3(1), dim3(kBlk), 0, st, p->d_seg_first, p->nseg,
+                     p->d_partials, norms, total);
+  FA_HIP_TRY(hipGetLastError());
+  return FA_OK;
+}
+
+int fa_prox_grad(const fa_norm_plan* p, const float* a, const float* b, const float* norms,
+                 const float* gout, float alpha, float* grad_a, float* grad_b, void* stream) {
+  if (!p || !a || !b || !norms || !gout || !grad_a)
+    return fa::set_err(FA_E_INVAL, "fa_prox_grad: NULL argument");
+  if (p->nchunks == 0) return FA_OK;
+  hipLaunchKernelGGL(prox_grad, dim3(p->nchunks), dim3(kBlk), 0, (hipStream_t)stream,
+                     p->d_chunks, a, b, norms, gout, alpha, grad_a, grad_b);
+  FA_HIP_TRY(hipGetLastError());
+  return FA_OK;
+}
+
+}  // extern "C"

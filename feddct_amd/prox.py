@@ -1,0 +1,127 @@
+"""FedProx proximal term on the flat buckets.
+
+Drop-in for the loop of train_fedprox.py:113-115:
+
+    proximal_term = 0.0
+    for w, w_t in zip(client_model.parameters(), global_model.parameters()):
+        proximal_term += (w - w_t).norm(2)
+
+becomes ``proximal_term = feddct_amd.prox.proximal_term(client_model,
+global_model)`` — the same value (to fp32 rounding) and the same gradients
+for BOTH models' parameters (the reference's graph also reaches the global
+model's parameters), computed by three HIP launches over the two arenas
+(csrc/prox.hip) instead of 2·K norm/sub kernels plus their backward.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .arena import get_arena
+
+
+class _NormPlan:
+    def __init__(self, segs: np.ndarray, numel: int):
+        arr, n = _lib.seg_array(segs)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib.fa_norm_plan_create(arr, n, int(numel), ctypes.byref(h)),
+                   "fa_norm_plan_create")
+        self.handle = h
+        self.nseg = n
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib.fa_norm_plan_destroy(h)
+            except Exception:
+                pass
+
+
+class _Prox(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, term, *params):
+        dev = term.ca.f32.device
+        norms = torch.empty(max(1, term.plan.nseg), dtype=torch.float32, device=dev)
+        total = torch.empty((), dtype=torch.float32, device=dev)
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _lib.check(_lib.lib.fa_prox_norms(term.plan.handle, term.ca.ptr32, term.ga.ptr32,
+                                          norms.data_ptr(), total.data_ptr(), s),
+                   "fa_prox_norms")
+        ctx.term = term
+        ctx.save_for_backward(norms)
+        return total
+
+    @staticmethod
+    def backward(ctx, gout):
+        term = ctx.term
+        (norms,) = ctx.saved_tensors
+        dev = norms.device
+        gout = gout.to(dtype=torch.float32).contiguous()
+        need_b = any(ctx.needs_input_grad[1 + len(term.slots):])
+        ga = torch.empty_like(term.ca.f32)
+        gb = torch.empty_like(term.ga.f32) if need_b else None
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _lib.check(_lib.lib.fa_prox_grad(term.plan.handle, term.ca.ptr32, term.ga.ptr32,
+                                         norms.data_ptr(), gout.data_ptr(), 1.0,
+                                         ga.data_ptr(), None if gb is None else gb.data_ptr(),
+                                         s), "fa_prox_grad")
+        grads_a = [ga[o:o + m].view(shape) for o, m, shape in term.slots]
+        grads_b = ([gb[o:o + m].view(shape) for o, m, shape in term.slots] if need_b
+                   else [None] * len(term.slots))
+        return (None, *grads_a, *grads_b)
+
+
+class ProximalTerm:
+    """Bound (client, global) pair: plan built once, reused every step."""
+
+    def __init__(self, client_model: torch.nn.Module, global_model: torch.nn.Module):
+        from .aggregate import engine
+        layout = engine().layout_of(global_model)
+        self.client_model, self.global_model = client_model, global_model
+        self.layout = layout
+        self.ca = get_arena(client_model, layout)
+        self.ga = get_arena(global_model, layout)
+        if self.ca.device.type != "cuda":
+            raise RuntimeError("feddct_amd.prox: models must be on the GPU (no CPU fallback)")
+        cn = [n for n, _ in client_model.named_parameters()]
+        gn = [n for n, _ in global_model.named_parameters()]
+        if len(cn) != len(gn):
+            raise RuntimeError("client and global models have different parameter counts")
+        slots = []
+        for a, b in zip(cn, gn):
+            sa, sb = layout.by_key.get(a), layout.by_key.get(b)
+            if sa is None or sb is None or sa.kind != "f32" or sb.offset != sa.offset:
+                raise NotImplementedError(
+                    f"proximal term pairs parameters by position; {a!r} / {b!r} are not the "
+                    "same fp32 slot of one layout")
+            slots.append((sa.offset, sa.numel, sa.shape))
+        self.slots = slots
+        segs = np.array([(o, m) for o, m, _ in slots], np.int64).reshape(-1, 2)
+        with torch.cuda.device(self.ca.device):
+            self.plan = _NormPlan(segs, layout.f32_numel)
+
+    def valid(self) -> bool:
+        return (getattr(self.client_model, "_fa_arena", None) is self.ca and self.ca.valid()
+                and getattr(self.global_model, "_fa_arena", None) is self.ga and self.ga.valid())
+
+    def __call__(self) -> torch.Tensor:
+        params = list(self.client_model.parameters()) + list(self.global_model.parameters())
+        return _Prox.apply(self, *params)
+
+
+_TERMS: Dict[Tuple[int, int], ProximalTerm] = {}
+
+
+def proximal_term(client_model: torch.nn.Module, global_model: torch.nn.Module) -> torch.Tensor:
+    """Σ_k ||w_k − w_t,k||₂ over zip(client.parameters(), global.parameters()),
+    differentiable w.r.t. both (train_fedprox.py:113-115)."""
+    key = (id(client_model), id(global_model))
+    t = _TERMS.get(key)
+    if t is None or not t.valid() or t.client_model is not client_model:
+        t = _TERMS[key] = ProximalTerm(client_model, global_model)
+    return t()

@@ -168,6 +168,23 @@ int fa_synth_fill_f32(float *dst, int64_t numel, int key_index, int client,
 int fa_synth_fill_i64(int64_t *dst, int64_t numel, int key_index, int client,
                       int mode, void *stream);
 
+/* ---- FedProx proximal term (train_fedprox.py:113-116), SURVEY.md §8 f3 ----
+ * sum_k ||a_k - b_k||_2 over the tensors (segments) of two flat buckets —
+ * the client's and the global's parameters — and its gradient.  A norm plan
+ * owns a small device scratch: use one plan from one stream at a time. */
+typedef struct fa_norm_plan fa_norm_plan;
+int fa_norm_plan_create(const fa_seg *segs, int nseg, int64_t numel,
+                        fa_norm_plan **out);
+int fa_norm_plan_destroy(fa_norm_plan *plan);
+/* norms[k] = ||a_k - b_k||_2 (device, nseg floats); *total = sum_k norms[k] */
+int fa_prox_norms(const fa_norm_plan *plan, const float *a, const float *b,
+                  float *norms, float *total, void *stream);
+/* grad_a[e] = (*gout) * alpha * (a[e]-b[e]) / norms[k]  (0 where norms[k]==0);
+ * grad_b (nullable) = -grad_a.  Only elements inside segments are written. */
+int fa_prox_grad(const fa_norm_plan *plan, const float *a, const float *b,
+                 const float *norms, const float *gout, float alpha,
+                 float *grad_a, float *grad_b, void *stream);
+
 /* Streaming copy (bandwidth ceiling calibration for the roofline). */
 int fa_copy_f32(const float *src, float *dst, int64_t numel, void *stream);
 

@@ -92,3 +92,12 @@ def test_stateless_plans_never_cover_gaps():
     for o, m in segs:
         want[o:o + m] = True
     assert np.array_equal(covered, want)
+
+
+def test_norm_plan_host_errors():
+    L = _lib.lib
+    h = ctypes.c_void_p()
+    assert L.fa_norm_plan_create(None, 0, 0, None) == _lib.FA_E_INVAL
+    segs, n = _lib.seg_array(np.array([[0, 100]], np.int64))
+    assert L.fa_norm_plan_create(segs, n, 50, ctypes.byref(h)) == _lib.FA_E_INVAL
+    assert L.fa_prox_norms(None, None, None, None, None, None) == _lib.FA_E_INVAL

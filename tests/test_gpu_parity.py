@@ -450,3 +450,52 @@ def test_host_pipeline_bit_exact_with_broadcast(lib):
         assert same(o32, o64)
     pipe.run(h32, h64, o32, o64, h32[1:3], h64[1:3])
     assert same(h32[2], h64[2]) and same(h32[1], h64[1]) and same(o32, o64)
+
+
+# ------------------------------------------------ FedProx proximal term --
+def _prox_models(seed, same=False):
+    torch.manual_seed(seed)
+    mk = lambda: torch.nn.Sequential(torch.nn.Conv2d(3, 16, 3), torch.nn.BatchNorm2d(16),  # noqa
+                                     torch.nn.Conv2d(16, 33, 3, bias=False), torch.nn.Linear(7, 5)).to(DEV)
+    c, g = mk(), mk()
+    if same:
+        g.load_state_dict(c.state_dict())
+    return c, g
+
+
+@pytest.mark.parametrize("same", [False, True])
+def test_proximal_term_matches_reference_loop(same):
+    from feddct_amd.prox import proximal_term
+    c, g = _prox_models(0, same)
+    c_ref, g_ref = _prox_models(0, same)
+    # reference: train_fedprox.py:113-115 on plain modules
+    pt = 0.0
+    for w, w_t in zip(c_ref.parameters(), g_ref.parameters()):
+        pt += (w - w_t).norm(2)
+    (pt * 0.37).backward()
+    got = proximal_term(c, g)
+    (got * 0.37).backward()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(got, pt.detach(), rtol=2e-6, atol=1e-7)
+    for (n, p), p_ref in zip(c.named_parameters(), c_ref.parameters()):
+        torch.testing.assert_close(p.grad, p_ref.grad, rtol=1e-5, atol=1e-8, msg=n)
+    for p, p_ref in zip(g.parameters(), g_ref.parameters()):
+        torch.testing.assert_close(p.grad, p_ref.grad, rtol=1e-5, atol=1e-8)
+
+
+def test_proximal_term_tracks_training_and_aggregation():
+    """Across an optimizer step and a server round the bound term stays
+    current (params are arena views)."""
+    from feddct_amd.fedprox import server_aggregate
+    from feddct_amd.prox import proximal_term
+    c, g = _prox_models(1)
+    opt = torch.optim.SGD(c.parameters(), lr=0.1)
+    for _ in range(3):
+        opt.zero_grad()
+        loss = c[3](torch.randn(4, 7, device=DEV)).square().sum() + 0.5 * proximal_term(c, g)
+        loss.backward()
+        opt.step()
+        ref = sum((w - w_t).norm(2) for w, w_t in zip(c.parameters(), g.parameters()))
+        torch.testing.assert_close(proximal_term(c, g).detach(), ref.detach(), rtol=2e-6, atol=1e-7)
+    server_aggregate(g, [c])
+    assert float(proximal_term(c, g)) == 0.0
