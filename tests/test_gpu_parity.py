@@ -499,3 +499,23 @@ def test_proximal_term_tracks_training_and_aggregation():
         torch.testing.assert_close(proximal_term(c, g).detach(), ref.detach(), rtol=2e-6, atol=1e-7)
     server_aggregate(g, [c])
     assert float(proximal_term(c, g)) == 0.0
+
+
+def test_checkpoint_from_device_bucket(tmp_path):
+    from feddct_amd.checkpoint import bucket_state_dict, load_into, save_checkpoint
+    from feddct_amd.fedavg import server_aggregate
+    man = load_manifest("wrnsl16_8_sf4_c10_main")
+    states = [synth.gen_state(man, i) for i in range(3)]
+    g = StateModule(man).to(DEV)
+    cl = _modules(man, states)
+    server_aggregate(g, cl)
+    p = save_checkpoint({"round": 1, "state_dict": g}, False, str(tmp_path))
+    ck = torch.load(p, weights_only=True)
+    for k, v in g.state_dict().items():
+        assert torch.equal(ck["state_dict"][k], v.cpu()), k
+    fresh = StateModule(man).to(DEV)
+    server_aggregate(fresh, [StateModule(man).to(DEV)])  # bind it
+    load_into(fresh, ck["state_dict"])
+    for k, v in g.state_dict().items():
+        assert torch.equal(fresh.state_dict()[k], v), k
+    assert list(bucket_state_dict(g)) == list(g.state_dict())
