@@ -40,6 +40,7 @@ EXPORTS = [
     "fa_mean_i64_trunc", "fa_div_f32", "fa_div_trunc_i64", "fa_broadcast_f32",
     "fa_synth_fill_f32", "fa_synth_fill_i64", "fa_copy_f32",
     "fa_norm_plan_create", "fa_norm_plan_destroy", "fa_prox_norms", "fa_prox_grad",
+    "fa_read_probe_f32",
 ]
 
 
@@ -94,6 +95,7 @@ def _load():
         "fa_synth_fill_f32": (_I, [_P, _I64, _I, _I, ctypes.c_float, ctypes.c_float, _I, _P]),
         "fa_synth_fill_i64": (_I, [_P, _I64, _I, _I, _I, _P]),
         "fa_copy_f32": (_I, [_P, _P, _I64, _P]),
+        "fa_read_probe_f32": (_I, [_P, _I64, _P, _I, _P]),
         "fa_norm_plan_create": (_I, [_P, _I, _I64, ctypes.POINTER(_P)]),
         "fa_norm_plan_destroy": (_I, [_P]),
         "fa_prox_norms": (_I, [_P, _P, _P, _P, _P, _P]),

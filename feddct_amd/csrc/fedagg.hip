@@ -401,6 +401,24 @@ __global__ __launch_bounds__(kBlock) void copy_kernel(const float* __restrict__ 
     dst[4 * nv + threadIdx.x] = src[4 * nv + threadIdx.x];
 }
 
+// Read-only streaming probe: per workgroup sum of its float4s (calibrates the
+// read-bandwidth ceiling the reduce kernel, 95 % reads, is measured against).
+__global__ __launch_bounds__(kBlock) void read_probe_kernel(const float* __restrict__ src,
+                                                            int64_t nv, float* __restrict__ out) {
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (; v + 3 * stride < nv; v += 4 * stride) {
+    const f4 a = ld4<true>(src + 4 * v), b = ld4<true>(src + 4 * (v + stride));
+    const f4 c = ld4<true>(src + 4 * (v + 2 * stride)), d = ld4<true>(src + 4 * (v + 3 * stride));
+    acc += (a + b) + (c + d);
+  }
+  for (; v < nv; v += stride) acc += ld4<true>(src + 4 * v);
+  float s = acc.x + acc.y + acc.z + acc.w;
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out + blockIdx.x, s);
+}
+
 // ------------------------------------------- synthetic state (synth.py) --
 __device__ __forceinline__ uint64_t hash64(uint64_t seed, uint64_t idx) {
   uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx * 0xD1B54A32D192ED03ull;
@@ -591,7 +609,8 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   switch (vec_u) {
     case 1: return b_env == 16 ? launch_u<1, 16>(a, ntiles, deep, w, nt, st)
                                : launch_u<1, 8>(a, ntiles, deep, w, nt, st);
-    case 4: return launch_u<4, 8>(a, ntiles, deep, w, nt, st);
+    case 4: return b_env == 16 ? launch_u<4, 16>(a, ntiles, deep, w, nt, st)
+                               : launch_u<4, 8>(a, ntiles, deep, w, nt, st);
     default: return b_env == 16 ? launch_u<2, 16>(a, ntiles, deep, w, nt, st)
                                 : launch_u<2, 8>(a, ntiles, deep, w, nt, st);
   }
@@ -925,6 +944,15 @@ int fa_synth_fill_i64(int64_t* dst, int64_t numel, int key_index, int client, in
   if (numel == 0) return FA_OK;
   hipLaunchKernelGGL(synth_i64_kernel, dim3(grid_for(numel, kBlock)), dim3(kBlock), 0,
                      (hipStream_t)stream, dst, numel, key_index, client, mode);
+  HIP_TRY(hipGetLastError());
+  return FA_OK;
+}
+
+int fa_read_probe_f32(const float* src, int64_t numel, float* out, int grid, void* stream) {
+  if (numel < 4 || !src || !out || grid < 1) return set_err(FA_E_INVAL, "fa_read_probe_f32: bad args");
+  if (!aligned16(src)) return set_err(FA_E_ALIGN, "fa_read_probe_f32: unaligned");
+  hipLaunchKernelGGL(read_probe_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, src,
+                     numel / 4, out);
   HIP_TRY(hipGetLastError());
   return FA_OK;
 }

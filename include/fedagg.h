@@ -187,6 +187,10 @@ int fa_prox_grad(const fa_norm_plan *plan, const float *a, const float *b,
 
 /* Streaming copy (bandwidth ceiling calibration for the roofline). */
 int fa_copy_f32(const float *src, float *dst, int64_t numel, void *stream);
+/* Read-only streaming probe (read-bandwidth ceiling): out[grid] partial sums
+ * (accumulated: zero out first). */
+int fa_read_probe_f32(const float *src, int64_t numel, float *out, int grid,
+                      void *stream);
 
 #ifdef __cplusplus
 }

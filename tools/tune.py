@@ -25,7 +25,7 @@ def main():
     variants = []
     for u in (1, 2, 4):
         for nt in (True, False):
-            for b16 in ((False, True) if u < 4 else (False,)):
+            for b16 in (False, True):
                 fl = _lib.FA_PLAN_GAPS_ARE_PADDING | (0 if nt else _lib.FA_PLAN_TUNE_NO_NT) | \
                     (0 if b16 else _lib.FA_PLAN_TUNE_BATCH8)
                 plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
@@ -47,6 +47,26 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[name].append(e0.elapsed_time(e1) / 20 * 1e3)
+    # read-only and copy ceilings on a 2 GiB buffer (beyond the 256 MiB MALL)
+    big = torch.empty(512 * 1024 * 1024, dtype=torch.float32, device=dev)
+    big.uniform_()
+    for grid in (1024, 2048, 4096, 8192):
+        part = torch.zeros(grid, device=dev)
+        fn = lambda: _lib.check(_lib.lib.fa_read_probe_f32(  # noqa: E731
+            big.data_ptr(), big.numel(), part.data_ptr(), grid,
+            torch.cuda.current_stream().cuda_stream))
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 10 * 1e-3
+        print(json.dumps({"probe": "read_only", "grid": grid, "GBps": round(big.numel() * 4 / t / 1e9, 1)}))
+    del big
     ref32, ref64 = variants[0][2], variants[0][3]
     for name, _, o32, o64 in variants:
         ts = sorted(times[name])
