@@ -204,6 +204,61 @@ def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
     return res
 
 
+def other_configs(dev, steps=20):
+    """The other BASELINE.json configs on this GPU (device-resident), each
+    checked against the reference digests where they exist:
+    cfg3 FedDCT sf4 C10, 5 slots, main + proxy (two launches), working set
+      rotated over 2 copies (> the 256 MiB Infinity Cache);
+    cfg4 FedProx C100, 20 clients, client-size-weighted (extension);
+    cfg5 FedDCT sf4 C100, 24 slots, main + proxy, all on one GPU."""
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        dig = json.load(f)
+    res = {}
+
+    def run(name, parts, rot, digests):
+        sets = []
+        for r in range(rot):
+            reds = []
+            for lay_name, n, w in parts:
+                man = load_manifest(lay_name)
+                lay = BucketLayout.from_manifest(man)
+                cl = make_clients(lay, man, range(n), dev)
+                o32, o64 = torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])
+                reds.append((lay_name, lay, n, Reducer(lay, cl, o32, o64, weights=w), o32, o64))
+            sets.append(reds)
+        k = [0]
+
+        def step():
+            for r in sets[k[0] % rot]:
+                r[3]()
+            k[0] += 1
+        t, _ = timed_launches(step, steps, 3)
+        nbytes = sum(r[1].algorithmic_bytes(r[2]) for r in sets[0])
+        out = {"GBps": round(nbytes / t / 1e9, 1), "us_per_step": round(t * 1e6, 1),
+               "algorithmic_bytes": nbytes, "rotated_sets": rot}
+        if digests:
+            ok = True
+            for lay_name, lay, n, _, o32, o64 in sets[0]:
+                key = digests.get(lay_name)
+                if key:
+                    ok &= digest_of(lay, o32, o64) == dig[key]
+            out["bit_exact_vs_reference_digest"] = bool(ok)
+        res[name] = out
+
+    run("cfg3_feddct_c10_n5", [("wrnsl16_8_sf4_c10_main", 5, None),
+                               ("wrnsl16_8_sf4_c10_proxy", 5, None)], 2,
+        {"wrnsl16_8_sf4_c10_main": "feddct/wrnsl16_8_sf4_c10_main/n5",
+         "wrnsl16_8_sf4_c10_proxy": "feddct/wrnsl16_8_sf4_c10_proxy/n5"})
+    from oracle.torch_order import weights_from_sizes
+    sizes = [2500 + 97 * ((7 * i) % 11) for i in range(20)]  # quantity-skewed shards
+    run("cfg4_fedprox_c100_n20_weighted", [("wrn16_8_c100", 20, weights_from_sizes(sizes))], 1, {})
+    run("cfg5_feddct_c100_n24_one_gpu", [("wrnsl16_8_sf4_c100_main", 24, None),
+                                         ("wrnsl16_8_sf4_c100_proxy", 24, None)], 1,
+        {"wrnsl16_8_sf4_c100_main": "feddct/wrnsl16_8_sf4_c100_main/n24",
+         "wrnsl16_8_sf4_c100_proxy": "feddct/wrnsl16_8_sf4_c100_proxy/n24"})
+    return res
+
+
 def _holder_class(layout):
     class Holder(torch.nn.Module):
         def __init__(self):
@@ -331,6 +386,7 @@ def main():
             tb, _ = timed_launches(fused, max(10, args.steps // 2), 3)
             extra["round_with_fused_broadcast_us"] = round(tb * 1e6, 1)
             extra["dropin"] = dropin_timing(layout, clients, dev)
+            extra["other_configs"] = other_configs(dev)
     else:
         from feddct_amd.dist import ShardedAggregator
         agg = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],

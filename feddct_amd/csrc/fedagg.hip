@@ -70,7 +70,7 @@ struct Tile {
 static_assert(sizeof(Tile) == 16, "tile is 16 B");
 
 constexpr int kBlock = 256;
-constexpr int kDefaultU = 2;  // float4 vectors per thread per client
+constexpr int kDefaultU = 1;  // float4 vectors per thread per client (tools/tune.py)
 
 constexpr int kInline = FA_INLINE_CLIENTS;
 
