@@ -17,6 +17,8 @@ def main():
     lay_name = sys.argv[1] if len(sys.argv) > 1 else "wrn16_8_c10"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    weighted = len(sys.argv) > 4 and sys.argv[4] == "w"
+    probe = len(sys.argv) > 5 and sys.argv[5] == "probe"
     dev = torch.device("cuda", 0)
     man = load_manifest(lay_name)
     lay = BucketLayout.from_manifest(man)
@@ -32,8 +34,12 @@ def main():
                                  tile_elems=1024 * u, flags=fl)
                 out32 = torch.zeros_like(clients[0][0])
                 out64 = torch.zeros_like(clients[0][1])
+                if not nt:
+                    continue
+                w = [1.0 / (i + 2) for i in range(n)] if weighted else None
                 variants.append((f"U{u}_{'nt' if nt else 'plain'}_B{16 if b16 else 8}",
-                                 Reducer(lay, clients, out32, out64, plan=plan), out32, out64))
+                                 Reducer(lay, clients, out32, out64, plan=plan, weights=w),
+                                 out32, out64))
     times = {v[0]: [] for v in variants}
     for _ in range(rounds):
         for name, red, _, _ in variants:
@@ -48,9 +54,9 @@ def main():
             torch.cuda.synchronize()
             times[name].append(e0.elapsed_time(e1) / 20 * 1e3)
     # read-only and copy ceilings on a 2 GiB buffer (beyond the 256 MiB MALL)
-    big = torch.empty(512 * 1024 * 1024, dtype=torch.float32, device=dev)
+    big = torch.empty(512 * 1024 * 1024 if probe else 1024, dtype=torch.float32, device=dev)
     big.uniform_()
-    for grid in (1024, 2048, 4096, 8192):
+    for grid in ((1024, 2048, 4096, 8192) if probe else ()):
         part = torch.zeros(grid, device=dev)
         fn = lambda: _lib.check(_lib.lib.fa_read_probe_f32(  # noqa: E731
             big.data_ptr(), big.numel(), part.data_ptr(), grid,
@@ -70,7 +76,7 @@ def main():
     ref32, ref64 = variants[0][2], variants[0][3]
     for name, _, o32, o64 in variants:
         ts = sorted(times[name])
-        print(json.dumps({"variant": name, "layout": lay_name, "n": n,
+        print(json.dumps({"variant": name, "layout": lay_name, "n": n, "weighted": weighted,
                           "us_median": round(ts[len(ts) // 2], 2), "us_min": round(ts[0], 2),
                           "GBps_median": round(nbytes / (ts[len(ts) // 2] * 1e-6) / 1e9, 1),
                           "same_as_first": bool(torch.equal(o32, ref32) and torch.equal(o64, ref64))}))
