@@ -210,6 +210,38 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0,
   }
 }
 
+// The last, partial batch (nb < NB clients): same issue-all-then-add shape,
+// every step guarded by a uniform (scalar) branch.
+template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, bool NT>
+__device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, int nb,
+                                           const int64_t (&off)[U], const bool (&ok)[U],
+                                           int lp, int mask) {
+  f4 x[NB][U];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b < nb) {
+      const float* p = cptr32(a, b0 + b);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (FULL) x[b][u] = ld4<NT>(p + off[u]);
+        else x[b][u] = ok[u] ? ld4<NT>(p + off[u]) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b < nb) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        f4 v = x[b][u];
+        if constexpr (WEIGHTED) v = mul4s(v, cw(a, b0 + b));
+        A.l0[u] = add4(A.l0[u], v);
+      }
+      promote<U, DEEP>(A, b0 + b + 1, lp, mask);
+    }
+  }
+}
+
 template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, bool NT>
 __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
                                          int count) {
@@ -229,8 +261,7 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
   int b0 = 0;
   for (; b0 + B <= n; b0 += B)
     batch<U, B, FULL, DEEP, WEIGHTED, NT>(a, A, b0, off, ok, lp, mask);
-  for (; b0 < n; ++b0)
-    batch<U, 1, FULL, DEEP, WEIGHTED, NT>(a, A, b0, off, ok, lp, mask);
+  if (b0 < n) batch_tail<U, B, FULL, DEEP, WEIGHTED, NT>(a, A, b0, n - b0, off, ok, lp, mask);
 
   const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
   const float fn = (float)n;
@@ -609,8 +640,7 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   switch (vec_u) {
     case 1: return b_env == 16 ? launch_u<1, 16>(a, ntiles, deep, w, nt, st)
                                : launch_u<1, 8>(a, ntiles, deep, w, nt, st);
-    case 4: return b_env == 16 ? launch_u<4, 16>(a, ntiles, deep, w, nt, st)
-                               : launch_u<4, 8>(a, ntiles, deep, w, nt, st);
+    case 4: return launch_u<4, 8>(a, ntiles, deep, w, nt, st);
     default: return b_env == 16 ? launch_u<2, 16>(a, ntiles, deep, w, nt, st)
                                 : launch_u<2, 8>(a, ntiles, deep, w, nt, st);
   }

@@ -27,7 +27,7 @@ def main():
     variants = []
     for u in (1, 2, 4):
         for nt in (True, False):
-            for b16 in (False, True):
+            for b16 in ((False, True) if u < 4 else (False,)):
                 fl = _lib.FA_PLAN_GAPS_ARE_PADDING | (0 if nt else _lib.FA_PLAN_TUNE_NO_NT) | \
                     (0 if b16 else _lib.FA_PLAN_TUNE_BATCH8)
                 plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
