@@ -507,6 +507,10 @@ struct fa_plan {
   Tile* d_tiles = nullptr;
   fa_plan_info info{};
   int vec_u = kDefaultU;
+  // auto plans (tile_elems == 0) also carry a 2048-float table: weighted or
+  // small-N reductions run it with 8-client batches (tools/tune.py sweep)
+  Tile* d_tiles_alt = nullptr;
+  int ntiles_alt = 0;
   unsigned flags = 0;
   bool has32 = false;  // the tile table touches the fp32 bucket
   bool has64 = false;  // ... the int64 bucket
@@ -636,7 +640,9 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   const bool deep = a.n >= 256;
   const bool w = a.flags & 0x100u;  // internal: weighted
   const bool nt = !(pflags & FA_PLAN_TUNE_NO_NT);
-  const int b_env = (pflags & FA_PLAN_TUNE_BATCH8) ? 8 : 16;
+  const bool small = w || a.n < 16;
+  const int b_env = (pflags & FA_PLAN_TUNE_BATCH8) ? 8
+                    : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (small ? 8 : 16);
   switch (vec_u) {
     case 1: return b_env == 16 ? launch_u<1, 16>(a, ntiles, deep, w, nt, st)
                                : launch_u<1, 8>(a, ntiles, deep, w, nt, st);
@@ -685,6 +691,7 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   if (!out) return set_err(FA_E_INVAL, "fa_plan_create: out is NULL");
   *out = nullptr;
   if (f32_numel < 0 || i64_numel < 0) return set_err(FA_E_INVAL, "negative bucket size");
+  const bool autosel = tile_elems == 0;
   if (tile_elems == 0) tile_elems = 4 * kBlock * kDefaultU;
   if (tile_elems != 4 * kBlock && tile_elems != 8 * kBlock && tile_elems != 16 * kBlock)
     return set_err(FA_E_INVAL, "tile_elems must be 1024, 2048 or 4096 (got %d)", tile_elems);
@@ -699,17 +706,28 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   p->info.tile_elems = tile_elems;
   p->vec_u = tile_elems / (4 * kBlock);
   p->flags = flags;
-  std::vector<Tile> tiles;
+  std::vector<Tile> tiles, alt;
   build_tiles(s32, s64, tile_elems, flags, &tiles, &p->info);
   set_kinds(p, tiles);
+  if (autosel) {
+    fa_plan_info ia{};
+    build_tiles(s32, s64, 8 * kBlock, flags, &alt, &ia);
+    p->ntiles_alt = (int)alt.size();
+  }
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess && !tiles.empty()) {
     e = hipMalloc(&p->d_tiles, tiles.size() * sizeof(Tile));
     if (e == hipSuccess)
       e = hipMemcpy(p->d_tiles, tiles.data(), tiles.size() * sizeof(Tile), hipMemcpyHostToDevice);
   }
+  if (e == hipSuccess && !alt.empty()) {
+    e = hipMalloc(&p->d_tiles_alt, alt.size() * sizeof(Tile));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_tiles_alt, alt.data(), alt.size() * sizeof(Tile), hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     if (p->d_tiles) (void)hipFree(p->d_tiles);
+    if (p->d_tiles_alt) (void)hipFree(p->d_tiles_alt);
     delete p;
     return set_err(FA_E_HIP, "fa_plan_create: %s", hipGetErrorString(e));
   }
@@ -809,6 +827,7 @@ int fa_plan_create_from_tiles(const fa_tile_desc* tiles, int ntiles, int64_t f32
 int fa_plan_destroy(fa_plan* plan) {
   if (!plan) return FA_OK;
   if (plan->d_tiles) HIP_TRY(hipFree(plan->d_tiles));
+  if (plan->d_tiles_alt) HIP_TRY(hipFree(plan->d_tiles_alt));
   delete plan;
   return FA_OK;
 }
@@ -881,7 +900,13 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
     a.tab64 = (const int64_t* const*)((const void**)table + n);
     a.tabw = (const float*)((const void**)table + 2 * n);
   }
-  hipError_t e = launch_reduce(a, in.ntiles, plan->vec_u, plan->flags, st);
+  int ntiles = in.ntiles, vec_u = plan->vec_u;
+  if (plan->d_tiles_alt && (weights || n < 16)) {
+    a.tiles = plan->d_tiles_alt;
+    ntiles = plan->ntiles_alt;
+    vec_u = 2;
+  }
+  hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st);
   if (table) {
     hipError_t e2 = hipFreeAsync(table, st);
     if (e == hipSuccess) e = e2;

@@ -74,7 +74,8 @@ extern "C" {
 /* Plan-build flags */
 #define FA_PLAN_GAPS_ARE_PADDING 1u /* bytes between segments may be written */
 #define FA_PLAN_TUNE_NO_NT 2u       /* tuning: plain (temporal) loads/stores   */
-#define FA_PLAN_TUNE_BATCH8 4u     /* tuning: 8 (not 16) clients per batch    */
+#define FA_PLAN_TUNE_BATCH8 4u     /* tuning: force 8 clients per load batch  */
+#define FA_PLAN_TUNE_BATCH16 8u    /* tuning: force 16 clients per load batch */
 
 /* One tensor (state_dict key) inside a flat bucket: [offset, offset+numel). */
 typedef struct fa_seg {

@@ -25,11 +25,16 @@ def main():
     clients = make_clients(lay, man, range(n), dev)
     nbytes = lay.algorithmic_bytes(n)
     variants = []
+    auto_plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel)
+    o32a, o64a = torch.zeros_like(clients[0][0]), torch.zeros_like(clients[0][1])
+    wa = [1.0 / (i + 2) for i in range(n)] if weighted else None
+    variants.append(("auto", Reducer(lay, clients, o32a, o64a, plan=auto_plan, weights=wa),
+                     o32a, o64a))
     for u in (1, 2, 4):
         for nt in (True, False):
             for b16 in ((False, True) if u < 4 else (False,)):
                 fl = _lib.FA_PLAN_GAPS_ARE_PADDING | (0 if nt else _lib.FA_PLAN_TUNE_NO_NT) | \
-                    (0 if b16 else _lib.FA_PLAN_TUNE_BATCH8)
+                    (_lib.FA_PLAN_TUNE_BATCH16 if b16 else _lib.FA_PLAN_TUNE_BATCH8)
                 plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
                                  tile_elems=1024 * u, flags=fl)
                 out32 = torch.zeros_like(clients[0][0])
