@@ -249,7 +249,7 @@ def other_configs(dev, steps=20):
                                ("wrnsl16_8_sf4_c10_proxy", 5, None)], 2,
         {"wrnsl16_8_sf4_c10_main": "feddct/wrnsl16_8_sf4_c10_main/n5",
          "wrnsl16_8_sf4_c10_proxy": "feddct/wrnsl16_8_sf4_c10_proxy/n5"})
-    from oracle.torch_order import weights_from_sizes
+    from feddct_amd.aggregate import client_weights as weights_from_sizes
     sizes = [2500 + 97 * ((7 * i) % 11) for i in range(20)]  # quantity-skewed shards
     run("cfg4_fedprox_c100_n20_weighted", [("wrn16_8_c100", 20, weights_from_sizes(sizes))], 1, {})
     run("cfg5_feddct_c100_n24_one_gpu", [("wrnsl16_8_sf4_c100_main", 24, None),
@@ -375,7 +375,7 @@ def main():
             del big, big2
             extra["host_inclusive"] = host_inclusive(layout, clients, reducer, out32, out64)
             # weighted variant (client-size weights, BASELINE config 4's extension)
-            from oracle.torch_order import weights_from_sizes
+            from feddct_amd.aggregate import client_weights as weights_from_sizes
             w = weights_from_sizes(np.arange(1, N_CLIENTS + 1))
             wred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
                            weights=w, plan=reducer.plan)

@@ -36,7 +36,7 @@ from . import _lib
 from .arena import ModuleArena, get_arena, state_owners
 from .layout import BucketLayout
 
-__all__ = ["server_aggregate", "server_aggregate_split", "aggregate_weighted",
+__all__ = ["server_aggregate", "server_aggregate_split", "aggregate_weighted", "client_weights",
            "Engine", "engine"]
 
 
@@ -179,6 +179,12 @@ def server_aggregate_split(global_model_a, global_model_b, models_a, models_b):
     e.reduce_modules(global_model_b, list(models_b))
 
 
+def client_weights(sizes) -> np.ndarray:
+    """FedAvg client weights w_i = fp32(n_i / Σn) (float64 ratio, one rounding)."""
+    s = np.asarray(sizes, np.float64)
+    return (s / s.sum()).astype(np.float32)
+
+
 def aggregate_weighted(global_model, client_models, weights=None, sizes=None,
                        broadcast=True):
     """Client-size-weighted FedAvg (SURVEY.md §8 a9 — an extension: the
@@ -189,8 +195,7 @@ def aggregate_weighted(global_model, client_models, weights=None, sizes=None,
     if weights is None and sizes is None:
         raise ValueError("give weights or sizes")
     if weights is None:
-        s = np.asarray(sizes, np.float64)
-        weights = (s / s.sum()).astype(np.float32)
+        weights = client_weights(sizes)
     w = np.asarray(weights, np.float32)
     if np.all(w == w[0]):
         engine().reduce_modules(global_model, list(client_models), None, broadcast)
