@@ -313,7 +313,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--chunks", type=int, default=4)
+    ap.add_argument("--chunks", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exact", action="store_true",
                     help="N>1: skip timing the column-striped exact mode")

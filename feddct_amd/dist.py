@@ -110,7 +110,7 @@ class ShardedAggregator:
 
     def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
                  local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
-                 out64: torch.Tensor, nchunks: int = 4, backend=None, group=None):
+                 out64: torch.Tensor, nchunks: int = 8, backend=None, group=None):
         self.layout = layout
         self.local32, self.local64 = local32, local64
         self.n_total = n_total
