@@ -34,6 +34,13 @@ FA_PLAN_GAPS_ARE_PADDING = 1
 FA_PLAN_TUNE_NO_NT = 2
 FA_PLAN_TUNE_BATCH8 = 4
 FA_PLAN_TUNE_BATCH16 = 8
+FA_PLAN_TUNE_XCD = 16
+
+
+def FA_PLAN_TUNE_BLOCKS_PER_CU(c):
+    return (int(c) & 0xF) << 8
+
+
 
 EXPORTS = [
     "fa_version", "fa_last_error", "fa_plan_create", "fa_plan_destroy",

@@ -83,6 +83,9 @@ struct ReduceArgs {
   int64_t* out64;
   int n;
   unsigned flags;
+  int ntiles;   // tiles in the table (== grid)
+  int nscalar;  // leading scalar tiles
+  int xcd_swz;  // tuning: give each XCD a contiguous range of vector tiles
   const float* const* tab32;
   const int64_t* const* tab64;
   const float* tabw;
@@ -382,7 +385,15 @@ template <int U, int B, bool DEEP, bool WEIGHTED, bool NT>
 __global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs args) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  const Tile t = a.tiles[blockIdx.x];
+  int ti = blockIdx.x;
+  if (a.xcd_swz && ti >= a.nscalar) {
+    // bijective: blocks i and i+8 share an XCD (round-robin dispatch); XCD x
+    // gets the contiguous tile range [x*q + min(x,r), ...) of the vector tiles
+    const int i = ti - a.nscalar, nv = a.ntiles - a.nscalar;
+    const int q = nv / 8, r = nv % 8, x = i % 8, j = i / 8;
+    ti = a.nscalar + x * q + min(x, r) + j;
+  }
+  const Tile t = a.tiles[ti];
   if (t.kind == K_F32_VEC) {
     if (t.count == 4 * U * kBlock) tile_vec<U, B, true, DEEP, WEIGHTED, NT>(a, t.start, t.count);
     else tile_vec<U, B, false, DEEP, WEIGHTED, NT>(a, t.start, t.count);
@@ -511,6 +522,7 @@ struct fa_plan {
   // small-N reductions run it with 8-client batches (tools/tune.py sweep)
   Tile* d_tiles_alt = nullptr;
   int ntiles_alt = 0;
+  int nscalar_alt = 0;
   unsigned flags = 0;
   bool has32 = false;  // the tile table touches the fp32 bucket
   bool has64 = false;  // ... the int64 bucket
@@ -618,9 +630,12 @@ int build_tiles(const std::vector<fa_seg>& s32, const std::vector<fa_seg>& s64, 
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+thread_local size_t t_dyn_lds = 0;  // tuning: occupancy cap through dynamic LDS
+
 template <int U, int B, bool DEEP, bool W, bool NT>
 hipError_t launch_one(const ReduceArgs& a, int ntiles, hipStream_t st) {
-  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, NT>), dim3(ntiles), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, NT>), dim3(ntiles), dim3(kBlock), t_dyn_lds,
+                     st, a);
   return hipGetLastError();
 }
 
@@ -643,6 +658,8 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   const bool small = w || a.n < 16;
   const int b_env = (pflags & FA_PLAN_TUNE_BATCH8) ? 8
                     : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (small ? 8 : 16);
+  const unsigned cap = (pflags >> 8) & 0xFu;  // FA_PLAN_TUNE_BLOCKS_PER_CU(c)
+  t_dyn_lds = cap ? (160u * 1024u / cap) & ~1023u : 0;
   switch (vec_u) {
     case 1: return b_env == 16 ? launch_u<1, 16>(a, ntiles, deep, w, nt, st)
                                : launch_u<1, 8>(a, ntiles, deep, w, nt, st);
@@ -713,6 +730,7 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
     fa_plan_info ia{};
     build_tiles(s32, s64, 8 * kBlock, flags, &alt, &ia);
     p->ntiles_alt = (int)alt.size();
+    p->nscalar_alt = ia.ntiles_tail;
   }
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess && !tiles.empty()) {
@@ -901,11 +919,15 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
     a.tabw = (const float*)((const void**)table + 2 * n);
   }
   int ntiles = in.ntiles, vec_u = plan->vec_u;
+  a.nscalar = in.ntiles_tail;
   if (plan->d_tiles_alt && (weights || n < 16)) {
     a.tiles = plan->d_tiles_alt;
     ntiles = plan->ntiles_alt;
+    a.nscalar = plan->nscalar_alt;
     vec_u = 2;
   }
+  a.ntiles = ntiles;
+  a.xcd_swz = (plan->flags & FA_PLAN_TUNE_XCD) ? 1 : 0;
   hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st);
   if (table) {
     hipError_t e2 = hipFreeAsync(table, st);

@@ -76,6 +76,9 @@ extern "C" {
 #define FA_PLAN_TUNE_NO_NT 2u       /* tuning: plain (temporal) loads/stores   */
 #define FA_PLAN_TUNE_BATCH8 4u     /* tuning: force 8 clients per load batch  */
 #define FA_PLAN_TUNE_BATCH16 8u    /* tuning: force 16 clients per load batch */
+#define FA_PLAN_TUNE_XCD 16u       /* tuning: contiguous tile range per XCD   */
+/* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
+#define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
 
 /* One tensor (state_dict key) inside a flat bucket: [offset, offset+numel). */
 typedef struct fa_seg {
