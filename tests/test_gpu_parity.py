@@ -519,3 +519,25 @@ def test_checkpoint_from_device_bucket(tmp_path):
     for k, v in g.state_dict().items():
         assert torch.equal(fresh.state_dict()[k], v), k
     assert list(bucket_state_dict(g)) == list(g.state_dict())
+
+
+@pytest.mark.parametrize("flags", ["xcd", "cap3", "batch8", "batch16", "plain"])
+def test_tuning_flags_keep_bits(lib, flags):
+    from feddct_amd.workload import make_clients
+    man = load_manifest("wrnsl16_8_sf4_c10_proxy")
+    layout = BucketLayout.from_manifest(man)
+    n = 19
+    cl = make_clients(layout, man, range(n), DEV, synth.MODE_ADVERSARIAL)
+    ref32, ref64 = _reduce(lib, layout, cl)
+    fl = lib.FA_PLAN_GAPS_ARE_PADDING | {
+        "xcd": lib.FA_PLAN_TUNE_XCD, "cap3": lib.FA_PLAN_TUNE_BLOCKS_PER_CU(3),
+        "batch8": lib.FA_PLAN_TUNE_BATCH8, "batch16": lib.FA_PLAN_TUNE_BATCH16,
+        "plain": lib.FA_PLAN_TUNE_NO_NT}[flags]
+    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel, 1024, fl)
+    from feddct_amd.workload import Reducer
+    o32 = torch.full_like(ref32, np.nan)
+    o64 = torch.full_like(ref64, -1)
+    Reducer(layout, cl, o32, o64, plan=plan)()
+    torch.cuda.synchronize()
+    for (k, a), (_, b) in zip(buckets_to_state(layout, o32, o64), buckets_to_state(layout, ref32, ref64)):
+        assert bits_equal(a, b), (flags, k)
