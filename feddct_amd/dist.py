@@ -139,15 +139,19 @@ class ShardedAggregator:
             self.backend.partial_sum(c, self.local32, self.partial)
             works.append(dist.all_reduce(self.partial[lo:hi], op=dist.ReduceOp.SUM,
                                          group=self.group, async_op=True))
+        w64 = None
         if self.layout.i64_numel:
             for j, t in enumerate(self.local64):
                 self.stack64[j].copy_(t)
-            works.append(dist.all_gather_into_tensor(self.gather64, self.stack64,
-                                                     group=self.group, async_op=True))
-        for w in works:
+            w64 = dist.all_gather_into_tensor(self.gather64, self.stack64, group=self.group,
+                                              async_op=True)
+        # finish chunk c (/N_total) as soon as its exchange lands, while the
+        # exchanges of the later chunks are still on the wire
+        for w, (_, lo, hi) in zip(works, self.chunks):
             w.wait()
-        self.backend.divide(self.partial, float(self.n_total), self.out32)
-        if self.layout.i64_numel:
+            self.backend.divide(self.partial[lo:hi], float(self.n_total), self.out32[lo:hi])
+        if w64 is not None:
+            w64.wait()
             self.backend.reduce_i64([self.gather64[r] for r in self.rows64], self.out64)
 
 
