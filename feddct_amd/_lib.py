@@ -41,6 +41,10 @@ def FA_PLAN_TUNE_BLOCKS_PER_CU(c):
     return (int(c) & 0xF) << 8
 
 
+def FA_PLAN_TUNE_PERSIST(k):
+    return (int(k) & 0xF) << 12
+
+
 
 EXPORTS = [
     "fa_version", "fa_last_error", "fa_plan_create", "fa_plan_destroy",

@@ -382,10 +382,7 @@ __device__ void tile_scalar(KArgs& a, const Tile& t) {
 }
 
 template <int U, int B, bool DEEP, bool WEIGHTED, bool NT>
-__global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs args) {
-  (void)args;
-  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  int ti = blockIdx.x;
+__device__ __forceinline__ void run_tile(KArgs& a, int ti) {
   if (a.xcd_swz && ti >= a.nscalar) {
     // bijective: blocks i and i+8 share an XCD (round-robin dispatch); XCD x
     // gets the contiguous tile range [x*q + min(x,r), ...) of the vector tiles
@@ -399,6 +396,22 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs args) {
     else tile_vec<U, B, false, DEEP, WEIGHTED, NT>(a, t.start, t.count);
   } else {
     tile_scalar<WEIGHTED>(a, t);
+  }
+}
+
+// One workgroup per tile (default), or a persistent grid walking the table
+// with stride gridDim.x (tuning: FA_PLAN_TUNE_PERSIST).
+template <int U, int B, bool DEEP, bool WEIGHTED, bool NT>
+__global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs args) {
+  (void)args;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  if ((int)gridDim.x >= a.ntiles) {
+    run_tile<U, B, DEEP, WEIGHTED, NT>(a, blockIdx.x);
+  } else {
+    for (int ti = blockIdx.x; ti < a.ntiles; ti += gridDim.x) {
+      run_tile<U, B, DEEP, WEIGHTED, NT>(a, ti);
+      __syncthreads();  // scalar tiles exit threads early; keep the block in step
+    }
   }
 }
 
@@ -632,9 +645,12 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 thread_local size_t t_dyn_lds = 0;  // tuning: occupancy cap through dynamic LDS
 
+thread_local int t_grid_cap = 0;     // tuning: persistent grid size
+
 template <int U, int B, bool DEEP, bool W, bool NT>
 hipError_t launch_one(const ReduceArgs& a, int ntiles, hipStream_t st) {
-  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, NT>), dim3(ntiles), dim3(kBlock), t_dyn_lds,
+  const int grid = (t_grid_cap > 0 && t_grid_cap < ntiles) ? t_grid_cap : ntiles;
+  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, NT>), dim3(grid), dim3(kBlock), t_dyn_lds,
                      st, a);
   return hipGetLastError();
 }
@@ -660,6 +676,7 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
                     : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (small ? 8 : 16);
   const unsigned cap = (pflags >> 8) & 0xFu;  // FA_PLAN_TUNE_BLOCKS_PER_CU(c)
   t_dyn_lds = cap ? (160u * 1024u / cap) & ~1023u : 0;
+  t_grid_cap = 256 * (int)((pflags >> 12) & 0xFu);  // FA_PLAN_TUNE_PERSIST(k)
   switch (vec_u) {
     case 1: return b_env == 16 ? launch_u<1, 16>(a, ntiles, deep, w, nt, st)
                                : launch_u<1, 8>(a, ntiles, deep, w, nt, st);

@@ -79,6 +79,8 @@ extern "C" {
 #define FA_PLAN_TUNE_XCD 16u       /* tuning: contiguous tile range per XCD   */
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
 #define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
+/* tuning: persistent grid of 256*k workgroups striding over the tiles */
+#define FA_PLAN_TUNE_PERSIST(k) (((unsigned)(k) & 0xFu) << 12)
 
 /* One tensor (state_dict key) inside a flat bucket: [offset, offset+numel). */
 typedef struct fa_seg {
