@@ -27,13 +27,13 @@ are bound to pinned host buckets and staged through device buckets
 from __future__ import annotations
 
 import ctypes
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
 
 from . import _lib
-from .arena import ModuleArena, get_arena, state_owners
+from .arena import ModuleArena, get_arena
 from .layout import BucketLayout
 
 __all__ = ["server_aggregate", "server_aggregate_split", "aggregate_weighted", "client_weights",

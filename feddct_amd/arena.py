@@ -21,7 +21,7 @@ from typing import Dict, List, Tuple
 
 import torch
 
-from .layout import KIND_F32, KIND_I64, KIND_PACKF, BucketLayout
+from .layout import KIND_I64, KIND_PACKF, BucketLayout
 
 
 def state_owners(module: torch.nn.Module) -> Dict[str, Tuple[dict, str]]:

@@ -16,7 +16,7 @@ bit-identical to the one-shot path: each chunk is a tile subset.
 from __future__ import annotations
 
 import ctypes
-from typing import List, Optional, Sequence
+from typing import Sequence
 
 import torch
 

@@ -2,15 +2,12 @@
 shim) against the oracle and the reference's own outputs.  Bit-exact for
 every fp32 and int64 key (NaN positions must match; payloads are free)."""
 import ctypes
-import hashlib
-import json
-import os
 
 import numpy as np
 import pytest
 import torch
 
-from conftest import ROOT, load_manifest
+from conftest import load_manifest
 from feddct_amd import synth
 from feddct_amd.layout import BucketLayout
 from helpers import StateModule, bits_equal, buckets_to_state, states_to_buckets

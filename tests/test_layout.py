@@ -1,6 +1,5 @@
 """Bucket layouts of the reference's models (manifests committed from the
 reference's own model code by tests/golden/make_golden.py)."""
-import numpy as np
 import pytest
 import torch
 
