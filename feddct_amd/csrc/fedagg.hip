@@ -70,7 +70,7 @@ struct Tile {
 static_assert(sizeof(Tile) == 16, "tile is 16 B");
 
 constexpr int kBlock = 256;
-constexpr int kDefaultU = 1;  // float4 vectors per thread per client (tools/tune.py)
+constexpr int kDefaultU = 2;  // float4 vectors per thread per client (tools/tune.py)
 
 constexpr int kInline = FA_INLINE_CLIENTS;
 
@@ -531,8 +531,8 @@ struct fa_plan {
   Tile* d_tiles = nullptr;
   fa_plan_info info{};
   int vec_u = kDefaultU;
-  // auto plans (tile_elems == 0) also carry a 2048-float table: weighted or
-  // small-N reductions run it with 8-client batches (tools/tune.py sweep)
+  // auto plans (tile_elems == 0) also carry a 1024-float table, used for
+  // unweighted reductions over >= 64 clients (tools/tune.py sweep)
   Tile* d_tiles_alt = nullptr;
   int ntiles_alt = 0;
   int nscalar_alt = 0;
@@ -745,7 +745,7 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   set_kinds(p, tiles);
   if (autosel) {
     fa_plan_info ia{};
-    build_tiles(s32, s64, 8 * kBlock, flags, &alt, &ia);
+    build_tiles(s32, s64, 4 * kBlock, flags, &alt, &ia);
     p->ntiles_alt = (int)alt.size();
     p->nscalar_alt = ia.ntiles_tail;
   }
@@ -937,11 +937,11 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
   }
   int ntiles = in.ntiles, vec_u = plan->vec_u;
   a.nscalar = in.ntiles_tail;
-  if (plan->d_tiles_alt && (weights || n < 16)) {
+  if (plan->d_tiles_alt && !weights && n >= 64) {
     a.tiles = plan->d_tiles_alt;
     ntiles = plan->ntiles_alt;
     a.nscalar = plan->nscalar_alt;
-    vec_u = 2;
+    vec_u = 1;
   }
   a.ntiles = ntiles;
   a.xcd_swz = (plan->flags & FA_PLAN_TUNE_XCD) ? 1 : 0;
