@@ -390,8 +390,21 @@ def main():
     else:
         from feddct_amd.dist import ShardedAggregator
         agg = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
-                                N_CLIENTS * world, out32, out64, nchunks=args.chunks)
+                                N_CLIENTS * world, out32, out64, nchunks=args.chunks,
+                                final="reduce")
         t_step, wall = timed_launches(agg.step, args.steps, args.warmup, sync_group=group)
+        # the same round with the global state delivered to every GPU
+        a32, a64 = torch.zeros_like(out32), torch.zeros_like(out64)
+        agg_all = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
+                                    N_CLIENTS * world, a32, a64, nchunks=args.chunks,
+                                    final="allreduce")
+        t_all, _ = timed_launches(agg_all.step, max(10, args.steps // 2), 5, sync_group=group)
+        ta = torch.tensor([t_all], dtype=torch.float64, device=dev)
+        dist.all_reduce(ta, op=dist.ReduceOp.MAX)
+        extra["allreduce_mode"] = {
+            "mode": "client shards + RCCL all-reduce (global state on every GPU)",
+            "ms_per_step": round(float(ta.item()) * 1e3, 4),
+            "GBps": round(nbytes_rank * world / float(ta.item()) / 1e9, 2)}
         # kernel-only launch time for the roofline: the same reduce over this
         # rank's clients into scratch outputs (out32/out64 hold the round's result)
         kred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
@@ -426,7 +439,9 @@ def main():
             torch.cuda.synchronize()
             extra["parity"] = {"vs": f"exact single-GPU torch order over {N_CLIENTS * world} clients",
                                "max_ulp_fp32": ulp_dist(out32, ex32),
-                               "int64_bit_exact": bool(torch.equal(out64, ex64))}
+                               "max_abs_err_fp32": float((out32 - ex32).abs().max()),
+                               "int64_bit_exact": bool(torch.equal(out64, ex64)),
+                               "allreduce_mode_same_as_reduce_mode": bool(torch.equal(a32, out32))}
             if striped is not None:
                 striped["bit_exact"] = bool(torch.equal(s32, ex32) and torch.equal(s64, ex64))
                 extra["exact_mode"] = striped
@@ -451,7 +466,8 @@ def main():
                                "(82 fp32 + 16 int64 keys), unweighted mean (reference semantics)",
                    "clients_per_gpu": N_CLIENTS, "bytes_per_client": layout.state_bytes(),
                    "algorithmic_bytes_per_step": nbytes_rank * world,
-                   "parallelism": f"client-shard x{world}" if world > 1 else "single GPU"},
+                   "parallelism": (f"client-shard x{world}, chunked RCCL reduce to rank 0"
+                                   if world > 1 else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_us": round(t_kernel * 1e6, 2)},

@@ -106,11 +106,22 @@ class HipBackend:
 
 
 class ShardedAggregator:
-    """The cross-GPU round over pre-bound buckets (bench.py's N>1 step)."""
+    """The cross-GPU round over pre-bound buckets (bench.py's N>1 step).
+
+    ``final="reduce"`` (default): the north_star's final RCCL reduce — the
+    global state lands on ``root`` (the server), like the single-process
+    reference where the global model is one module; ``final="allreduce"``:
+    every rank gets it (reduce + the cross-GPU half of the broadcast)."""
 
     def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
                  local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
-                 out64: torch.Tensor, nchunks: int = 8, backend=None, group=None):
+                 out64: torch.Tensor, nchunks: int = 8, backend=None, group=None,
+                 final: str = "reduce", root: int = 0):
+        if final not in ("reduce", "allreduce"):
+            raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
+        self.final = final
+        self.root = root
+        self.rank = dist.get_rank(group)
         self.layout = layout
         self.local32, self.local64 = local32, local64
         self.n_total = n_total
@@ -135,24 +146,34 @@ class ShardedAggregator:
 
     def step(self) -> None:
         works = []
+        to_root = self.final == "reduce"
+        gdst = self.root if self.group is None else dist.get_global_rank(self.group, self.root)
         for c, (_, lo, hi) in enumerate(self.chunks):
             self.backend.partial_sum(c, self.local32, self.partial)
-            works.append(dist.all_reduce(self.partial[lo:hi], op=dist.ReduceOp.SUM,
+            if to_root:
+                works.append(dist.reduce(self.partial[lo:hi], dst=gdst, op=dist.ReduceOp.SUM,
                                          group=self.group, async_op=True))
+            else:
+                works.append(dist.all_reduce(self.partial[lo:hi], op=dist.ReduceOp.SUM,
+                                             group=self.group, async_op=True))
         w64 = None
         if self.layout.i64_numel:
             for j, t in enumerate(self.local64):
                 self.stack64[j].copy_(t)
             w64 = dist.all_gather_into_tensor(self.gather64, self.stack64, group=self.group,
                                               async_op=True)
+        has_result = not to_root or self.rank == self.root
         # finish chunk c (/N_total) as soon as its exchange lands, while the
         # exchanges of the later chunks are still on the wire
         for w, (_, lo, hi) in zip(works, self.chunks):
             w.wait()
-            self.backend.divide(self.partial[lo:hi], float(self.n_total), self.out32[lo:hi])
+            if has_result:
+                self.backend.divide(self.partial[lo:hi], float(self.n_total),
+                                    self.out32[lo:hi])
         if w64 is not None:
             w64.wait()
-            self.backend.reduce_i64([self.gather64[r] for r in self.rows64], self.out64)
+            if has_result:
+                self.backend.reduce_i64([self.gather64[r] for r in self.rows64], self.out64)
 
 
 # --------------------------------------------------------------------------
