@@ -419,7 +419,8 @@ def main():
             from feddct_amd.dist import StripedAggregator
             s32 = torch.zeros_like(out32)
             s64 = torch.zeros_like(out64)
-            sagg = StripedAggregator(layout, N_CLIENTS * world, s32, s64, group=group)
+            sagg = StripedAggregator(layout, N_CLIENTS * world, s32, s64, group=group,
+                                     final="reduce")
             lc32 = [c[0] for c in clients]
             lc64 = [c[1] for c in clients]
             ts, _ = timed_launches(lambda: sagg.step_device(lc32, lc64),

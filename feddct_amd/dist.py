@@ -231,8 +231,12 @@ class StripedAggregator:
     """
 
     def __init__(self, layout: BucketLayout, n_total: int, out32: torch.Tensor,
-                 out64: torch.Tensor, group=None, backend=None):
+                 out64: torch.Tensor, group=None, backend=None, final: str = "allreduce",
+                 root: int = 0):
         from .partition import i64_tiles, layout_tiles, split_tiles
+        if final not in ("reduce", "allreduce"):
+            raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
+        self.final, self.root = final, root
         self.layout = layout
         self.n_total = n_total
         self.out32, self.out64 = out32, out64
@@ -261,16 +265,17 @@ class StripedAggregator:
         return r if self.group is None else dist.get_global_rank(self.group, r)
 
     def _gather_stripes(self, ops):
-        """Every rank's stripe of out32 to every other rank (P2P into views)."""
+        """Finished stripes of out32 to every other rank ("allreduce") or to
+        the root only ("reduce"), P2P straight into out32 views."""
         me = self.rank
         for r in range(self.world):
             if r == me:
                 continue
             lo, hi = self.ranges[r]
-            if self.hi > self.lo:
+            if self.hi > self.lo and (self.final == "allreduce" or r == self.root):
                 ops.append(dist.P2POp(dist.isend, self.out32[self.lo:self.hi], self._peer(r),
                                       self.group))
-            if hi > lo:
+            if hi > lo and (self.final == "allreduce" or me == self.root):
                 ops.append(dist.P2POp(dist.irecv, self.out32[lo:hi], self._peer(r), self.group))
 
     def _run(self, ops):

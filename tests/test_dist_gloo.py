@@ -166,7 +166,7 @@ class OracleStripeBackend:
             out[o:o + m] = torch.from_numpy(O.mean_i64_trunc(x))
 
 
-def _striped_worker(rank, world, port, n_total, host, q):
+def _striped_worker(rank, world, port, n_total, host, q, final="allreduce"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from feddct_amd.dist import StripedAggregator
@@ -177,7 +177,7 @@ def _striped_worker(rank, world, port, n_total, host, q):
     info, tiles = layout_tiles(layout)
     lo, hi, _ = split_tiles(tiles, world, layout.f32_numel)[rank]
     agg = StripedAggregator(layout, n_total, out32, out64,
-                            backend=OracleStripeBackend(layout, lo, hi))
+                            backend=OracleStripeBackend(layout, lo, hi), final=final)
     if host:
         allb = [_bucket(layout, synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL))
                 for c in range(n_total)]
@@ -191,12 +191,15 @@ def _striped_worker(rank, world, port, n_total, host, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_total,host", [(2, 20, False), (3, 7, False), (2, 9, True)])
-def test_striped_round_is_exact_gloo(world, n_total, host):
+@pytest.mark.parametrize("world,n_total,host,final", [(2, 20, False, "allreduce"),
+                                                    (3, 7, False, "allreduce"),
+                                                    (2, 9, True, "allreduce"),
+                                                    (3, 7, False, "reduce")])
+def test_striped_round_is_exact_gloo(world, n_total, host, final):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_striped_worker, args=(r, world, port, n_total, host, q))
+    procs = [ctx.Process(target=_striped_worker, args=(r, world, port, n_total, host, q, final))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -207,7 +210,9 @@ def test_striped_round_is_exact_gloo(world, n_total, host):
     layout = BucketLayout.from_manifest(MAN)
     states = [synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL) for c in range(n_total)]
     exact = dict(O.aggregate_state(states))
-    for _, o32, o64 in res:  # every rank holds the full, exact global state
+    for rk, o32, o64 in res:  # every rank (or the root) holds the full, exact state
+        if final == "reduce" and rk != 0:
+            continue
         for s in layout.slots:
             src = o64 if s.kind == "i64" else o32
             got = src[s.offset:s.offset + s.numel].reshape(s.shape)
