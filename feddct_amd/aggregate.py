@@ -171,12 +171,51 @@ def server_aggregate(global_model, client_models):
     engine().reduce_modules(global_model, list(client_models))
 
 
+class _Pair(torch.nn.Module):
+    """A FedDCT client slot as one module: (main client, proxy) under the
+    keys "0." and "1.".  Binding a pair puts both halves' state in ONE bucket,
+    so a round is one launch; the per-key arithmetic is unchanged."""
+
+    def __init__(self, a, b):
+        super().__init__()
+        self.add_module("0", a)
+        self.add_module("1", b)
+
+
+def _pair(a, b) -> "_Pair":
+    """The cached pair wrapper of (a, b), kept on ``a`` (a reference cycle the
+    GC collects with the modules, no global registry)."""
+    cache = a.__dict__.setdefault("_fa_pairs", {})
+    p = cache.get(id(b))
+    if p is None or p._modules["1"] is not b:
+        p = cache[id(b)] = _Pair(a, b)
+    return p
+
+
 def server_aggregate_split(global_model_a, global_model_b, models_a, models_b):
     """train_feddct.py:34-56 / train_splitfed.py:34-56: main-client and proxy
-    (or client and server) halves reduced and broadcast independently."""
+    (or client and server) halves reduced and broadcast independently.
+
+    When every slot has both halves, each slot's pair is bound to one bucket
+    and both reductions + both broadcasts run as ONE launch.  Anything the
+    joint path would report differently from the reference (a missing or
+    mismatched key, extra keys) takes the two-call path, which reproduces the
+    reference's errors and their order exactly."""
     e = engine()
-    e.reduce_modules(global_model_a, list(models_a))
-    e.reduce_modules(global_model_b, list(models_b))
+    models_a, models_b = list(models_a), list(models_b)
+    if len(models_a) == len(models_b) and len(models_a) > 0:
+        try:
+            g = _pair(global_model_a, global_model_b)
+            pairs = [_pair(a, b) for a, b in zip(models_a, models_b)]
+            layout = e.layout_of(g)
+            arenas = [get_arena(p, layout) for p in pairs]
+            if not any(a.extra_keys for a in arenas):
+                e.reduce_modules(g, pairs)
+                return
+        except (KeyError, RuntimeError, TypeError):
+            pass  # fall through: the reference's own two-step semantics
+    e.reduce_modules(global_model_a, models_a)
+    e.reduce_modules(global_model_b, models_b)
 
 
 def client_weights(sizes) -> np.ndarray:

@@ -15,7 +15,6 @@ model's parameters), computed by three HIP launches over the two arenas
 from __future__ import annotations
 
 import ctypes
-from typing import Dict, Tuple
 
 import numpy as np
 import torch
@@ -114,14 +113,12 @@ class ProximalTerm:
         return _Prox.apply(self, *params)
 
 
-_TERMS: Dict[Tuple[int, int], ProximalTerm] = {}
-
-
 def proximal_term(client_model: torch.nn.Module, global_model: torch.nn.Module) -> torch.Tensor:
     """Σ_k ||w_k − w_t,k||₂ over zip(client.parameters(), global.parameters()),
-    differentiable w.r.t. both (train_fedprox.py:113-115)."""
-    key = (id(client_model), id(global_model))
-    t = _TERMS.get(key)
-    if t is None or not t.valid() or t.client_model is not client_model:
-        t = _TERMS[key] = ProximalTerm(client_model, global_model)
+    differentiable w.r.t. both (train_fedprox.py:113-115).  The bound term is
+    cached on the client module (no global registry)."""
+    cache = client_model.__dict__.setdefault("_fa_prox", {})
+    t = cache.get(id(global_model))
+    if t is None or t.global_model is not global_model or not t.valid():
+        t = cache[id(global_model)] = ProximalTerm(client_model, global_model)
     return t()

@@ -538,3 +538,26 @@ def test_tuning_flags_keep_bits(lib, flags):
     torch.cuda.synchronize()
     for (k, a), (_, b) in zip(buckets_to_state(layout, o32, o64), buckets_to_state(layout, ref32, ref64)):
         assert bits_equal(a, b), (flags, k)
+
+
+def test_split_joint_bucket_and_fallback_errors(golden):
+    from feddct_amd.feddct import server_aggregate
+    mm, pm = golden["manifest"]["main"], golden["manifest"]["proxy"]
+    n = 5
+    ms = _modules(mm, [synth.gen_state(mm, i, synth.MODE_ADVERSARIAL) for i in range(n)])
+    ps = _modules(pm, [synth.gen_state(pm, 100 + i, synth.MODE_ADVERSARIAL) for i in range(n)])
+    gm, gp = StateModule(mm).to(DEV), StateModule(pm).to(DEV)
+    server_aggregate(gm, gp, ms, ps)
+    # both halves of a slot live in one bucket: one launch per round
+    pair = ms[2]._fa_pairs[id(ps[2])]
+    buf = pair._fa_arena.f32
+    for t in list(ms[2].parameters()) + list(ps[2].parameters()):
+        assert buf.data_ptr() <= t.data_ptr() < buf.data_ptr() + buf.numel() * 4
+    torch.cuda.synchronize()
+    for k, v in gp.state_dict().items():
+        assert bits_equal(v.cpu().numpy(), golden["gold"][f"feddct/n5/proxy/{k}"]), k
+    # a main client missing a key: the reference's KeyError, unprefixed
+    bad = StateModule({"keys": mm["keys"][1:]}).to(DEV)
+    with pytest.raises(KeyError) as ei:
+        server_aggregate(gm, gp, ms[:2] + [bad], ps[:3])
+    assert ei.value.args[0] == mm["keys"][0]["key"]
