@@ -72,14 +72,17 @@ def timed_launches(fn, steps, warmup, sync_group=None):
     return e0.elapsed_time(e1) / 1e3 / steps, wall / steps
 
 
-def digest_of(layout, out32, out64):
+def digest_of(layout, out32, out64, prefix=""):
+    """SHA-256 of the keys under ``prefix`` (stripped), as tests/golden does."""
     import hashlib
     f = out32.cpu().numpy()
     i = out64.cpu().numpy()
     h = hashlib.sha256()
     for s in layout.slots:
+        if not s.key.startswith(prefix):
+            continue
         src = i if s.kind == "i64" else f
-        h.update(s.key.encode())
+        h.update(s.key[len(prefix):].encode())
         h.update(np.ascontiguousarray(src[s.offset:s.offset + s.numel]).tobytes())
     return h.hexdigest()
 
@@ -216,44 +219,51 @@ def other_configs(dev, steps=20):
     res = {}
 
     def run(name, parts, rot, digests):
+        """parts: [(manifest names joined in ONE layout, n, weights)] — a
+        FedDCT slot's main + proxy share one bucket (aggregate._Pair), so a
+        round is one launch."""
+        from feddct_amd.workload import joint_manifest
         sets = []
         for r in range(rot):
             reds = []
-            for lay_name, n, w in parts:
-                man = load_manifest(lay_name)
+            for names, n, w in parts:
+                mans = [load_manifest(x) for x in names]
+                prefixes = ("0.", "1.") if len(names) > 1 else ("",)
+                man = joint_manifest(mans, prefixes) if len(names) > 1 else mans[0]
                 lay = BucketLayout.from_manifest(man)
-                cl = make_clients(lay, man, range(n), dev)
+                cl = make_clients(lay, list(zip(mans, prefixes)), range(n), dev)
                 o32, o64 = torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])
-                reds.append((lay_name, lay, n, Reducer(lay, cl, o32, o64, weights=w), o32, o64))
+                reds.append((names, prefixes, lay, n, Reducer(lay, cl, o32, o64, weights=w),
+                             o32, o64))
             sets.append(reds)
         k = [0]
 
         def step():
             for r in sets[k[0] % rot]:
-                r[3]()
+                r[4]()
             k[0] += 1
         t, _ = timed_launches(step, steps, 3)
-        nbytes = sum(r[1].algorithmic_bytes(r[2]) for r in sets[0])
+        nbytes = sum(r[2].algorithmic_bytes(r[3]) for r in sets[0])
         out = {"GBps": round(nbytes / t / 1e9, 1), "us_per_step": round(t * 1e6, 1),
-               "algorithmic_bytes": nbytes, "rotated_sets": rot}
+               "algorithmic_bytes": nbytes, "rotated_sets": rot,
+               "launches_per_step": len(sets[0])}
         if digests:
             ok = True
-            for lay_name, lay, n, _, o32, o64 in sets[0]:
-                key = digests.get(lay_name)
-                if key:
-                    ok &= digest_of(lay, o32, o64) == dig[key]
+            for names, prefixes, lay, n, _, o32, o64 in sets[0]:
+                for nm, pf in zip(names, prefixes):
+                    ok &= digest_of(lay, o32, o64, pf) == dig[digests[nm]]
             out["bit_exact_vs_reference_digest"] = bool(ok)
         res[name] = out
 
-    run("cfg3_feddct_c10_n5", [("wrnsl16_8_sf4_c10_main", 5, None),
-                               ("wrnsl16_8_sf4_c10_proxy", 5, None)], 2,
+    run("cfg3_feddct_c10_n5", [(("wrnsl16_8_sf4_c10_main", "wrnsl16_8_sf4_c10_proxy"), 5, None)], 2,
         {"wrnsl16_8_sf4_c10_main": "feddct/wrnsl16_8_sf4_c10_main/n5",
          "wrnsl16_8_sf4_c10_proxy": "feddct/wrnsl16_8_sf4_c10_proxy/n5"})
     from feddct_amd.aggregate import client_weights as weights_from_sizes
     sizes = [2500 + 97 * ((7 * i) % 11) for i in range(20)]  # quantity-skewed shards
-    run("cfg4_fedprox_c100_n20_weighted", [("wrn16_8_c100", 20, weights_from_sizes(sizes))], 1, {})
-    run("cfg5_feddct_c100_n24_one_gpu", [("wrnsl16_8_sf4_c100_main", 24, None),
-                                         ("wrnsl16_8_sf4_c100_proxy", 24, None)], 1,
+    run("cfg4_fedprox_c100_n20_weighted", [(("wrn16_8_c100",), 20, weights_from_sizes(sizes))],
+        1, {})
+    run("cfg5_feddct_c100_n24_one_gpu", [(("wrnsl16_8_sf4_c100_main", "wrnsl16_8_sf4_c100_proxy"),
+                                          24, None)], 1,
         {"wrnsl16_8_sf4_c100_main": "feddct/wrnsl16_8_sf4_c100_main/n24",
          "wrnsl16_8_sf4_c100_proxy": "feddct/wrnsl16_8_sf4_c100_proxy/n24"})
     return res

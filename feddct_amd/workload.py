@@ -24,11 +24,23 @@ def load_manifest(name: str) -> dict:
         return json.load(f)
 
 
+def joint_manifest(manifests, prefixes=("0.", "1.")) -> dict:
+    """One layout for several models (FedDCT's main + proxy slot): the keys
+    of each under its prefix, in order — the layout of aggregate._Pair."""
+    keys = []
+    for m, p in zip(manifests, prefixes):
+        keys += [dict(e, key=p + e["key"]) for e in m["keys"]]
+    return {"name": "+".join(m.get("name", "?") for m in manifests), "keys": keys}
+
+
 def fill_client(layout: BucketLayout, manifest: dict, f32: torch.Tensor, i64: torch.Tensor,
-                client: int, mode: int = synth.MODE_REALISTIC) -> None:
+                client: int, mode: int = synth.MODE_REALISTIC, prefix: str = "") -> None:
+    """Client ``client``'s synthetic state for ``manifest``'s keys (key index
+    = position in that manifest), written at ``layout``'s slots of
+    ``prefix + key``."""
     stream = ctypes.c_void_p(torch.cuda.current_stream(f32.device).cuda_stream)
     for j, e in enumerate(manifest["keys"]):
-        s = layout.by_key[e["key"]]
+        s = layout.by_key[prefix + e["key"]]
         if s.alias_of is not None:
             continue
         if s.kind == KIND_I64:
@@ -40,13 +52,16 @@ def fill_client(layout: BucketLayout, manifest: dict, f32: torch.Tensor, i64: to
                                                   mu, sigma, mode, stream), "fa_synth_fill_f32")
 
 
-def make_clients(layout: BucketLayout, manifest: dict, clients, device,
+def make_clients(layout: BucketLayout, manifest, clients, device,
                  mode: int = synth.MODE_REALISTIC) -> List[Tuple[torch.Tensor, torch.Tensor]]:
+    """``manifest`` may be a list of (manifest, prefix) for a joint layout."""
+    parts = manifest if isinstance(manifest, list) else [(manifest, "")]
     out = []
     for c in clients:
         f32 = torch.zeros(max(layout.f32_numel, 64), dtype=torch.float32, device=device)
         i64 = torch.zeros(max(layout.i64_numel, 1), dtype=torch.int64, device=device)
-        fill_client(layout, manifest, f32, i64, c, mode)
+        for m, prefix in parts:
+            fill_client(layout, m, f32, i64, c, mode, prefix)
         out.append((f32, i64))
     return out
 

@@ -561,3 +561,19 @@ def test_split_joint_bucket_and_fallback_errors(golden):
     with pytest.raises(KeyError) as ei:
         server_aggregate(gm, gp, ms[:2] + [bad], ps[:3])
     assert ei.value.args[0] == mm["keys"][0]["key"]
+
+
+@pytest.mark.parametrize("tag,n", [("c10", 5), ("c100", 24)])
+def test_full_size_joint_feddct_digest(lib, golden, tag, n):
+    """FedDCT slot = main + proxy in ONE bucket (aggregate._Pair layout): one
+    launch reproduces both reference digests."""
+    from feddct_amd.workload import joint_manifest, make_clients
+    mm = load_manifest(f"wrnsl16_8_sf4_{tag}_main")
+    pm = load_manifest(f"wrnsl16_8_sf4_{tag}_proxy")
+    layout = BucketLayout.from_manifest(joint_manifest([mm, pm]))
+    cl = make_clients(layout, [(mm, "0."), (pm, "1.")], range(n), DEV)
+    out32, out64 = _reduce(lib, layout, cl)
+    state = buckets_to_state(layout, out32, out64)
+    for pf, lay in (("0.", "main"), ("1.", "proxy")):
+        part = [(k[2:], v) for k, v in state if k.startswith(pf)]
+        assert O.state_digest(part) == golden["digests"][f"feddct/wrnsl16_8_sf4_{tag}_{lay}/n{n}"]
