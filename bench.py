@@ -441,6 +441,31 @@ def main():
             striped = {"mode": "column-striped exact (grouped P2P stripe exchange over RCCL)",
                        "ms_per_step": round(ts * 1e3, 3),
                        "GBps": round(nbytes_rank * world / ts / 1e9, 2)}
+            # host ingress (the north_star's CPU-tensor clients): each GPU
+            # uploads only ITS column stripe of every client over its own PCIe
+            # link, reduces it exactly, stripes meet on the root
+            from feddct_amd.workload import fill_client
+            h32 = torch.zeros_like(out32)
+            h64 = torch.zeros_like(out64)
+            hagg = StripedAggregator(layout, N_CLIENTS * world, h32, h64, group=group,
+                                     final="reduce")
+            lo, hi = hagg.lo, hagg.hi
+            scratch32, scratch64 = torch.zeros_like(out32), torch.zeros_like(out64)
+            stripes, host64 = [], []
+            for c in range(N_CLIENTS * world):
+                fill_client(layout, manifest, scratch32, scratch64, c)
+                stripes.append(scratch32[lo:hi].cpu().pin_memory())
+                host64.append(scratch64.cpu().pin_memory())
+            th, _ = timed_launches(lambda: hagg.step_host(stripes, host64), 3, 1,
+                                   sync_group=group)
+            tt = torch.tensor([th], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            th = float(tt.item())
+            striped_host = {"mode": "column-striped exact, host ingress (stripe-only H2D per GPU)",
+                            "ms_per_step": round(th * 1e3, 3),
+                            "GBps": round(nbytes_rank * world / th / 1e9, 2),
+                            "H2D_bytes_per_gpu": int((hi - lo) * 4 * N_CLIENTS * world)}
+            del stripes, host64
         if rank == 0 and not args.kernel_only:
             # accuracy of the re-associated cross-GPU sum vs the exact order
             allc = make_clients(layout, manifest, range(N_CLIENTS * world), dev)
@@ -456,6 +481,8 @@ def main():
             if striped is not None:
                 striped["bit_exact"] = bool(torch.equal(s32, ex32) and torch.equal(s64, ex64))
                 extra["exact_mode"] = striped
+                striped_host["bit_exact"] = bool(torch.equal(h32, ex32) and torch.equal(h64, ex64))
+                extra["exact_mode_host_ingress"] = striped_host
             del allc
 
     achieved = nbytes_rank / t_kernel / 1e9
