@@ -100,8 +100,8 @@ def test_special_values_and_subnormals(lib):
     assert got.view(np.uint32)[0] == 0
 
 
-def test_weighted_matches_oracle(lib):
-    n = 20
+@pytest.mark.parametrize("n", [3, 20, 200])
+def test_weighted_matches_oracle(lib, n):
     man = _rand_manifest(None, SIZES)
     layout = BucketLayout.from_manifest(man)
     states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
