@@ -35,6 +35,7 @@ FA_PLAN_TUNE_NO_NT = 2
 FA_PLAN_TUNE_BATCH8 = 4
 FA_PLAN_TUNE_BATCH16 = 8
 FA_PLAN_TUNE_XCD = 16
+FA_PLAN_TUNE_WAVE_CONTIG = 32
 
 
 def FA_PLAN_TUNE_BLOCKS_PER_CU(c):

@@ -113,6 +113,8 @@ __device__ __forceinline__ float cw(KArgs& a, int i) {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+constexpr unsigned kWaveContig = 0x200u;  // internal a.flags bit (FA_PLAN_TUNE_WAVE_CONTIG)
+
 // c10::utils::CeilLog2 / ATen multi_row_sum level power
 __host__ __device__ inline int ceil_log2_i(int64_t n) {
   if (n <= 1) return 0;
@@ -256,7 +258,11 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
   bool ok[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int v = threadIdx.x + u * kBlock;
+    // block-strided (default): lane t takes vectors t, t+256, ...; wave-
+    // contiguous (tuning flag): each wave owns U*1 KiB of adjacent bytes
+    const int v = (a.flags & kWaveContig)
+                      ? (int)(threadIdx.x & ~63u) * U + u * 64 + (int)(threadIdx.x & 63u)
+                      : (int)threadIdx.x + u * kBlock;
     off[u] = start + 4 * (int64_t)v;
     ok[u] = FULL || 4 * v < count;
     A.l0[u] = A.l1[u] = A.l2[u] = A.l3[u] = f4{0.f, 0.f, 0.f, 0.f};
@@ -889,7 +895,8 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
   a.out32 = out32;
   a.out64 = out64;
   a.n = n;
-  a.flags = flags | (weights ? 0x100u : 0u);
+  a.flags = flags | (weights ? 0x100u : 0u) |
+            ((plan->flags & FA_PLAN_TUNE_WAVE_CONTIG) ? kWaveContig : 0u);
   const bool need32 = plan->has32, need64 = plan->has64;
   if (need32) {
     if (!c32 || !out32) return set_err(FA_E_INVAL, "fa_reduce: fp32 buckets required");

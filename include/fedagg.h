@@ -77,6 +77,7 @@ extern "C" {
 #define FA_PLAN_TUNE_BATCH8 4u     /* tuning: force 8 clients per load batch  */
 #define FA_PLAN_TUNE_BATCH16 8u    /* tuning: force 16 clients per load batch */
 #define FA_PLAN_TUNE_XCD 16u       /* tuning: contiguous tile range per XCD   */
+#define FA_PLAN_TUNE_WAVE_CONTIG 32u /* tuning: each wave reads adjacent KiBs  */
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
 #define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
 /* tuning: persistent grid of 256*k workgroups striding over the tiles */

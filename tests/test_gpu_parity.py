@@ -518,7 +518,8 @@ def test_checkpoint_from_device_bucket(tmp_path):
     assert list(bucket_state_dict(g)) == list(g.state_dict())
 
 
-@pytest.mark.parametrize("flags", ["xcd", "cap3", "batch8", "batch16", "plain", "persist"])
+@pytest.mark.parametrize("flags", ["xcd", "cap3", "batch8", "batch16", "plain", "persist",
+                                   "wavecontig"])
 def test_tuning_flags_keep_bits(lib, flags):
     from feddct_amd.workload import make_clients
     man = load_manifest("wrnsl16_8_sf4_c10_proxy")
@@ -529,8 +530,10 @@ def test_tuning_flags_keep_bits(lib, flags):
     fl = lib.FA_PLAN_GAPS_ARE_PADDING | {
         "xcd": lib.FA_PLAN_TUNE_XCD, "cap3": lib.FA_PLAN_TUNE_BLOCKS_PER_CU(3),
         "batch8": lib.FA_PLAN_TUNE_BATCH8, "batch16": lib.FA_PLAN_TUNE_BATCH16,
-        "plain": lib.FA_PLAN_TUNE_NO_NT, "persist": lib.FA_PLAN_TUNE_PERSIST(1)}[flags]
-    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel, 1024, fl)
+        "plain": lib.FA_PLAN_TUNE_NO_NT, "persist": lib.FA_PLAN_TUNE_PERSIST(1),
+        "wavecontig": lib.FA_PLAN_TUNE_WAVE_CONTIG}[flags]
+    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
+                    4096 if flags == "wavecontig" else 1024, fl)
     from feddct_amd.workload import Reducer
     o32 = torch.full_like(ref32, np.nan)
     o64 = torch.full_like(ref64, -1)

@@ -24,14 +24,14 @@ def main():
     nbytes = lay.algorithmic_bytes(n)
     base = _lib.FA_PLAN_GAPS_ARE_PADDING | _lib.FA_PLAN_TUNE_BATCH16
     variants = []
-    for tile in (1024, 2048):
-        for xcd in (False,):
-            for cap in (0, 4, 6, 8, 12):  # here: persistent grid = 256 * cap (0 = one WG per tile)
-                fl = base | (_lib.FA_PLAN_TUNE_XCD if xcd else 0) | _lib.FA_PLAN_TUNE_PERSIST(cap)
+    for tile in (2048, 4096):
+        for xcd in (False, True):  # here: wave-contiguous mapping
+            for cap in (0,):
+                fl = base | (_lib.FA_PLAN_TUNE_WAVE_CONTIG if xcd else 0)
                 plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
                                  tile_elems=tile, flags=fl)
                 o32, o64 = torch.zeros_like(clients[0][0]), torch.zeros_like(clients[0][1])
-                variants.append((f"T{tile}_persist{cap}",
+                variants.append((f"T{tile}_{'wavecontig' if xcd else 'strided'}",
                                  Reducer(lay, clients, o32, o64, plan=plan), o32, o64))
     times = {v[0]: [] for v in variants}
     for _ in range(rounds):
