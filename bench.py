@@ -131,9 +131,14 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
 
     mods = [to_module(f, i) for f, i in clients]
     g = Holder()
-    t_loop, reps = time_call(lambda: reference_loop(g, mods), 5, budget_s * 0.8)
+    t_loop, reps = time_call(lambda: reference_loop(g, mods), 5, budget_s * 0.5)
     states = [m.state_dict() for m in mods]
-    t_core, _ = time_call(lambda: arithmetic_core(states), 3, budget_s * 0.2)
+    t_core, _ = time_call(lambda: arithmetic_core(states), 3, budget_s * 0.1)
+    # the same on one thread (SURVEY.md §8 d asks for both)
+    torch.set_num_threads(1)
+    t_loop1, reps1 = time_call(lambda: reference_loop(g, mods), 3, budget_s * 0.3)
+    t_core1, _ = time_call(lambda: arithmetic_core(states), 3, budget_s * 0.1)
+    torch.set_num_threads(threads)
     nbytes = layout.algorithmic_bytes(len(clients))
     return {"value": round(nbytes / t_loop / 1e9, 3), "unit": "GB/s", "cores": threads,
             "kind": "port",
@@ -143,7 +148,9 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
                        f"arithmetic-only stack+mean {t_core * 1e3:.1f} ms "
                        f"({nbytes / t_core / 1e9:.2f} GB/s)"),
             "loop_ms": round(t_loop * 1e3, 2), "core_ms": round(t_core * 1e3, 2),
-            "cpu": _cpu_model()}
+            "one_thread": {"loop_ms": round(t_loop1 * 1e3, 2), "core_ms": round(t_core1 * 1e3, 2),
+                           "loop_GBps": round(nbytes / t_loop1 / 1e9, 3), "runs": reps1},
+            "host_cpus": os.cpu_count(), "cpu": _cpu_model()}
 
 
 def _cpu_model():
