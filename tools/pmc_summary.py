@@ -37,6 +37,11 @@ def counter_per_dispatch(d, counter):
 
 def main():
     trace_dir, fetch_dir, write_dir, out = sys.argv[1:5]
+    bench_line = None
+    if len(sys.argv) > 5 and os.path.exists(sys.argv[5]):
+        for line in open(sys.argv[5]):
+            if line.startswith("{"):
+                bench_line = json.loads(line)
     stats = [r for r in rows(trace_dir, "*kernel_stats.csv") if KERNEL in r["Name"]]
     fetch = counter_per_dispatch(fetch_dir, "FETCH_SIZE")
     write = counter_per_dispatch(write_dir, "WRITE_SIZE")
@@ -54,6 +59,10 @@ def main():
         "hbm_bytes_per_launch": None if fk is None or wk is None else 2 * fk * 1024 + wk * 1024,
         "algorithmic_bytes_per_launch": 20 * 43888744 + 43888744,
         "correction": "FETCH_SIZE x2 (gfx950 wide-stream half count), KiB x1024",
+        # the HIP-event launch time bench.py measured inside the profiled run
+        "bench_kernel_us_same_run": (bench_line or {}).get("roofline", {}).get("kernel_us"),
+        "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --kernel-only "
+                   "--no-cpu-baseline --steps 100 --warmup 100",
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
