@@ -24,6 +24,22 @@ import torch
 from .layout import KIND_I64, KIND_PACKF, BucketLayout
 
 
+# Structure generation: bumped by torch's global registration hooks whenever
+# any module registers a parameter, buffer or submodule.  An arena re-checks
+# its module's key set only when this moved since it last looked, so the
+# per-call validity check stays O(tensors) with no module-tree walk.
+_STRUCT_GEN = [0]
+
+
+def _bump(*_args, **_kw):
+    _STRUCT_GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump)
+torch.nn.modules.module.register_module_buffer_registration_hook(_bump)
+torch.nn.modules.module.register_module_module_registration_hook(_bump)
+
+
 def state_owners(module: torch.nn.Module) -> Dict[str, Tuple[dict, str]]:
     """state_dict key → (the dict holding the tensor, name), in state_dict
     registration order (parameters then persistent buffers per module)."""
@@ -77,6 +93,8 @@ class ModuleArena:
         # keys the module has beyond the layout: the reference's broadcast
         # load_state_dict(strict=True) rejects such a client (train_fedavg.py:149)
         self.extra_keys = [k for k in tensors if k not in layout.by_key]
+        self._keyset = list(tensors.keys())
+        self._gen = _STRUCT_GEN[0]
         self.f32, self.i64 = alloc_buckets(layout, self.device, pinned)
         self._checks: List[tuple] = []
         self._packed: List[tuple] = []
@@ -96,6 +114,12 @@ class ModuleArena:
         self.module_ref = module
 
     def valid(self) -> bool:
+        if self._gen != _STRUCT_GEN[0]:
+            # something somewhere registered a tensor/module: is it ours?
+            m = self.module_ref
+            if list(state_owners(m).keys()) != self._keyset:
+                return False
+            self._gen = _STRUCT_GEN[0]
         for d, name, t, ptr in self._checks:
             if d.get(name) is not t or t.data_ptr() != ptr:
                 return False

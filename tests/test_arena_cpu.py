@@ -100,3 +100,22 @@ def test_empty_client_list_like_torch_stack():
     from feddct_amd.aggregate import server_aggregate
     with pytest.raises(RuntimeError, match="non-empty"):
         server_aggregate(net(), [])
+
+
+def test_structure_change_after_binding_is_seen():
+    """A buffer registered after binding changes the key set: the arena turns
+    invalid and the engine's layout picks the new key up (the reference's
+    per-call state_dict() would see it)."""
+    from feddct_amd.aggregate import Engine
+    m = net()
+    e = Engine()
+    L = e.layout_of(m)
+    a = get_arena(m, L)
+    assert a.valid() and e.layout_of(m) is L
+    other = torch.nn.Linear(2, 2)  # registering elsewhere bumps the generation only
+    assert a.valid()
+    m[1].register_buffer("extra_stat", torch.ones(3))
+    assert not a.valid()
+    L2 = e.layout_of(m)
+    assert "1.extra_stat" in L2.keys and L2 is not L
+    del other

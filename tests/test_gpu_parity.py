@@ -618,3 +618,26 @@ def test_distance_to_torch_gpu_mean(lib, record_property):
     print(f"vs torch GPU mean: bit-identical {same}/{total}, max ULP {worst_ulp}, "
           f"max error {worst_rel:.2f} eps x mean|x|")
     assert worst_rel <= 2 * n
+
+
+def test_shim_empty_and_unit_tensors():
+    """Keys with no elements or one element (shape [0], [1,1], []) as the
+    reference's stack().mean(0) handles them."""
+    from feddct_amd.fedavg import server_aggregate
+    man = {"keys": [{"key": "e", "shape": [0], "dtype": "float32"},
+                    {"key": "u", "shape": [1, 1], "dtype": "float32"},
+                    {"key": "s", "shape": [], "dtype": "float32"},
+                    {"key": "w", "shape": [37], "dtype": "float32"},
+                    {"key": "e64", "shape": [0], "dtype": "int64"}]}
+    n = 9
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    g = StateModule(man).to(DEV)
+    clients = _modules(man, states)
+    server_aggregate(g, clients)
+    torch.cuda.synchronize()
+    cpu = [StateModule(man).load_numpy(s) for s in states]
+    for k, v in g.state_dict().items():
+        ref = torch.stack([c.state_dict()[k].float() for c in cpu], 0).mean(0)
+        want = cpu[0].state_dict()[k].clone()
+        want.copy_(ref)
+        assert v.shape == want.shape and torch.equal(v.cpu(), want), k
