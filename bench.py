@@ -276,6 +276,47 @@ def other_configs(dev, steps=20):
     return res
 
 
+def exact_modes(layout, manifest, clients, out32, out64, world, group, dev, nbytes_rank,
+                steps):
+    """N>1: the exact column-striped mode (feddct_amd/dist.py),
+    with device-resident client shards and with host ingress."""
+    from feddct_amd.dist import StripedAggregator
+    from feddct_amd.workload import fill_client
+    n_total = N_CLIENTS * world
+
+    def timed_max(fn, k, w):
+        t, _ = timed_launches(fn, k, w, sync_group=group)
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    s32, s64 = torch.zeros_like(out32), torch.zeros_like(out64)
+    sagg = StripedAggregator(layout, n_total, s32, s64, group=group, final="reduce")
+    lc32, lc64 = [c[0] for c in clients], [c[1] for c in clients]
+    ts = timed_max(lambda: sagg.step_device(lc32, lc64), steps, 2)
+    striped = {"mode": "column-striped exact (grouped P2P stripe exchange over RCCL)",
+               "ms_per_step": round(ts * 1e3, 3),
+               "GBps": round(nbytes_rank * world / ts / 1e9, 2)}
+    # host ingress (the north_star's CPU-tensor clients): each GPU uploads only
+    # ITS column stripe of every client over its own PCIe link, reduces it
+    # exactly, the stripes meet on the root
+    h32, h64 = torch.zeros_like(out32), torch.zeros_like(out64)
+    hagg = StripedAggregator(layout, n_total, h32, h64, group=group, final="reduce")
+    lo, hi = hagg.lo, hagg.hi
+    scratch32, scratch64 = torch.zeros_like(out32), torch.zeros_like(out64)
+    stripes, host64 = [], []
+    for c in range(n_total):
+        fill_client(layout, manifest, scratch32, scratch64, c)
+        stripes.append(scratch32[lo:hi].cpu().pin_memory())
+        host64.append(scratch64.cpu().pin_memory())
+    th = timed_max(lambda: hagg.step_host(stripes, host64), 3, 1)
+    striped_host = {"mode": "column-striped exact, host ingress (stripe-only H2D per GPU)",
+                    "ms_per_step": round(th * 1e3, 3),
+                    "GBps": round(nbytes_rank * world / th / 1e9, 2),
+                    "H2D_bytes_per_gpu": int((hi - lo) * 4 * n_total)}
+    return striped, striped_host, (s32, s64, h32, h64)
+
+
 def _holder_class(layout):
     class Holder(torch.nn.Module):
         def __init__(self):
@@ -411,17 +452,23 @@ def main():
                                 final="reduce")
         t_step, wall = timed_launches(agg.step, args.steps, args.warmup, sync_group=group)
         # the same round with the global state delivered to every GPU
+        # (extras are guarded: an error every rank hits alike is reported in
+        # the line instead of losing the headline)
         a32, a64 = torch.zeros_like(out32), torch.zeros_like(out64)
-        agg_all = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
-                                    N_CLIENTS * world, a32, a64, nchunks=args.chunks,
-                                    final="allreduce")
-        t_all, _ = timed_launches(agg_all.step, max(10, args.steps // 2), 5, sync_group=group)
-        ta = torch.tensor([t_all], dtype=torch.float64, device=dev)
-        dist.all_reduce(ta, op=dist.ReduceOp.MAX)
-        extra["allreduce_mode"] = {
-            "mode": "client shards + RCCL all-reduce (global state on every GPU)",
-            "ms_per_step": round(float(ta.item()) * 1e3, 4),
-            "GBps": round(nbytes_rank * world / float(ta.item()) / 1e9, 2)}
+        try:
+            agg_all = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
+                                        N_CLIENTS * world, a32, a64, nchunks=args.chunks,
+                                        final="allreduce")
+            t_all, _ = timed_launches(agg_all.step, max(10, args.steps // 2), 5,
+                                      sync_group=group)
+            ta = torch.tensor([t_all], dtype=torch.float64, device=dev)
+            dist.all_reduce(ta, op=dist.ReduceOp.MAX)
+            extra["allreduce_mode"] = {
+                "mode": "client shards + RCCL all-reduce (global state on every GPU)",
+                "ms_per_step": round(float(ta.item()) * 1e3, 4),
+                "GBps": round(nbytes_rank * world / float(ta.item()) / 1e9, 2)}
+        except Exception as e:  # noqa: BLE001
+            extra["allreduce_mode"] = {"error": repr(e)}
         # kernel-only launch time for the roofline: the same reduce over this
         # rank's clients into scratch outputs (out32/out64 hold the round's result)
         kred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
@@ -431,48 +478,14 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_step = float(tt.item())
         # the exact (column-striped) mode on the same client placement
-        striped = None
+        striped = striped_host = None
         if not args.kernel_only and not args.no_exact:
-            from feddct_amd.dist import StripedAggregator
-            s32 = torch.zeros_like(out32)
-            s64 = torch.zeros_like(out64)
-            sagg = StripedAggregator(layout, N_CLIENTS * world, s32, s64, group=group,
-                                     final="reduce")
-            lc32 = [c[0] for c in clients]
-            lc64 = [c[1] for c in clients]
-            ts, _ = timed_launches(lambda: sagg.step_device(lc32, lc64),
-                                   max(3, args.steps // 10), 2, sync_group=group)
-            tt = torch.tensor([ts], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            ts = float(tt.item())
-            striped = {"mode": "column-striped exact (grouped P2P stripe exchange over RCCL)",
-                       "ms_per_step": round(ts * 1e3, 3),
-                       "GBps": round(nbytes_rank * world / ts / 1e9, 2)}
-            # host ingress (the north_star's CPU-tensor clients): each GPU
-            # uploads only ITS column stripe of every client over its own PCIe
-            # link, reduces it exactly, stripes meet on the root
-            from feddct_amd.workload import fill_client
-            h32 = torch.zeros_like(out32)
-            h64 = torch.zeros_like(out64)
-            hagg = StripedAggregator(layout, N_CLIENTS * world, h32, h64, group=group,
-                                     final="reduce")
-            lo, hi = hagg.lo, hagg.hi
-            scratch32, scratch64 = torch.zeros_like(out32), torch.zeros_like(out64)
-            stripes, host64 = [], []
-            for c in range(N_CLIENTS * world):
-                fill_client(layout, manifest, scratch32, scratch64, c)
-                stripes.append(scratch32[lo:hi].cpu().pin_memory())
-                host64.append(scratch64.cpu().pin_memory())
-            th, _ = timed_launches(lambda: hagg.step_host(stripes, host64), 3, 1,
-                                   sync_group=group)
-            tt = torch.tensor([th], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            th = float(tt.item())
-            striped_host = {"mode": "column-striped exact, host ingress (stripe-only H2D per GPU)",
-                            "ms_per_step": round(th * 1e3, 3),
-                            "GBps": round(nbytes_rank * world / th / 1e9, 2),
-                            "H2D_bytes_per_gpu": int((hi - lo) * 4 * N_CLIENTS * world)}
-            del stripes, host64
+            try:
+                striped, striped_host, (s32, s64, h32, h64) = exact_modes(
+                    layout, manifest, clients, out32, out64, world, group, dev, nbytes_rank,
+                    max(3, min(5, args.steps // 10)))
+            except Exception as e:  # noqa: BLE001
+                extra["exact_mode"] = {"error": repr(e)}
         if rank == 0 and not args.kernel_only:
             # accuracy of the re-associated cross-GPU sum vs the exact order
             allc = make_clients(layout, manifest, range(N_CLIENTS * world), dev)
@@ -488,6 +501,7 @@ def main():
             if striped is not None:
                 striped["bit_exact"] = bool(torch.equal(s32, ex32) and torch.equal(s64, ex64))
                 extra["exact_mode"] = striped
+            if striped_host is not None:
                 striped_host["bit_exact"] = bool(torch.equal(h32, ex32) and torch.equal(h64, ex64))
                 extra["exact_mode_host_ingress"] = striped_host
             del allc
