@@ -7,9 +7,9 @@ in.  Small CNN, synthetic CIFAR-shaped data, everything on the GPU.
 
 Each round: every client slot trains locally (SGD, optional FedProx term),
 then ``server_aggregate(global_model, client_models)`` replaces the
-reference's loop of state_dict() / stack / mean / load_state_dict.  With
-``--check`` the global model is compared bit-for-bit with the reference
-arithmetic restated on CPU (oracle/torch_mirror.py) every round.
+reference's loop of state_dict() / stack / mean / load_state_dict.
+(tests/test_gpu_e2e.py runs this loop with a per-round bit-exactness check
+against the reference arithmetic.)
 """
 from __future__ import annotations
 
@@ -45,7 +45,9 @@ class SmallNet(nn.Module):
         return self.fc(x)
 
 
-def run(rounds=3, clients=4, steps=5, mu=0.0, check=False, seed=0, device="cuda"):
+def run(rounds=3, clients=4, steps=5, mu=0.0, check=None, seed=0, device="cuda"):
+    """``check(snapshot, global_model, client_models) -> dict`` (optional) is
+    called after every aggregation with the clients' pre-round CPU states."""
     torch.manual_seed(seed)
     dev = torch.device(device)
     global_model = SmallNet().to(dev)
@@ -74,16 +76,7 @@ def run(rounds=3, clients=4, steps=5, mu=0.0, check=False, seed=0, device="cuda"
         t2 = time.perf_counter()
         entry = {"round": r, "train_s": round(t1 - t0, 4), "aggregate_ms": round((t2 - t1) * 1e3, 3)}
         if check:
-            from oracle.torch_mirror import arithmetic_core
-            ref = arithmetic_core(snap)
-            ok = True
-            for k, v in global_model.state_dict().items():
-                want = v.detach().cpu().clone()
-                want.copy_(ref[k])          # load_state_dict's copy_ into the key's dtype
-                ok &= torch.equal(v.cpu(), want)
-                for m in client_models:
-                    ok &= torch.equal(m.state_dict()[k], v)
-            entry["bit_exact_vs_reference"] = bool(ok)
+            entry.update(check(snap, global_model, client_models))
         log.append(entry)
     return log
 
@@ -94,9 +87,8 @@ def main():
     ap.add_argument("--clients", type=int, default=4)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--mu", type=float, default=0.0)
-    ap.add_argument("--check", action="store_true")
     a = ap.parse_args()
-    for e in run(a.rounds, a.clients, a.steps, a.mu, a.check):
+    for e in run(a.rounds, a.clients, a.steps, a.mu):
         print(e)
 
 

@@ -12,8 +12,22 @@ pytestmark = pytest.mark.gpu
 sys.path.insert(0, os.path.join(ROOT, "examples"))
 
 
+def _check(snap, global_model, client_models):
+    import torch
+    from oracle.torch_mirror import arithmetic_core
+    ref = arithmetic_core(snap)
+    ok = True
+    for k, v in global_model.state_dict().items():
+        want = v.detach().cpu().clone()
+        want.copy_(ref[k])  # load_state_dict's copy_ into the key's dtype
+        ok &= torch.equal(v.cpu(), want)
+        for m in client_models:
+            ok &= torch.equal(m.state_dict()[k], v)
+    return {"bit_exact_vs_reference": bool(ok)}
+
+
 @pytest.mark.parametrize("mu", [0.0, 0.01])
 def test_round_loop_bit_exact(mu):
     from fedavg_loop import run
-    log = run(rounds=3, clients=5, steps=3, mu=mu, check=True)
+    log = run(rounds=3, clients=5, steps=3, mu=mu, check=_check)
     assert all(e["bit_exact_vs_reference"] for e in log), log
