@@ -276,6 +276,50 @@ def other_configs(dev, steps=20):
     return res
 
 
+def cfg1_host_resident(dev, reps=5):
+    """BASELINE config 1's shape — FedAvg, 2 clients, wide_resnet16_8 C10,
+    modules in HOST memory — through the drop-in server_aggregate (pinned
+    arenas, chunked H2D / reduce / D2H incl. the broadcast back into both
+    clients), checked against the reference digest."""
+    from feddct_amd.aggregate import server_aggregate
+    man = load_manifest("wrn16_8_c10")
+    layout = BucketLayout.from_manifest(man)
+    Holder = _holder_class(layout)
+    n = 2
+    dev_clients = make_clients(layout, man, range(n), dev)
+    mods = []
+    for f32, i64 in dev_clients:
+        m = Holder()
+        sd = m.state_dict()
+        with torch.no_grad():
+            for s in layout.slots:
+                src = i64 if s.kind == "i64" else f32
+                sd[s.key].copy_(src[s.offset:s.offset + s.numel].view(s.shape).cpu())
+        mods.append(m)
+    snap = [{k: v.clone() for k, v in m.state_dict().items()} for m in mods]
+    g = Holder()
+    server_aggregate(g, mods)  # binds the pinned arenas
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        want = json.load(f)["fedavg/wrn16_8_c10/n2"]
+    import hashlib
+    h = hashlib.sha256()
+    for k, v in g.state_dict().items():
+        h.update(k.encode())
+        h.update(v.numpy().tobytes())
+    ok = h.hexdigest() == want
+    ts = []
+    for _ in range(reps):
+        for m, sn in zip(mods, snap):  # restore the inputs (the round broadcast over them)
+            m.load_state_dict(sn)
+        t0 = time.perf_counter()
+        server_aggregate(g, mods)
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    t = ts[len(ts) // 2]
+    return {"server_aggregate_ms": round(t * 1e3, 2), "bit_exact_vs_reference_digest": bool(ok),
+            "note": "host-resident modules, pinned arenas, PCIe H2D/D2H incl. broadcast"}
+
+
 def exact_modes(layout, manifest, clients, out32, out64, world, group, dev, nbytes_rank,
                 steps):
     """N>1: the exact column-striped mode (feddct_amd/dist.py),
@@ -445,6 +489,10 @@ def main():
             extra["round_with_fused_broadcast_us"] = round(tb * 1e6, 1)
             extra["dropin"] = dropin_timing(layout, clients, dev)
             extra["other_configs"] = other_configs(dev)
+            try:
+                extra["cfg1_host_resident_n2"] = cfg1_host_resident(dev)
+            except Exception as e:  # noqa: BLE001
+                extra["cfg1_host_resident_n2"] = {"error": repr(e)}
     else:
         from feddct_amd.dist import ShardedAggregator
         agg = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
