@@ -36,6 +36,8 @@ FA_PLAN_TUNE_BATCH8 = 4
 FA_PLAN_TUNE_BATCH16 = 8
 FA_PLAN_TUNE_XCD = 16
 FA_PLAN_TUNE_WAVE_CONTIG = 32
+FA_PLAN_TUNE_ST_PLAIN = 64
+FA_PLAN_TUNE_LD_PLAIN = 128
 
 
 def FA_PLAN_TUNE_BLOCKS_PER_CU(c):

@@ -189,7 +189,7 @@ __device__ __forceinline__ void promote(Acc<U, DEEP>& A, int ii, int lp, int mas
 
 // One batch of NB clients starting at b0.  FULL: every lane's U vectors are
 // inside the tile (no per-lane predicate).
-template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, bool NT>
+template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL>
 __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0,
                                       const int64_t (&off)[U], const bool (&ok)[U],
                                       int lp, int mask) {
@@ -199,8 +199,8 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0,
     const float* p = cptr32(a, b0 + b);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if constexpr (FULL) x[b][u] = ld4<NT>(p + off[u]);
-      else x[b][u] = ok[u] ? ld4<NT>(p + off[u]) : f4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (FULL) x[b][u] = ld4<(POL & 1) != 0>(p + off[u]);
+      else x[b][u] = ok[u] ? ld4<(POL & 1) != 0>(p + off[u]) : f4{0.f, 0.f, 0.f, 0.f};
     }
   }
 #pragma unroll
@@ -217,7 +217,7 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0,
 
 // The last, partial batch (nb < NB clients): same issue-all-then-add shape,
 // every step guarded by a uniform (scalar) branch.
-template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, bool NT>
+template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL>
 __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, int nb,
                                            const int64_t (&off)[U], const bool (&ok)[U],
                                            int lp, int mask) {
@@ -228,8 +228,8 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
       const float* p = cptr32(a, b0 + b);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if constexpr (FULL) x[b][u] = ld4<NT>(p + off[u]);
-        else x[b][u] = ok[u] ? ld4<NT>(p + off[u]) : f4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (FULL) x[b][u] = ld4<(POL & 1) != 0>(p + off[u]);
+        else x[b][u] = ok[u] ? ld4<(POL & 1) != 0>(p + off[u]) : f4{0.f, 0.f, 0.f, 0.f};
       }
     }
   }
@@ -247,7 +247,7 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
   }
 }
 
-template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, bool NT>
+template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, int POL>
 __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
                                          int count) {
   const int n = a.n;
@@ -269,8 +269,8 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
   }
   int b0 = 0;
   for (; b0 + B <= n; b0 += B)
-    batch<U, B, FULL, DEEP, WEIGHTED, NT>(a, A, b0, off, ok, lp, mask);
-  if (b0 < n) batch_tail<U, B, FULL, DEEP, WEIGHTED, NT>(a, A, b0, n - b0, off, ok, lp, mask);
+    batch<U, B, FULL, DEEP, WEIGHTED, POL>(a, A, b0, off, ok, lp, mask);
+  if (b0 < n) batch_tail<U, B, FULL, DEEP, WEIGHTED, POL>(a, A, b0, n - b0, off, ok, lp, mask);
 
   const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
   const float fn = (float)n;
@@ -285,9 +285,9 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
       s = add4(s, A.l3[u]);
     }
     const f4 r = sum_only ? s : div4s(s, fn);
-    st4<NT>(a.out32 + off[u], r);
+    st4<(POL & 2) != 0>(a.out32 + off[u], r);
     if (a.flags & FA_F_BCAST) {
-      for (int i = 0; i < n; ++i) st4<NT>(const_cast<float*>(cptr32(a, i)) + off[u], r);
+      for (int i = 0; i < n; ++i) st4<(POL & 2) != 0>(const_cast<float*>(cptr32(a, i)) + off[u], r);
     }
   }
 }
@@ -387,7 +387,7 @@ __device__ void tile_scalar(KArgs& a, const Tile& t) {
   }
 }
 
-template <int U, int B, bool DEEP, bool WEIGHTED, bool NT>
+template <int U, int B, bool DEEP, bool WEIGHTED, int POL>
 __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
   if (a.xcd_swz && ti >= a.nscalar) {
     // bijective: blocks i and i+8 share an XCD (round-robin dispatch); XCD x
@@ -398,8 +398,8 @@ __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
   }
   const Tile t = a.tiles[ti];
   if (t.kind == K_F32_VEC) {
-    if (t.count == 4 * U * kBlock) tile_vec<U, B, true, DEEP, WEIGHTED, NT>(a, t.start, t.count);
-    else tile_vec<U, B, false, DEEP, WEIGHTED, NT>(a, t.start, t.count);
+    if (t.count == 4 * U * kBlock) tile_vec<U, B, true, DEEP, WEIGHTED, POL>(a, t.start, t.count);
+    else tile_vec<U, B, false, DEEP, WEIGHTED, POL>(a, t.start, t.count);
   } else {
     tile_scalar<WEIGHTED>(a, t);
   }
@@ -407,15 +407,15 @@ __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
 
 // One workgroup per tile (default), or a persistent grid walking the table
 // with stride gridDim.x (tuning: FA_PLAN_TUNE_PERSIST).
-template <int U, int B, bool DEEP, bool WEIGHTED, bool NT>
+template <int U, int B, bool DEEP, bool WEIGHTED, int POL>
 __global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs args) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   if ((int)gridDim.x >= a.ntiles) {
-    run_tile<U, B, DEEP, WEIGHTED, NT>(a, blockIdx.x);
+    run_tile<U, B, DEEP, WEIGHTED, POL>(a, blockIdx.x);
   } else {
     for (int ti = blockIdx.x; ti < a.ntiles; ti += gridDim.x) {
-      run_tile<U, B, DEEP, WEIGHTED, NT>(a, ti);
+      run_tile<U, B, DEEP, WEIGHTED, POL>(a, ti);
       __syncthreads();  // scalar tiles exit threads early; keep the block in step
     }
   }
@@ -653,30 +653,37 @@ thread_local size_t t_dyn_lds = 0;  // tuning: occupancy cap through dynamic LDS
 
 thread_local int t_grid_cap = 0;     // tuning: persistent grid size
 
-template <int U, int B, bool DEEP, bool W, bool NT>
+template <int U, int B, bool DEEP, bool W, int POL>
 hipError_t launch_one(const ReduceArgs& a, int ntiles, hipStream_t st) {
   const int grid = (t_grid_cap > 0 && t_grid_cap < ntiles) ? t_grid_cap : ntiles;
-  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, NT>), dim3(grid), dim3(kBlock), t_dyn_lds,
+  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, POL>), dim3(grid), dim3(kBlock), t_dyn_lds,
                      st, a);
   return hipGetLastError();
 }
 
 
 template <int U, int B>
-hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, bool nt, hipStream_t st) {
-  if (deep) return w ? launch_one<U, B, true, true, true>(a, ntiles, st)
-                     : launch_one<U, B, true, false, true>(a, ntiles, st);
-  if (w) return nt ? launch_one<U, B, false, true, true>(a, ntiles, st)
-                   : launch_one<U, B, false, true, false>(a, ntiles, st);
-  return nt ? launch_one<U, B, false, false, true>(a, ntiles, st)
-            : launch_one<U, B, false, false, false>(a, ntiles, st);
+hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, int pol, hipStream_t st) {
+  // pol: bit 0 = non-temporal loads, bit 1 = non-temporal stores (default 3)
+  if (deep) return w ? launch_one<U, B, true, true, 3>(a, ntiles, st)
+                     : launch_one<U, B, true, false, 3>(a, ntiles, st);
+  if (w) return pol == 3 ? launch_one<U, B, false, true, 3>(a, ntiles, st)
+                         : launch_one<U, B, false, true, 0>(a, ntiles, st);
+  switch (pol) {
+    case 0: return launch_one<U, B, false, false, 0>(a, ntiles, st);
+    case 1: return launch_one<U, B, false, false, 1>(a, ntiles, st);
+    case 2: return launch_one<U, B, false, false, 2>(a, ntiles, st);
+    default: return launch_one<U, B, false, false, 3>(a, ntiles, st);
+  }
 }
 
 hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pflags,
                          hipStream_t st) {
   const bool deep = a.n >= 256;
   const bool w = a.flags & 0x100u;  // internal: weighted
-  const bool nt = !(pflags & FA_PLAN_TUNE_NO_NT);
+  int nt = (pflags & FA_PLAN_TUNE_NO_NT) ? 0 : 3;
+  if (pflags & FA_PLAN_TUNE_ST_PLAIN) nt &= ~2;
+  if (pflags & FA_PLAN_TUNE_LD_PLAIN) nt &= ~1;
   const bool small = w || a.n < 16;
   const int b_env = (pflags & FA_PLAN_TUNE_BATCH8) ? 8
                     : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (small ? 8 : 16);

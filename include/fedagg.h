@@ -78,6 +78,8 @@ extern "C" {
 #define FA_PLAN_TUNE_BATCH16 8u    /* tuning: force 16 clients per load batch */
 #define FA_PLAN_TUNE_XCD 16u       /* tuning: contiguous tile range per XCD   */
 #define FA_PLAN_TUNE_WAVE_CONTIG 32u /* tuning: each wave reads adjacent KiBs  */
+#define FA_PLAN_TUNE_ST_PLAIN 64u  /* tuning: plain (temporal) stores only     */
+#define FA_PLAN_TUNE_LD_PLAIN 128u /* tuning: plain (temporal) loads only      */
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
 #define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
 /* tuning: persistent grid of 256*k workgroups striding over the tiles */
