@@ -517,6 +517,26 @@ def main():
                 "GBps": round(nbytes_rank * world / float(ta.item()) / 1e9, 2)}
         except Exception as e:  # noqa: BLE001
             extra["allreduce_mode"] = {"error": repr(e)}
+        # the same round through the native C ABI (libfedagg_comm.so: its own
+        # RCCL communicator, chunked ncclReduce on an internal stream)
+        n32 = n64 = None
+        try:
+            from feddct_amd.comm import Comm, NativeShardedAggregator
+            ncomm = Comm.from_process_group(group)
+            n32, n64 = torch.zeros_like(out32), torch.zeros_like(out64)
+            nagg = NativeShardedAggregator(layout, [c[0] for c in clients],
+                                           [c[1] for c in clients], N_CLIENTS * world, n32, n64,
+                                           ncomm, nchunks=args.chunks, final="reduce")
+            t_nat, _ = timed_launches(nagg.step, max(10, args.steps // 2), 5, sync_group=group)
+            tn = torch.tensor([t_nat], dtype=torch.float64, device=dev)
+            dist.all_reduce(tn, op=dist.ReduceOp.MAX)
+            extra["native_mode"] = {
+                "mode": "C ABI fa_reduce_sharded: client shards + chunked ncclReduce to rank 0",
+                "ms_per_step": round(float(tn.item()) * 1e3, 4),
+                "GBps": round(nbytes_rank * world / float(tn.item()) / 1e9, 2)}
+        except Exception as e:  # noqa: BLE001
+            extra["native_mode"] = {"error": repr(e)}
+            n32 = None
         # kernel-only launch time for the roofline: the same reduce over this
         # rank's clients into scratch outputs (out32/out64 hold the round's result)
         kred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
@@ -546,6 +566,9 @@ def main():
                                "max_abs_err_fp32": float((out32 - ex32).abs().max()),
                                "int64_bit_exact": bool(torch.equal(out64, ex64)),
                                "allreduce_mode_same_as_reduce_mode": bool(torch.equal(a32, out32))}
+            if n32 is not None and "error" not in extra.get("native_mode", {}):
+                extra["native_mode"]["max_ulp_fp32_vs_exact"] = ulp_dist(n32, ex32)
+                extra["native_mode"]["int64_bit_exact"] = bool(torch.equal(n64, ex64))
             if striped is not None:
                 striped["bit_exact"] = bool(torch.equal(s32, ex32) and torch.equal(s64, ex64))
                 extra["exact_mode"] = striped

@@ -19,13 +19,31 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off", "-fno-fast-math", "-Wall"]
 
 
+# The multi-GPU exchange (RCCL) is a separate library over libfedagg.so's
+# public ABI, so the core library does not depend on RCCL.  librccl.so.1
+# resolves to the copy torch has already loaded (same soname).
+COMM_SRC = os.path.join(HERE, "csrc", "fedcomm.hip")
+COMM_DEPS = [COMM_SRC, os.path.join(HERE, "csrc", "common.h"),
+             os.path.join(HERE, "..", "include", "fedagg.h"),
+             os.path.join(HERE, "..", "include", "fedagg_comm.h")]
+COMM_OUT = os.path.join(HERE, "libfedagg_comm.so")
+
+
+def _stale(out, deps):
+    return not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(d)
+                                                                   for d in deps)
+
+
 def build(force: bool = False, extra=()) -> str:
-    if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= max(
-            os.path.getmtime(d) for d in DEPS):
-        return OUT
-    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", *SRCS]
-    subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
+    if force or _stale(OUT, DEPS):
+        cmd = [HIPCC, *FLAGS, *extra, "-Wl,-soname,libfedagg.so", "-o", OUT + ".tmp", *SRCS]
+        subprocess.run(cmd, check=True)
+        os.replace(OUT + ".tmp", OUT)
+    if force or _stale(COMM_OUT, COMM_DEPS + [OUT]):
+        cmd = [HIPCC, *FLAGS, *extra, "-o", COMM_OUT + ".tmp", COMM_SRC, "-L" + HERE, "-lfedagg",
+               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,$ORIGIN"]
+        subprocess.run(cmd, check=True)
+        os.replace(COMM_OUT + ".tmp", COMM_OUT)
     return OUT
 
 

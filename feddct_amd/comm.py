@@ -1,0 +1,191 @@
+"""Native multi-GPU round over RCCL (libfedagg_comm.so, include/fedagg_comm.h).
+
+The C-ABI form of feddct_amd.dist.ShardedAggregator (SURVEY.md §8 b, e1): one
+process per GPU, client slots sharded contiguously in slot order; per round
+the library sums the rank's clients in the exact torch order column chunk by
+column chunk and exchanges each chunk (ncclReduce to the server rank, or
+ncclAllReduce) on its own stream while the next chunk is summed; int64 keys
+are all-gathered and reduced exactly.  torch.distributed only carries the
+communicator's 128-byte id from rank 0 to the others; the data path is the
+library's own RCCL communicator.
+
+No fallback: loading raises if libfedagg_comm.so is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .dist import shard_range
+from .layout import BucketLayout
+
+COMM_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfedagg_comm.so")
+FA_E_COMM = -6
+FA_COMM_UID_BYTES = 128
+
+COMM_EXPORTS = ["fa_comm_unique_id", "fa_comm_init_rank", "fa_comm_init", "fa_comm_destroy",
+                "fa_comm_info", "fa_shard_plan_create", "fa_shard_plan_destroy",
+                "fa_reduce_sharded"]
+
+_P, _I, _I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+
+
+class FaShardIO(ctypes.Structure):
+    _fields_ = [("c32", _P), ("c64", _P), ("weights", _P), ("out32", _P), ("out64", _P),
+                ("stream", _P)]
+
+
+def _load():
+    if not os.path.exists(COMM_PATH):
+        raise ImportError(f"feddct_amd: {COMM_PATH} not built (run __graft_entry__.build()); "
+                          "there is no fallback")
+    lib = ctypes.CDLL(COMM_PATH)
+    sig = {
+        "fa_comm_unique_id": [ctypes.c_char_p, _I],
+        "fa_comm_init_rank": [_I, _I, ctypes.c_char_p, _I, ctypes.POINTER(_P)],
+        "fa_comm_init": [_I, ctypes.POINTER(_I), ctypes.POINTER(_P)],
+        "fa_comm_destroy": [_P],
+        "fa_comm_info": [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I)],
+        "fa_shard_plan_create": [_P, _P, _I, _I64, _P, _I, _I64, ctypes.POINTER(_I), _I,
+                                 ctypes.c_uint, ctypes.POINTER(_P)],
+        "fa_shard_plan_destroy": [_P],
+        "fa_reduce_sharded": [ctypes.POINTER(_P), _I, ctypes.POINTER(FaShardIO), _I],
+    }
+    for name, args in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = _I
+        fn.argtypes = args
+    return lib
+
+
+_clib = None
+
+
+def lib():
+    global _clib
+    if _clib is None:
+        _clib = _load()
+    return _clib
+
+
+def unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(FA_COMM_UID_BYTES)
+    _lib.check(lib().fa_comm_unique_id(buf, FA_COMM_UID_BYTES), "fa_comm_unique_id")
+    return buf.raw
+
+
+class Comm:
+    """An RCCL communicator of the library, on the current device."""
+
+    def __init__(self, nranks: int, rank: int, uid: bytes):
+        h = _P()
+        _lib.check(lib().fa_comm_init_rank(nranks, rank, uid, len(uid), ctypes.byref(h)),
+                   "fa_comm_init_rank")
+        self.handle = h
+        self.nranks, self.rank = nranks, rank
+
+    @classmethod
+    def from_process_group(cls, group=None) -> "Comm":
+        """Every rank of ``group`` (torch.distributed) joins one communicator;
+        rank 0's id travels over the group."""
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        obj = [unique_id() if rank == 0 else None]
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(obj, src=src, group=group)
+        return cls(world, rank, obj[0])
+
+    @classmethod
+    def single(cls) -> "Comm":
+        """A one-rank communicator (no process group needed)."""
+        return cls(1, 0, unique_id())
+
+    def info(self):
+        n, r, d = _I(), _I(), _I()
+        _lib.check(lib().fa_comm_info(self.handle, ctypes.byref(n), ctypes.byref(r),
+                                      ctypes.byref(d)), "fa_comm_info")
+        return n.value, r.value, d.value
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            _lib.check(lib().fa_comm_destroy(self.handle), "fa_comm_destroy")
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ShardPlan:
+    """This rank's shard plan for a layout (chunk subplans + scratch)."""
+
+    def __init__(self, comm: Comm, layout: BucketLayout, counts: Sequence[int],
+                 nchunks: int = 8):
+        a32, n32 = _lib.seg_array(layout.segs32 if len(layout.segs32)
+                                  else np.zeros((0, 2), np.int64))
+        a64, n64 = _lib.seg_array(layout.segs64 if len(layout.segs64)
+                                  else np.zeros((0, 2), np.int64))
+        c = (_I * len(counts))(*map(int, counts))
+        h = _P()
+        _lib.check(lib().fa_shard_plan_create(comm.handle, a32, n32, int(layout.f32_numel), a64,
+                                              n64, int(layout.i64_numel), c, int(nchunks),
+                                              _lib.FA_PLAN_GAPS_ARE_PADDING, ctypes.byref(h)),
+                   "fa_shard_plan_create")
+        self.handle = h
+        self.comm = comm  # the plan must not outlive its communicator
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                lib().fa_shard_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+class NativeShardedAggregator:
+    """The cross-GPU round of ``dist.ShardedAggregator`` through the C ABI:
+    ``step()`` is ONE fa_reduce_sharded call (kernels, chunked RCCL exchange,
+    /N, int64 gather + exact reduce), stream-ordered on the current stream.
+
+    ``final="reduce"``: the global state lands on ``root`` (out buffers of the
+    other ranks are untouched); ``"allreduce"``: on every rank."""
+
+    def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
+                 local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
+                 out64: torch.Tensor, comm: Comm, nchunks: int = 8, final: str = "reduce",
+                 root: int = 0, weights: Optional[Sequence[float]] = None):
+        if final not in ("reduce", "allreduce"):
+            raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
+        world, rank, _ = comm.info()
+        counts = [b - a for a, b in (shard_range(n_total, world, r) for r in range(world))]
+        if len(local32) != counts[rank]:
+            raise ValueError(f"rank {rank} holds {len(local32)} clients, shard is {counts[rank]}")
+        self.plan = ShardPlan(comm, layout, counts, nchunks)
+        self.root = root if final == "reduce" else -1
+        self._a32 = _lib.ptr_array([t.data_ptr() for t in local32])
+        self._a64 = _lib.ptr_array([t.data_ptr() for t in local64])
+        self._w = (None if weights is None
+                   else (ctypes.c_float * max(1, len(weights)))(*map(float, weights)))
+        self._plans = (_P * 1)(self.plan.handle.value)
+        self.io = FaShardIO()
+        self.io.c32 = ctypes.cast(self._a32, _P)
+        self.io.c64 = ctypes.cast(self._a64, _P) if layout.i64_numel else None
+        self.io.weights = ctypes.cast(self._w, _P) if self._w is not None else None
+        self.io.out32 = out32.data_ptr()
+        self.io.out64 = out64.data_ptr() if layout.i64_numel else None
+        self._keep = (local32, local64, out32, out64)
+
+    def step(self, stream=None) -> None:
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self.io.stream = s
+        _lib.check(lib().fa_reduce_sharded(self._plans, 1, ctypes.byref(self.io), self.root),
+                   "fa_reduce_sharded")

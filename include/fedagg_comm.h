@@ -1,0 +1,101 @@
+/*
+ * fedagg_comm.h — C ABI of libfedagg_comm.so: the multi-GPU form of the
+ * server-side aggregation (SURVEY.md §8 b "fa_comm_init / fa_mean_f32_multi",
+ * §8 e1), natively over RCCL (xGMI inside one node).
+ *
+ * Reference: the round loops aggregate every client of a round into one
+ * global model (train_fedavg.py:138-149, train_feddct.py:34-56); when the
+ * clients' states do not fit one GPU, the client slots are sharded across the
+ * GPUs of the node — rank r holds a contiguous run of slots, in slot order —
+ * and a round is
+ *
+ *   1. per rank, the torch-order sum of its own clients for every fp32 key
+ *      (fa_reduce with FA_F_SUM_ONLY, over a column chunk at a time);
+ *   2. an RCCL sum of those partial buckets — ncclReduce to the server rank
+ *      (root >= 0), or ncclAllReduce (root < 0: every rank gets the global
+ *      state, e.g. to reload its own client slots) — chunk c on an internal
+ *      communication stream while the kernel sums chunk c+1;
+ *   3. /N_total (IEEE division) on the ranks that hold the result.
+ *   int64 keys (num_batches_tracked) are all-gathered raw and reduced exactly
+ *   over all N_total clients, so they match the single-GPU result bit for bit.
+ *
+ * The cross-rank sum re-associates fp32: the fp32 result is NOT bit-identical
+ * to the single-process reference (the exact element-striped mode lives in
+ * feddct_amd/dist.py StripedAggregator).  With one rank it is bit-identical.
+ *
+ * Process models:
+ *   - one process per GPU (the product's): rank 0 calls fa_comm_unique_id,
+ *     ships the 128 bytes to every rank (e.g. a torch.distributed broadcast),
+ *     each rank calls fa_comm_init_rank on its current device;
+ *   - one process driving several GPUs: fa_comm_init(ndev, devs, comms).
+ *   fa_reduce_sharded takes an array of local shard plans (one per GPU this
+ *   process drives: 1 in the per-process model) and groups the RCCL calls.
+ *
+ * Conventions as in fedagg.h: caller-owned device buffers (zero-copy), 0 or a
+ * negative FA_E* code, message in fa_last_error(); work is stream-ordered on
+ * the caller's stream (the internal communication stream joins it before
+ * fa_reduce_sharded returns).  Scratch (one partial bucket + the int64 gather
+ * rows) lives in the shard plan.
+ */
+#ifndef FEDAGG_COMM_H
+#define FEDAGG_COMM_H
+
+#include <stdint.h>
+
+#include "fedagg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA_E_COMM (-6)          /* RCCL error (message in fa_last_error)      */
+#define FA_COMM_UID_BYTES 128   /* == sizeof(ncclUniqueId)                     */
+#define FA_COMM_MAX_CHUNKS 64
+
+typedef struct fa_comm fa_comm;
+typedef struct fa_shard_plan fa_shard_plan;
+
+/* 128 opaque bytes identifying a new communicator (call on one rank). */
+int fa_comm_unique_id(unsigned char *id, int len);
+/* One process per GPU: rank `rank` of `nranks`, on the CURRENT device. */
+int fa_comm_init_rank(int nranks, int rank, const unsigned char *id, int len,
+                      fa_comm **out);
+/* One process driving ndev GPUs (devs[i] becomes rank i): comms[ndev]. */
+int fa_comm_init(int ndev, const int *devs, fa_comm **comms);
+int fa_comm_destroy(fa_comm *comm);
+int fa_comm_info(const fa_comm *comm, int *nranks, int *rank, int *device);
+
+/* Shard plan of one rank for a bucket layout (as fa_plan_create; the layout
+ * must be built with FA_PLAN_GAPS_ARE_PADDING: chunk exchanges span the
+ * padding between tensors).  counts[r] = client slots held by rank r (all
+ * ranks pass the same array); nchunks = column chunks of the exchange
+ * (0 = 8).  Created on the comm's device. */
+int fa_shard_plan_create(fa_comm *comm, const fa_seg *seg32, int nseg32,
+                         int64_t f32_numel, const fa_seg *seg64, int nseg64,
+                         int64_t i64_numel, const int *counts, int nchunks,
+                         unsigned flags, fa_shard_plan **out);
+int fa_shard_plan_destroy(fa_shard_plan *plan);
+
+/* Per local GPU arguments of one round. */
+typedef struct fa_shard_io {
+  const float *const *c32;      /* this rank's counts[rank] fp32 buckets      */
+  const int64_t *const *c64;    /* ... int64 buckets (NULL if no int64 keys)  */
+  const float *weights;         /* NULL: mean; else per local client fp32 w   */
+  float *out32;                 /* result (root / every rank); NULL elsewhere */
+  int64_t *out64;
+  void *stream;                 /* hipStream_t of the caller                  */
+} fa_shard_io;
+
+/* One round across the ranks.  plans[d] / io[d]: the d-th GPU this process
+ * drives (nlocal = 1 in the one-process-per-GPU model).  root >= 0: the
+ * global state lands on rank `root` only (the north_star's final reduce);
+ * root < 0: on every rank (all-reduce).  Weighted: fp32 keys = sum over all
+ * clients of fp32(x_i * w_i) (no division); int64 keys always take the
+ * mean-and-truncate path. */
+int fa_reduce_sharded(fa_shard_plan *const *plans, int nlocal,
+                      const fa_shard_io *io, int root);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEDAGG_COMM_H */

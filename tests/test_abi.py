@@ -101,3 +101,23 @@ def test_norm_plan_host_errors():
     segs, n = _lib.seg_array(np.array([[0, 100]], np.int64))
     assert L.fa_norm_plan_create(segs, n, 50, ctypes.byref(h)) == _lib.FA_E_INVAL
     assert L.fa_prox_norms(None, None, None, None, None, None) == _lib.FA_E_INVAL
+
+
+def test_comm_library_exports_every_declared_symbol():
+    """libfedagg_comm.so (the RCCL exchange) exports include/fedagg_comm.h."""
+    from feddct_amd import comm
+    src = open(os.path.join(ROOT, "include", "fedagg_comm.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    fns = sorted(set(re.findall(r"\b(fa_[a-z0-9_]+)\s*\(", src)))
+    so = comm.lib()
+    for f in fns:
+        assert hasattr(so, f), f"{f} declared in include/fedagg_comm.h but not exported"
+    assert set(fns) == set(comm.COMM_EXPORTS)
+    # host-side argument checks (no GPU, no communicator needed)
+    h = ctypes.c_void_p()
+    assert so.fa_comm_init_rank(0, 0, b"x" * 128, 128, ctypes.byref(h)) == _lib.FA_E_INVAL
+    assert so.fa_comm_unique_id(None, 0) == _lib.FA_E_INVAL
+    assert so.fa_reduce_sharded(None, 0, None, 0) == _lib.FA_E_INVAL
+    assert so.fa_shard_plan_create(None, None, 0, 0, None, 0, 0, None, 0, 1,
+                                   ctypes.byref(h)) == _lib.FA_E_INVAL
+    assert b"NULL" in _lib.lib.fa_last_error()  # one error channel for both libraries

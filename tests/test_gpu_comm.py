@@ -1,0 +1,136 @@
+"""GPU: the native RCCL round (libfedagg_comm.so) on a one-rank communicator
+(the box has one GPU; RCCL refuses two ranks on one device).  With one rank
+the exchange is the identity, so the result must equal the single-GPU
+reduction bit for bit — which checks the chunking (every column summed once,
+padding-spanning exchanges), the /N finish on the comm stream, the int64
+gather + exact reduce and the stream joins.  The multi-rank orchestration is
+covered on CPU with gloo (tests/test_dist_gloo.py) and by bench.py --gpus N."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_manifest
+from feddct_amd import synth
+from feddct_amd.layout import BucketLayout
+from feddct_amd.workload import make_clients
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def comm():
+    torch.cuda.set_device(DEV)
+    from feddct_amd import comm as C
+    c = C.Comm.single()
+    yield c
+    c.close()
+
+
+def _single_gpu(layout, clients, weights=None):
+    from feddct_amd import _lib
+    from feddct_amd.workload import Reducer
+    o32, o64 = torch.zeros_like(clients[0][0]), torch.zeros_like(clients[0][1])
+    Reducer(layout, clients, o32, o64, weights=weights)()
+    torch.cuda.synchronize()
+    return o32, o64
+
+
+def _layout_pad_mask(layout):
+    m = np.zeros(layout.f32_numel, bool)
+    for o, n in layout.segs32:
+        m[o:o + n] = True
+    return torch.from_numpy(m).to(DEV)
+
+
+@pytest.mark.parametrize("lay", ["wrn16_8_c10", "wrnsl16_8_sf4_c10_proxy"])
+@pytest.mark.parametrize("final", ["reduce", "allreduce"])
+@pytest.mark.parametrize("nchunks", [1, 8, 13])
+def test_native_round_one_rank_is_bit_exact(comm, lay, final, nchunks):
+    from feddct_amd.comm import NativeShardedAggregator
+    man = load_manifest(lay)
+    layout = BucketLayout.from_manifest(man)
+    n = 20
+    clients = make_clients(layout, man, range(n), DEV, mode=synth.MODE_ADVERSARIAL)
+    want32, want64 = _single_gpu(layout, clients)
+    out32 = torch.full_like(clients[0][0], float("nan"))
+    out64 = torch.full_like(clients[0][1], -7)
+    agg = NativeShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], n,
+                                  out32, out64, comm, nchunks=nchunks, final=final)
+    for _ in range(2):  # the second round reuses the plan's scratch and events
+        agg.step()
+    torch.cuda.synchronize()
+    mask = _layout_pad_mask(layout)
+    a, b = out32[mask].view(torch.int32), want32[mask].view(torch.int32)
+    nan = torch.isnan(want32[mask])
+    assert torch.equal(torch.isnan(out32[mask]), nan)
+    assert torch.equal(a[~nan], b[~nan])
+    assert torch.equal(out64, want64)
+
+
+def test_native_round_weighted(comm):
+    from feddct_amd.comm import NativeShardedAggregator
+    man = load_manifest("wrn16_8_c100")
+    layout = BucketLayout.from_manifest(man)
+    n = 7
+    clients = make_clients(layout, man, range(n), DEV)
+    w = [float(np.float32(k / 28.0)) for k in range(1, n + 1)]
+    want32, want64 = _single_gpu(layout, clients, weights=w)
+    out32, out64 = torch.zeros_like(want32), torch.zeros_like(want64)
+    NativeShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], n, out32,
+                            out64, comm, weights=w).step()
+    torch.cuda.synchronize()
+    mask = _layout_pad_mask(layout)
+    assert torch.equal(out32[mask], want32[mask])
+    assert torch.equal(out64, want64)
+
+
+def test_single_process_multi_device_form():
+    """fa_comm_init(ndev, devs) + fa_reduce_sharded over an array of local
+    plans (here ndev = 1: the one GPU of the box)."""
+    from feddct_amd import _lib
+    from feddct_amd import comm as C
+    torch.cuda.set_device(DEV)
+    man = load_manifest("wrnsl16_8_sf4_c10_main")
+    layout = BucketLayout.from_manifest(man)
+    n = 5
+    clients = make_clients(layout, man, range(n), DEV)
+    want32, want64 = _single_gpu(layout, clients)
+    devs = (ctypes.c_int * 1)(0)
+    hs = (ctypes.c_void_p * 1)()
+    _lib.check(C.lib().fa_comm_init(1, devs, hs), "fa_comm_init")
+    comm = C.Comm.__new__(C.Comm)
+    comm.handle, comm.nranks, comm.rank = ctypes.c_void_p(hs[0]), 1, 0
+    assert comm.info() == (1, 0, 0)
+    out32, out64 = torch.zeros_like(want32), torch.zeros_like(want64)
+    agg = C.NativeShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], n,
+                                    out32, out64, comm, final="allreduce")
+    agg.step()
+    torch.cuda.synchronize()
+    mask = _layout_pad_mask(layout)
+    assert torch.equal(out32[mask], want32[mask])
+    assert torch.equal(out64, want64)
+    del agg
+    comm.close()
+
+
+def test_native_errors(comm):
+    from feddct_amd import _lib
+    from feddct_amd.comm import NativeShardedAggregator, ShardPlan
+    man = load_manifest("wrnsl16_8_sf4_c10_main")
+    layout = BucketLayout.from_manifest(man)
+    clients = make_clients(layout, man, range(3), DEV)
+    o32, o64 = torch.zeros_like(clients[0][0]), torch.zeros_like(clients[0][1])
+    with pytest.raises(ValueError, match="shard"):
+        NativeShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], 4,
+                                o32, o64, comm)
+    agg = NativeShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], 3,
+                                  o32, o64, comm)
+    agg.root = 5
+    with pytest.raises(_lib.FedaggError, match="root"):
+        agg.step()
+    with pytest.raises(_lib.FedaggError, match="clients in total"):
+        ShardPlan(comm, layout, [0])
