@@ -25,6 +25,7 @@ D2H).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -380,6 +381,136 @@ def _holder_class(layout):
     return Holder
 
 
+def _param_module(layout, dev, seed):
+    """An nn.Module with ``layout``'s state_dict, BN running stats and int64
+    counters as buffers (as in the reference models), parameters filled
+    from a seeded generator."""
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            for sl in layout.slots:
+                parts = sl.key.split(".")
+                mod = self
+                for q in parts[:-1]:
+                    if q not in mod._modules:
+                        mod.add_module(q, torch.nn.Module())
+                    mod = mod._modules[q]
+                t = torch.zeros(sl.shape, dtype=sl.dtype)
+                if sl.dtype == torch.int64 or parts[-1].startswith("running_"):
+                    mod.register_buffer(parts[-1], t)
+                else:
+                    mod.register_parameter(parts[-1], torch.nn.Parameter(t))
+    m = M().to(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    with torch.no_grad():
+        for p_ in m.parameters():
+            p_.copy_(torch.randn(p_.shape, generator=g, device=dev) * 0.05)
+    return m
+
+
+def next_rows(dev, steps=30):
+    """SURVEY.md §8 f3/f4 measured beside the reference's own code on this box.
+
+    f3: the FedProx proximal term sum_k ||w_k - w_t,k||_2 and its backward
+    (train_fedprox.py:113-116), wrn16_8 C100 client vs global: ours (arenas,
+    prox_partials + prox_finish forward, prox_grad backward) vs the
+    reference's per-parameter loop on torch-ROCm on the same GPU; kernel
+    roofline over the algorithmic bytes (forward reads both models' P
+    parameters, backward reads both and writes both gradients: 24 B/param).
+    f4: the per-round checkpoint save (train_fedavg.py:421-442,
+    utils/metric.py:9-14) of the GPU global model, bucket DMA vs
+    torch.save(model.state_dict())."""
+    import tempfile
+    from feddct_amd.checkpoint import save_checkpoint
+    from feddct_amd.prox import proximal_term
+    man = load_manifest("wrn16_8_c100")
+    layout = BucketLayout.from_manifest(man)
+    client, glob = _param_module(layout, dev, 1), _param_module(layout, dev, 2)
+    P = sum(p_.numel() for p_ in client.parameters())
+
+    def ours():
+        client.zero_grad(set_to_none=True)
+        glob.zero_grad(set_to_none=True)
+        proximal_term(client, glob).backward()
+
+    def reference():
+        client.zero_grad(set_to_none=True)
+        glob.zero_grad(set_to_none=True)
+        pt = 0.0
+        for w, w_t in zip(client.parameters(), glob.parameters()):
+            pt += (w - w_t).norm(2)
+        pt.backward()
+
+    ours()
+    want = sum((w - w_t).norm(2) for w, w_t in zip(client.parameters(), glob.parameters()))
+    got = proximal_term(client, glob)
+    t_ours, _ = timed_launches(ours, steps, 3)
+    t_ref, _ = timed_launches(reference, steps, 3)
+    # kernel-only: the three launches over the bound arenas
+    # (4 rotated sets of client/global/grad buckets: 704 MB > the 256 MB MALL)
+    term = client.__dict__["_fa_prox"][id(glob)]
+    norms = torch.empty(max(1, term.plan.nseg), device=dev)
+    total = torch.empty((), device=dev)
+    one = torch.ones((), device=dev)
+    sets = [(term.ca.f32.clone(), term.ga.f32.clone(), torch.empty_like(term.ca.f32),
+             torch.empty_like(term.ga.f32)) for _ in range(4)]
+    rot = [0]
+
+    def kernels():
+        a, b, ga, gb = sets[rot[0] % 4]
+        rot[0] += 1
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        _lib.check(_lib.lib.fa_prox_norms(term.plan.handle, a.data_ptr(), b.data_ptr(),
+                                          norms.data_ptr(), total.data_ptr(), st))
+        _lib.check(_lib.lib.fa_prox_grad(term.plan.handle, a.data_ptr(), b.data_ptr(),
+                                         norms.data_ptr(), one.data_ptr(), 1.0, ga.data_ptr(),
+                                         gb.data_ptr(), st))
+    t_k, _ = timed_launches(kernels, steps * 4, 4)
+    del sets
+    kbytes = 24 * P
+    f3 = {"params": P, "step_us": round(t_ours * 1e6, 1),
+          "reference_loop_step_us": round(t_ref * 1e6, 1),
+          "speedup_vs_reference_loop": round(t_ref / t_ours, 2),
+          "kernels_us": round(t_k * 1e6, 1),
+          "kernels_GBps": round(kbytes / t_k / 1e9, 1),
+          "kernels_roofline_frac": round(kbytes / t_k / 1e9 / HBM_PEAK_GBS, 4),
+          "rel_err_vs_torch": float(abs(got.item() - want.item()) / abs(want.item())),
+          "note": "fwd+bwd per training step incl. autograd; reference = its loop on torch-ROCm"}
+    # f4: checkpoint save of the bound global model
+    from feddct_amd.aggregate import server_aggregate
+    server_aggregate(glob, [client])  # binds glob's arena (and client's)
+    d = tempfile.mkdtemp(prefix="fa_ckpt_")
+    try:
+        def save_ours():
+            save_checkpoint({"round": 1, "arch": "wrn16_8", "state_dict": glob,
+                             "best_acc1": 0.0}, False, d, "ours.pth.tar")
+
+        def save_ref():
+            torch.save({"round": 1, "arch": "wrn16_8", "state_dict": glob.state_dict(),
+                        "best_acc1": 0.0}, os.path.join(d, "ref.pth.tar"))
+
+        def wall(fn, reps=5):
+            fn()
+            ts = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t0)
+            return sorted(ts)[reps // 2]
+        to, tr = wall(save_ours), wall(save_ref)
+        a = torch.load(os.path.join(d, "ours.pth.tar"), weights_only=True)["state_dict"]
+        b = torch.load(os.path.join(d, "ref.pth.tar"), weights_only=True)["state_dict"]
+        same = list(a.keys()) == list(b.keys()) and all(torch.equal(a[k].cpu(), b[k].cpu()) for k in a)
+        f4 = {"save_ms": round(to * 1e3, 2), "reference_save_ms": round(tr * 1e3, 2),
+              "files_equal": bool(same), "bytes": layout.state_bytes()}
+    finally:
+        import shutil
+        shutil.rmtree(d, ignore_errors=True)
+    return {"f3_fedprox_proximal_term": f3, "f4_checkpoint_save": f4}
+
+
 def dropin_timing(layout, clients, dev, reps=20):
     """Wall time of the drop-in ``server_aggregate(global, clients)`` on
     nn.Modules with the wrn16_8 state_dict (arena validation + one fused
@@ -489,6 +620,10 @@ def main():
             extra["round_with_fused_broadcast_us"] = round(tb * 1e6, 1)
             extra["dropin"] = dropin_timing(layout, clients, dev)
             extra["other_configs"] = other_configs(dev)
+            try:
+                extra["next_rows"] = next_rows(dev)
+            except Exception as e:  # noqa: BLE001
+                extra["next_rows"] = {"error": repr(e)}
             try:
                 extra["cfg1_host_resident_n2"] = cfg1_host_resident(dev)
             except Exception as e:  # noqa: BLE001

@@ -14,7 +14,7 @@
 //
 //   prox_partials : one workgroup per chunk (<= 4096 floats of ONE tensor),
 //                   sum of (a-b)^2 with 16-B loads, wave + LDS reduction;
-//   prox_finish   : one workgroup: per tensor the chunk partials in fixed
+//   prox_finish   : one workgroup: per tensor the chunk partials in a fixed
 //                   order -> sqrt -> norms[k]; sum of norms -> total
 //                   (deterministic: no atomics);
 //   prox_grad     : d/dw ||w - w_t|| = (w - w_t)/||w - w_t|| (0 where the
@@ -64,24 +64,37 @@ __device__ __forceinline__ float block_sum(float v, float* lds) {
   return r;  // valid in thread 0
 }
 
+// Every lane owns kVec float4 of the chunk (lane t: vectors t, t+256, ...);
+// all of them are loaded before any arithmetic, so a workgroup keeps its
+// whole 2 x 16 KiB in flight.  Chunk starts are 16-B aligned (tensors start
+// on 256-B boundaries in the bucket, chunks are 4096 floats); a count that is
+// not a multiple of 4 finishes with scalar elements.
+constexpr int kVec = kChunk / (4 * kBlk);
+
 __global__ __launch_bounds__(kBlk) void prox_partials(const NormChunk* __restrict__ chunks,
                                                       const float* __restrict__ a,
                                                       const float* __restrict__ b,
                                                       float* __restrict__ partials) {
   __shared__ float lds[kBlk / 64];
   const NormChunk c = chunks[blockIdx.x];
-  float acc = 0.f;
   const int nv = c.count / 4;
-  const bool al = (c.start % 4) == 0;
-  if (al) {
-    const f4* pa = reinterpret_cast<const f4*>(a + c.start);
-    const f4* pb = reinterpret_cast<const f4*>(b + c.start);
-    for (int v = threadIdx.x; v < nv; v += kBlk) {
-      const f4 d = pa[v] - pb[v];
-      acc += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
-    }
+  const f4* pa = reinterpret_cast<const f4*>(a + c.start);
+  const f4* pb = reinterpret_cast<const f4*>(b + c.start);
+  f4 xa[kVec], xb[kVec];
+#pragma unroll
+  for (int u = 0; u < kVec; ++u) {
+    const int v = threadIdx.x + u * kBlk;
+    const bool ok = v < nv;
+    xa[u] = ok ? pa[v] : f4{0.f, 0.f, 0.f, 0.f};
+    xb[u] = ok ? pb[v] : f4{0.f, 0.f, 0.f, 0.f};
   }
-  for (int j = (al ? 4 * nv : 0) + threadIdx.x; j < c.count; j += kBlk) {
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < kVec; ++u) {
+    const f4 d = xa[u] - xb[u];
+    acc += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
+  }
+  for (int j = 4 * nv + threadIdx.x; j < c.count; j += kBlk) {
     const float d = a[c.start + j] - b[c.start + j];
     acc += d * d;
   }
@@ -89,22 +102,68 @@ __global__ __launch_bounds__(kBlk) void prox_partials(const NormChunk* __restric
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 
-__global__ __launch_bounds__(kBlk) void prox_finish(const int* __restrict__ seg_first,
-                                                    int nseg, const float* __restrict__ partials,
-                                                    float* __restrict__ norms,
-                                                    float* __restrict__ total) {
-  __shared__ float lds[kBlk / 64];
-  float acc = 0.f;
-  for (int k = threadIdx.x; k < nseg; k += kBlk) {
-    float sq = 0.f;
-    for (int c = seg_first[k]; c < seg_first[k + 1]; ++c) sq += partials[c];
-    const float nk = sqrtf(sq);
-    norms[k] = nk;
-    acc += nk;
+// One workgroup of 1024 threads.  Its latency is the point (the work is a
+// few thousand floats): the chunk partials and the tensor boundaries come in
+// with ONE round of independent loads into LDS (when they fit, else they are
+// read from global memory in the same order); then wave w sums tensors w,
+// w+16, ... (lane l: partials l, l+64, ... of the tensor, then a shuffle
+// tree) -> norms[k], and the norms are summed the same way -> total.  Fixed
+// order throughout: deterministic, no atomics.
+constexpr int kFinBlk = 1024;
+constexpr int kFinWaves = kFinBlk / 64;
+constexpr int kFinLoads = 8;
+
+template <bool LDS>
+__global__ __launch_bounds__(kFinBlk) void prox_finish(const int* __restrict__ seg_first,
+                                                       int nseg, int nchunks,
+                                                       const float* __restrict__ partials,
+                                                       float* __restrict__ norms,
+                                                       float* __restrict__ total) {
+  extern __shared__ float dyn[];  // [nchunks partials][nseg + 1 boundaries]
+  __shared__ float red[kFinWaves];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float* P = partials;
+  const int* F = seg_first;
+  if constexpr (LDS) {
+    float* sp = dyn;
+    int* sf = reinterpret_cast<int*>(dyn + nchunks);
+    for (int base = 0; base < nchunks; base += kFinBlk * kFinLoads) {
+      float x[kFinLoads];
+#pragma unroll
+      for (int i = 0; i < kFinLoads; ++i) {
+        const int j = base + threadIdx.x + i * kFinBlk;
+        x[i] = j < nchunks ? partials[j] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < kFinLoads; ++i) {
+        const int j = base + threadIdx.x + i * kFinBlk;
+        if (j < nchunks) sp[j] = x[i];
+      }
+    }
+    for (int j = threadIdx.x; j <= nseg; j += kFinBlk) sf[j] = seg_first[j];
+    __syncthreads();
+    P = sp;
+    F = sf;
   }
-  const float s = block_sum(acc, lds);
-  if (threadIdx.x == 0) *total = s;
+  for (int k = wave; k < nseg; k += kFinWaves) {
+    float sq = 0.f;
+    for (int i = F[k] + lane; i < F[k + 1]; i += 64) sq += P[i];
+    sq = wave_sum(sq);
+    if (lane == 0) norms[k] = sqrtf(sq);
+  }
+  __syncthreads();  // norms[] (global) written by this workgroup's waves
+  float t = 0.f;
+  for (int k = threadIdx.x; k < nseg; k += kFinBlk) t += norms[k];
+  t = wave_sum(t);
+  if (lane == 0) red[wave] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+    for (int i = 0; i < kFinWaves; ++i) r += red[i];
+    *total = r;
+  }
 }
+constexpr size_t kFinLdsMax = 64 * 1024;  // the default dynamic-LDS limit
 
 __global__ __launch_bounds__(kBlk) void prox_grad(const NormChunk* __restrict__ chunks,
                                                   const float* __restrict__ a,
@@ -115,7 +174,29 @@ __global__ __launch_bounds__(kBlk) void prox_grad(const NormChunk* __restrict__ 
   const NormChunk c = chunks[blockIdx.x];
   const float nk = norms[c.seg];
   const float g = nk > 0.f ? (*gout) * alpha / nk : 0.f;
-  for (int j = threadIdx.x; j < c.count; j += kBlk) {
+  const int nv = c.count / 4;
+  const f4* pa = reinterpret_cast<const f4*>(a + c.start);
+  const f4* pb = reinterpret_cast<const f4*>(b + c.start);
+  f4* qa = reinterpret_cast<f4*>(ga + c.start);
+  f4* qb = reinterpret_cast<f4*>(gb + c.start);
+  f4 xa[kVec], xb[kVec];
+#pragma unroll
+  for (int u = 0; u < kVec; ++u) {
+    const int v = threadIdx.x + u * kBlk;
+    const bool ok = v < nv;
+    xa[u] = ok ? pa[v] : f4{0.f, 0.f, 0.f, 0.f};
+    xb[u] = ok ? pb[v] : f4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int u = 0; u < kVec; ++u) {
+    const int v = threadIdx.x + u * kBlk;
+    if (v < nv) {
+      const f4 d = g * (xa[u] - xb[u]);
+      qa[v] = d;
+      if (gb) qb[v] = -d;
+    }
+  }
+  for (int j = 4 * nv + threadIdx.x; j < c.count; j += kBlk) {
     const int64_t e = c.start + j;
     const float d = g * (a[e] - b[e]);
     ga[e] = d;
@@ -148,6 +229,8 @@ int fa_norm_plan_create(const fa_seg* segs, int nseg, int64_t numel, fa_norm_pla
     first[k] = (int)ch.size();
     if (segs[k].offset < 0 || segs[k].numel < 0 || segs[k].offset + segs[k].numel > numel)
       return fa::set_err(FA_E_INVAL, "fa_norm_plan_create: segment %d outside bucket", k);
+    if (segs[k].offset % 4)
+      return fa::set_err(FA_E_ALIGN, "fa_norm_plan_create: segment %d not 16-B aligned", k);
     for (int64_t c = 0; c < segs[k].numel; c += kChunk)
       ch.push_back(NormChunk{segs[k].offset + c, (int32_t)std::min<int64_t>(kChunk, segs[k].numel - c), k});
   }
@@ -187,14 +270,21 @@ int fa_norm_plan_destroy(fa_norm_plan* p) {
 int fa_prox_norms(const fa_norm_plan* p, const float* a, const float* b, float* norms,
                   float* total, void* stream) {
   if (!p || !a || !b || !norms || !total) return fa::set_err(FA_E_INVAL, "fa_prox_norms: NULL argument");
+  if (((uintptr_t)a | (uintptr_t)b) & 15u)
+    return fa::set_err(FA_E_ALIGN, "fa_prox_norms: buckets must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
   if (p->nchunks > 0) {
     hipLaunchKernelGGL(prox_partials, dim3(p->nchunks), dim3(kBlk), 0, st, p->d_chunks, a, b,
                        p->d_partials);
     FA_HIP_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(prox_finish, dim3(1), dim3(kBlk), 0, st, p->d_seg_first, p->nseg,
-                     p->d_partials, norms, total);
+  const size_t lds = (size_t)(p->nchunks + p->nseg + 1) * 4;
+  if (lds <= kFinLdsMax)
+    hipLaunchKernelGGL(prox_finish<true>, dim3(1), dim3(kFinBlk), lds, st, p->d_seg_first,
+                       p->nseg, p->nchunks, p->d_partials, norms, total);
+  else
+    hipLaunchKernelGGL(prox_finish<false>, dim3(1), dim3(kFinBlk), 0, st, p->d_seg_first,
+                       p->nseg, p->nchunks, p->d_partials, norms, total);
   FA_HIP_TRY(hipGetLastError());
   return FA_OK;
 }
@@ -203,6 +293,8 @@ int fa_prox_grad(const fa_norm_plan* p, const float* a, const float* b, const fl
                  const float* gout, float alpha, float* grad_a, float* grad_b, void* stream) {
   if (!p || !a || !b || !norms || !gout || !grad_a)
     return fa::set_err(FA_E_INVAL, "fa_prox_grad: NULL argument");
+  if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)grad_a | (uintptr_t)grad_b) & 15u)
+    return fa::set_err(FA_E_ALIGN, "fa_prox_grad: buckets must be 16-B aligned");
   if (p->nchunks == 0) return FA_OK;
   hipLaunchKernelGGL(prox_grad, dim3(p->nchunks), dim3(kBlk), 0, (hipStream_t)stream,
                      p->d_chunks, a, b, norms, gout, alpha, grad_a, grad_b);

@@ -9,7 +9,7 @@ Drop-in for the loop of train_fedprox.py:113-115:
 becomes ``proximal_term = feddct_amd.prox.proximal_term(client_model,
 global_model)`` — the same value (to fp32 rounding) and the same gradients
 for BOTH models' parameters (the reference's graph also reaches the global
-model's parameters), computed by three HIP launches over the two arenas
+model's parameters), computed by three HIP launches (two forward, one backward) over the two arenas
 (csrc/prox.hip) instead of 2·K norm/sub kernels plus their backward.
 """
 from __future__ import annotations
@@ -100,6 +100,9 @@ class ProximalTerm:
                     "same fp32 slot of one layout")
             slots.append((sa.offset, sa.numel, sa.shape))
         self.slots = slots
+        # the parameter objects are pinned by the arenas' validity checks:
+        # a replaced parameter invalidates the arena and with it this term
+        self.params = tuple(client_model.parameters()) + tuple(global_model.parameters())
         segs = np.array([(o, m) for o, m, _ in slots], np.int64).reshape(-1, 2)
         with torch.cuda.device(self.ca.device):
             self.plan = _NormPlan(segs, layout.f32_numel)
@@ -109,8 +112,7 @@ class ProximalTerm:
                 and getattr(self.global_model, "_fa_arena", None) is self.ga and self.ga.valid())
 
     def __call__(self) -> torch.Tensor:
-        params = list(self.client_model.parameters()) + list(self.global_model.parameters())
-        return _Prox.apply(self, *params)
+        return _Prox.apply(self, *self.params)
 
 
 def proximal_term(client_model: torch.nn.Module, global_model: torch.nn.Module) -> torch.Tensor:

@@ -180,7 +180,9 @@ int fa_synth_fill_i64(int64_t *dst, int64_t numel, int key_index, int client,
 /* ---- FedProx proximal term (train_fedprox.py:113-116), SURVEY.md §8 f3 ----
  * sum_k ||a_k - b_k||_2 over the tensors (segments) of two flat buckets —
  * the client's and the global's parameters — and its gradient.  A norm plan
- * owns a small device scratch: use one plan from one stream at a time. */
+ * owns a small device scratch: use one plan from one stream at a time.
+ * Segments start on 16-B boundaries (offset % 4 == 0, as every arena layout
+ * places them) and all bucket pointers are 16-B aligned (else FA_E_ALIGN). */
 typedef struct fa_norm_plan fa_norm_plan;
 int fa_norm_plan_create(const fa_seg *segs, int nseg, int64_t numel,
                         fa_norm_plan **out);
