@@ -40,15 +40,24 @@ def _arena(module) -> ModuleArena:
     return a if a is not None and a.valid() else None
 
 
-def bucket_state_dict(module: torch.nn.Module) -> "OrderedDict[str, torch.Tensor]":
+def bucket_state_dict(module: torch.nn.Module, _stage: bool = False
+                      ) -> "OrderedDict[str, torch.Tensor]":
     """CPU state_dict of ``module`` copied out of its arena in one transfer
-    per bucket (falls back to ``module.state_dict()`` when not bound)."""
+    per bucket (falls back to ``module.state_dict()`` when not bound).
+    ``_stage``: reuse a pinned staging buffer kept on the arena (the result is
+    only valid until the next staged call — save_checkpoint's use)."""
     a = _arena(module)
     if a is None:
         return OrderedDict((k, v.detach().cpu()) for k, v in module.state_dict().items())
     pin = a.f32.device.type == "cuda"
-    h32 = torch.empty(a.f32.shape, dtype=a.f32.dtype, pin_memory=pin)
-    h64 = torch.empty(a.i64.shape, dtype=a.i64.dtype, pin_memory=pin)
+    stage = getattr(a, "_ckpt_stage", None) if _stage else None
+    if stage is None:
+        h32 = torch.empty(a.f32.shape, dtype=a.f32.dtype, pin_memory=pin)
+        h64 = torch.empty(a.i64.shape, dtype=a.i64.dtype, pin_memory=pin)
+        if _stage:
+            a._ckpt_stage = (h32, h64)
+    else:
+        h32, h64 = stage
     h32.copy_(a.f32, non_blocking=pin)
     h64.copy_(a.i64, non_blocking=pin)
     if pin:
@@ -69,7 +78,7 @@ def save_checkpoint(state: dict, is_best: bool, model_dir: str,
     state = dict(state)
     sd = state.get("state_dict")
     if isinstance(sd, torch.nn.Module):
-        state["state_dict"] = bucket_state_dict(sd)
+        state["state_dict"] = bucket_state_dict(sd, _stage=True)  # serialised before return
     path = os.path.join(model_dir, filename)
     torch.save(state, path)
     if is_best:
