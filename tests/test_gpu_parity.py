@@ -65,6 +65,58 @@ def test_reduce_matches_oracle(lib, n, mode):
         assert k == k2 and bits_equal(g, want), (n, mode, k)
 
 
+@pytest.mark.parametrize("n", [511, 512, 1000, 4095, 4096])
+def test_many_clients_up_to_the_maximum(lib, n):
+    """Up to FA_MAX_CLIENTS: the device pointer table, the cascade's third
+    level (promotion after 16^3 = 4096 rows) and every column rule, against
+    the oracle and torch itself.  torch runs single-threaded here: with
+    N*M >= 32768 its column chunking across threads can move a tensor's last
+    few tail columns to another order; the engine defines the
+    single-thread order, which is what torch produces for the reference's
+    layouts."""
+    man = _rand_manifest(np.random.default_rng(n), [0, 1, 5, 33, 100, 1060])
+    layout = BucketLayout.from_manifest(man)
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    out32, out64 = _reduce(lib, layout, states_to_buckets(layout, states, DEV))
+    got = buckets_to_state(layout, out32, out64)
+    for j, ((k, want), (k2, g)) in enumerate(zip(O.aggregate_state(states), got)):
+        assert k == k2 and bits_equal(g, want), (n, k)
+        x = np.stack([s[j][1] for s in states])
+        if x.dtype == np.float32:
+            nthr = torch.get_num_threads()
+            torch.set_num_threads(1)
+            try:
+                ref = torch.from_numpy(x).mean(0).numpy()
+            finally:
+                torch.set_num_threads(nthr)
+            assert bits_equal(g, ref), (n, k, "vs torch")
+
+
+def test_weighted_many_clients(lib):
+    n = 1000
+    man = _rand_manifest(None, [1, 7, 100, 2049])
+    layout = BucketLayout.from_manifest(man)
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    w = O.weights_from_sizes(np.arange(1, n + 1) * 13)
+    out32, out64 = _reduce(lib, layout, states_to_buckets(layout, states, DEV), weights=w)
+    got = dict(buckets_to_state(layout, out32, out64))
+    for j, (k, _) in enumerate(states[0]):
+        x = np.stack([s[j][1] for s in states])
+        want = O.mean_i64_trunc(x) if x.dtype == np.int64 else O.weighted_sum0(x, w)
+        assert bits_equal(got[k], want), k
+
+
+def test_too_many_clients_is_refused(lib):
+    man = _rand_manifest(None, [4])
+    layout = BucketLayout.from_manifest(man)
+    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel)
+    n = lib.FA_MAX_CLIENTS + 1
+    b = torch.zeros(64, device=DEV)
+    rc = lib.lib.fa_reduce(plan.handle, lib.ptr_array([b.data_ptr()] * n), None, n, None,
+                           b.data_ptr(), None, 0, None)
+    assert rc == lib.FA_E_RANGE
+
+
 @pytest.mark.parametrize("tile_elems", [1024, 2048, 4096])
 def test_tile_sizes_bit_exact(lib, tile_elems):
     n = 20
