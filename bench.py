@@ -135,6 +135,10 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
     t_loop, reps = time_call(lambda: reference_loop(g, mods), 5, budget_s * 0.5)
     states = [m.state_dict() for m in mods]
     t_core, _ = time_call(lambda: arithmetic_core(states), 3, budget_s * 0.1)
+    # BASELINE config 1's shape: the loop over 2 clients (beside bench's
+    # cfg1_host_resident_n2 drop-in timing)
+    g2 = Holder()
+    t_cfg1, reps_cfg1 = time_call(lambda: reference_loop(g2, mods[:2]), 5, budget_s * 0.1)
     # the same on one thread (SURVEY.md §8 d asks for both)
     torch.set_num_threads(1)
     t_loop1, reps1 = time_call(lambda: reference_loop(g, mods), 3, budget_s * 0.3)
@@ -151,6 +155,7 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
             "loop_ms": round(t_loop * 1e3, 2), "core_ms": round(t_core * 1e3, 2),
             "one_thread": {"loop_ms": round(t_loop1 * 1e3, 2), "core_ms": round(t_core1 * 1e3, 2),
                            "loop_GBps": round(nbytes / t_loop1 / 1e9, 3), "runs": reps1},
+            "cfg1_n2": {"loop_ms": round(t_cfg1 * 1e3, 2), "runs": reps_cfg1},
             "host_cpus": os.cpu_count(), "cpu": _cpu_model()}
 
 
