@@ -38,6 +38,7 @@ FA_PLAN_TUNE_XCD = 16
 FA_PLAN_TUNE_WAVE_CONTIG = 32
 FA_PLAN_TUNE_ST_PLAIN = 64
 FA_PLAN_TUNE_LD_PLAIN = 128
+FA_PLAN_TUNE_ST_SC1 = 0x10000
 
 
 def FA_PLAN_TUNE_BLOCKS_PER_CU(c):

@@ -152,6 +152,21 @@ __device__ __forceinline__ void st4(float* p, f4 v) {
   else *reinterpret_cast<f4*>(p) = v;
 }
 
+// Result store of a vector tile.  POL bit 2: through a buffer op with the
+// sc1 cache-policy bit (explicit aux bits: 2 = nt, 16 = sc1) instead of the
+// global nt store; the descriptor is based at the tile start (uniform).
+template <int POL>
+__device__ __forceinline__ void st_out(float* out, int64_t start, int64_t off, f4 v) {
+  if constexpr ((POL & 4) != 0) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(out + start, (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(4 * (off - start)), 0,
+                                           (POL & 2) ? 18 : 16);
+  } else {
+    st4<(POL & 2) != 0>(out + off, v);
+  }
+}
+
 // -------------------------------------------------- vectorised cascade ----
 // ATen multi_row_sum over the n clients for 4*U columns per thread.  The
 // loop over clients is uniform (scalar control).  Clients go in batches of B:
@@ -285,7 +300,7 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
       s = add4(s, A.l3[u]);
     }
     const f4 r = sum_only ? s : div4s(s, fn);
-    st4<(POL & 2) != 0>(a.out32 + off[u], r);
+    st_out<POL>(a.out32, start, off[u], r);
     if (a.flags & FA_F_BCAST) {
       for (int i = 0; i < n; ++i) st4<(POL & 2) != 0>(const_cast<float*>(cptr32(a, i)) + off[u], r);
     }
@@ -664,12 +679,15 @@ hipError_t launch_one(const ReduceArgs& a, int ntiles, hipStream_t st) {
 
 template <int U, int B>
 hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, int pol, hipStream_t st) {
-  // pol: bit 0 = non-temporal loads, bit 1 = non-temporal stores (default 3)
+  // pol: bit 0 = non-temporal loads, bit 1 = non-temporal stores (default 3),
+  // bit 2 = result stores with sc1 (buffer op)
   if (deep) return w ? launch_one<U, B, true, true, 3>(a, ntiles, st)
                      : launch_one<U, B, true, false, 3>(a, ntiles, st);
   if (w) return pol == 3 ? launch_one<U, B, false, true, 3>(a, ntiles, st)
                          : launch_one<U, B, false, true, 0>(a, ntiles, st);
   switch (pol) {
+    case 5: return launch_one<U, B, false, false, 5>(a, ntiles, st);
+    case 7: return launch_one<U, B, false, false, 7>(a, ntiles, st);
     case 0: return launch_one<U, B, false, false, 0>(a, ntiles, st);
     case 1: return launch_one<U, B, false, false, 1>(a, ntiles, st);
     case 2: return launch_one<U, B, false, false, 2>(a, ntiles, st);
@@ -684,6 +702,7 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   int nt = (pflags & FA_PLAN_TUNE_NO_NT) ? 0 : 3;
   if (pflags & FA_PLAN_TUNE_ST_PLAIN) nt &= ~2;
   if (pflags & FA_PLAN_TUNE_LD_PLAIN) nt &= ~1;
+  if (pflags & FA_PLAN_TUNE_ST_SC1) nt |= 4;
   const bool small = w || a.n < 16;
   const int b_env = (pflags & FA_PLAN_TUNE_BATCH8) ? 8
                     : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (small ? 8 : 16);

@@ -80,6 +80,7 @@ extern "C" {
 #define FA_PLAN_TUNE_WAVE_CONTIG 32u /* tuning: each wave reads adjacent KiBs  */
 #define FA_PLAN_TUNE_ST_PLAIN 64u  /* tuning: plain (temporal) stores only     */
 #define FA_PLAN_TUNE_LD_PLAIN 128u /* tuning: plain (temporal) loads only      */
+#define FA_PLAN_TUNE_ST_SC1 0x10000u /* tuning: result stores with sc1         */
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
 #define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
 /* tuning: persistent grid of 256*k workgroups striding over the tiles */
