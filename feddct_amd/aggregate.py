@@ -102,6 +102,7 @@ class Engine:
         else:
             self._reduce_host(layout, ga, cas, weights, fuse_bcast)
         ga.unpack()
+        ga.mark_written()
         if broadcast and not fuse_bcast:
             for i, c in enumerate(cas):
                 if i == bad:
@@ -112,9 +113,11 @@ class Engine:
                 c.f32.copy_(ga.f32)
                 c.i64.copy_(ga.i64)
                 c.unpack()
+                c.mark_written()
         elif fuse_bcast:
             for c in cas:
                 c.unpack()
+                c.mark_written()
 
     def _weights_arg(self, weights, n):
         if weights is None:

@@ -20,6 +20,7 @@ from __future__ import annotations
 from typing import Dict, List, Tuple
 
 import torch
+from torch.autograd.graph import increment_version
 
 from .layout import KIND_I64, KIND_PACKF, BucketLayout
 
@@ -112,6 +113,15 @@ class ModuleArena:
                 t.data = view
                 self._checks.append((d, name, t, view.data_ptr()))
         self.module_ref = module
+        # tensors the kernel writes behind autograd's back (raw pointers)
+        self._written = tuple(t for _, _, t, _ in self._checks)
+
+    def mark_written(self) -> None:
+        """Bump the autograd version counter of every bucket-backed tensor,
+        as the reference's ``load_state_dict`` (an in-place ``copy_``) does:
+        a graph that saved the old values then fails loudly in backward
+        instead of using the overwritten ones.  One C++ call per arena."""
+        increment_version(self._written)
 
     def valid(self) -> bool:
         if self._gen != _STRUCT_GEN[0]:

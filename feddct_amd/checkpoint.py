@@ -124,5 +124,6 @@ def load_into(module: torch.nn.Module, state_dict) -> None:
                 if s.kind != "f32":
                     dst = module.state_dict()[s.key]
                     dst.copy_(state_dict[s.key])
+        a.mark_written()
         return
     module.load_state_dict(state_dict)

@@ -119,3 +119,21 @@ def test_structure_change_after_binding_is_seen():
     L2 = e.layout_of(m)
     assert "1.extra_stat" in L2.keys and L2 is not L
     del other
+
+
+def test_kernel_writes_bump_autograd_versions():
+    """The kernel overwrites bucket memory through raw pointers; like the
+    reference's load_state_dict (an in-place copy_), the shim then bumps every
+    bound tensor's version, so a graph that saved the old values fails loudly
+    in backward instead of silently using the new ones."""
+    m = net()
+    a = ModuleArena(m, BucketLayout.from_state_dict(m.state_dict()))
+    w = m[2].weight
+    y = (w * w).sum()  # saves w for backward
+    v0 = w._version
+    a.mark_written()
+    assert w._version > v0
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        y.backward()
+    # a graph built after the write is fine
+    (w * w).sum().backward()

@@ -31,3 +31,23 @@ def test_round_loop_bit_exact(mu):
     from fedavg_loop import run
     log = run(rounds=3, clients=5, steps=3, mu=mu, check=_check)
     assert all(e["bit_exact_vs_reference"] for e in log), log
+
+
+def test_stale_graph_fails_like_load_state_dict():
+    """After the round (kernel writes behind autograd's back) a graph that
+    saved a client's pre-round weights fails in backward, as it does after
+    the reference's load_state_dict broadcast."""
+    import torch
+    from feddct_amd.aggregate import server_aggregate
+    dev = torch.device("cuda", 0)
+
+    def mk():
+        return torch.nn.Sequential(torch.nn.Linear(8, 4), torch.nn.BatchNorm1d(4)).to(dev)
+    g, clients = mk(), [mk() for _ in range(3)]
+    server_aggregate(g, clients)  # binds the arenas
+    w = clients[1][0].weight
+    y = (w * w).sum()
+    server_aggregate(g, clients)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        y.backward()
+    (clients[1][0].weight ** 2).sum().backward()  # a fresh graph is fine
