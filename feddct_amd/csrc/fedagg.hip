@@ -141,29 +141,45 @@ __device__ __forceinline__ f4 div4s(f4 a, float s) {
             __fdiv_rn(a.w, s)};
 }
 
+// Global-address-space views: loads/stores compile to global_* (not flat_*)
+// instructions; with a uniform base and a 32-bit vector index they take the
+// SGPR-base + one-VGPR-offset form, so a batch of B clients costs no 64-bit
+// per-lane address arithmetic and no address VGPRs.
+typedef __attribute__((address_space(1))) const f4 gcf4;
+typedef __attribute__((address_space(1))) f4 gf4;
+
+template <bool NT>
+__device__ __forceinline__ f4 ldg4(const float* base, uint32_t vidx) {
+  gcf4* g = (gcf4*)base;
+  if constexpr (NT) return __builtin_nontemporal_load(g + vidx);
+  else return g[vidx];
+}
+template <bool NT>
+__device__ __forceinline__ void stg4(float* base, uint32_t vidx, f4 v) {
+  gf4* g = (gf4*)base;
+  if constexpr (NT) __builtin_nontemporal_store(v, g + vidx);
+  else g[vidx] = v;
+}
 template <bool NT>
 __device__ __forceinline__ f4 ld4(const float* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
-  else return *reinterpret_cast<const f4*>(p);
+  return ldg4<NT>(p, 0);
 }
 template <bool NT>
 __device__ __forceinline__ void st4(float* p, f4 v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
-  else *reinterpret_cast<f4*>(p) = v;
+  stg4<NT>(p, 0, v);
 }
 
 // Result store of a vector tile.  POL bit 2: through a buffer op with the
 // sc1 cache-policy bit (explicit aux bits: 2 = nt, 16 = sc1) instead of the
 // global nt store; the descriptor is based at the tile start (uniform).
 template <int POL>
-__device__ __forceinline__ void st_out(float* out, int64_t start, int64_t off, f4 v) {
+__device__ __forceinline__ void st_out(float* out, int64_t start, uint32_t vidx, f4 v) {
   if constexpr ((POL & 4) != 0) {
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(out + start, (short)0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(4 * (off - start)), 0,
-                                           (POL & 2) ? 18 : 16);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(16 * vidx), 0, (POL & 2) ? 18 : 16);
   } else {
-    st4<(POL & 2) != 0>(out + off, v);
+    stg4<(POL & 2) != 0>(out + start, vidx, v);
   }
 }
 
@@ -205,17 +221,17 @@ __device__ __forceinline__ void promote(Acc<U, DEEP>& A, int ii, int lp, int mas
 // One batch of NB clients starting at b0.  FULL: every lane's U vectors are
 // inside the tile (no per-lane predicate).
 template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL>
-__device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0,
-                                      const int64_t (&off)[U], const bool (&ok)[U],
+__device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t start,
+                                      const uint32_t (&vi)[U], const bool (&ok)[U],
                                       int lp, int mask) {
   f4 x[NB][U];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const float* p = cptr32(a, b0 + b);
+    const float* p = cptr32(a, b0 + b) + start;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if constexpr (FULL) x[b][u] = ld4<(POL & 1) != 0>(p + off[u]);
-      else x[b][u] = ok[u] ? ld4<(POL & 1) != 0>(p + off[u]) : f4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
+      else x[b][u] = ok[u] ? ldg4<(POL & 1) != 0>(p, vi[u]) : f4{0.f, 0.f, 0.f, 0.f};
     }
   }
 #pragma unroll
@@ -234,17 +250,17 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0,
 // every step guarded by a uniform (scalar) branch.
 template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL>
 __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, int nb,
-                                           const int64_t (&off)[U], const bool (&ok)[U],
-                                           int lp, int mask) {
+                                           int64_t start, const uint32_t (&vi)[U],
+                                           const bool (&ok)[U], int lp, int mask) {
   f4 x[NB][U];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     if (b < nb) {
-      const float* p = cptr32(a, b0 + b);
+      const float* p = cptr32(a, b0 + b) + start;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if constexpr (FULL) x[b][u] = ld4<(POL & 1) != 0>(p + off[u]);
-        else x[b][u] = ok[u] ? ld4<(POL & 1) != 0>(p + off[u]) : f4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
+        else x[b][u] = ok[u] ? ldg4<(POL & 1) != 0>(p, vi[u]) : f4{0.f, 0.f, 0.f, 0.f};
       }
     }
   }
@@ -269,7 +285,7 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
   const int lp = level_power(n);
   const int mask = (1 << lp) - 1;
   Acc<U, DEEP> A;
-  int64_t off[U];
+  uint32_t vi[U];
   bool ok[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -278,14 +294,15 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
     const int v = (a.flags & kWaveContig)
                       ? (int)(threadIdx.x & ~63u) * U + u * 64 + (int)(threadIdx.x & 63u)
                       : (int)threadIdx.x + u * kBlock;
-    off[u] = start + 4 * (int64_t)v;
+    vi[u] = (uint32_t)v;
     ok[u] = FULL || 4 * v < count;
     A.l0[u] = A.l1[u] = A.l2[u] = A.l3[u] = f4{0.f, 0.f, 0.f, 0.f};
   }
   int b0 = 0;
   for (; b0 + B <= n; b0 += B)
-    batch<U, B, FULL, DEEP, WEIGHTED, POL>(a, A, b0, off, ok, lp, mask);
-  if (b0 < n) batch_tail<U, B, FULL, DEEP, WEIGHTED, POL>(a, A, b0, n - b0, off, ok, lp, mask);
+    batch<U, B, FULL, DEEP, WEIGHTED, POL>(a, A, b0, start, vi, ok, lp, mask);
+  if (b0 < n)
+    batch_tail<U, B, FULL, DEEP, WEIGHTED, POL>(a, A, b0, n - b0, start, vi, ok, lp, mask);
 
   const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
   const float fn = (float)n;
@@ -300,9 +317,10 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
       s = add4(s, A.l3[u]);
     }
     const f4 r = sum_only ? s : div4s(s, fn);
-    st_out<POL>(a.out32, start, off[u], r);
+    st_out<POL>(a.out32, start, vi[u], r);
     if (a.flags & FA_F_BCAST) {
-      for (int i = 0; i < n; ++i) st4<(POL & 2) != 0>(const_cast<float*>(cptr32(a, i)) + off[u], r);
+      for (int i = 0; i < n; ++i)
+        stg4<(POL & 2) != 0>(const_cast<float*>(cptr32(a, i)) + start, vi[u], r);
     }
   }
 }

@@ -145,6 +145,42 @@ __global__ __launch_bounds__(256) void nstream_defer(const float* __restrict__ b
   }
 }
 
+// Persistent park: each workgroup of TPB threads reduces S sub-tiles of
+// TPB*4 floats (contiguous range, or interleaved with the other workgroups:
+// sub-tile s of workgroup g at s*G + g), keeps the S results in registers and
+// stores them all at the end (PARK), so writes come in one burst after reads.
+template <int S, int NB, int TPB, bool PARK, bool INTER>
+__global__ __launch_bounds__(TPB) void persist(const float* __restrict__ base, int64_t stride,
+                                               int n, float* __restrict__ out) {
+  f4 park[S];
+#pragma unroll
+  for (int sidx = 0; sidx < S; ++sidx) {
+    const int64_t tile = INTER ? (int64_t)sidx * gridDim.x + blockIdx.x
+                               : (int64_t)blockIdx.x * S + sidx;
+    const int64_t off = tile * TPB * 4 + 4 * (int64_t)threadIdx.x;
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+    int b0 = 0;
+    for (; b0 + NB <= n; b0 += NB) {
+      f4 x[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) x[b] = ld(base + (b0 + b) * stride + off);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) acc += x[b];
+    }
+    for (; b0 < n; ++b0) acc += ld(base + b0 * stride + off);
+    if (PARK) park[sidx] = acc;
+    else st(out + off, acc);
+  }
+  if (PARK) {
+#pragma unroll
+    for (int sidx = 0; sidx < S; ++sidx) {
+      const int64_t tile = INTER ? (int64_t)sidx * gridDim.x + blockIdx.x
+                                 : (int64_t)blockIdx.x * S + sidx;
+      st(out + tile * TPB * 4 + 4 * (int64_t)threadIdx.x, park[sidx]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void copy4(const float* __restrict__ s, float* __restrict__ d,
                                              int64_t nv) {
   for (int64_t v = blockIdx.x * 256ll + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256)
@@ -207,10 +243,26 @@ int main(int argc, char** argv) {
       time_ms([&] { nstream_pol<2, 16, LA, SA><<<m / 2048, 256>>>(base, stride, n, out); }, \
               20),                                                                     \
       rbytes + wbytes)
-    POL(2, 2); POL(2, 16); POL(2, 17); POL(2, 3);
-    POL(3, 2); POL(3, 16); POL(3, 17); POL(3, 3);
-    POL(18, 2); POL(18, 16); POL(18, 17); POL(18, 3);
-    POL(19, 2); POL(19, 16); POL(19, 17); POL(19, 3);
+    {
+      const int64_t mp = 256ll * 10 * 4096;  // 10,485,760 floats: 10 sub-tiles per CU
+      const double rb = (double)n * mp * 4, wb = (double)mp * 4;
+#define PERS(S, NB, TPB, PARK, INTER, G)                                                   \
+  rep("persist_S" #S "_B" #NB "_T" #TPB "_park" #PARK "_inter" #INTER "_G" #G,              \
+      time_ms([&] { persist<S, NB, TPB, PARK, INTER><<<G, TPB>>>(base, stride, n, out); }, 20), \
+      rb + wb)
+      PERS(10, 8, 1024, true, false, 256);
+      PERS(10, 8, 1024, true, true, 256);
+      PERS(10, 16, 1024, true, false, 256);
+      PERS(10, 4, 1024, true, false, 256);
+      PERS(10, 8, 512, true, false, 512);
+      PERS(10, 8, 256, true, false, 1024);
+      PERS(20, 8, 512, true, false, 256);
+      PERS(20, 8, 512, true, true, 256);
+      PERS(5, 8, 1024, true, false, 512);
+      PERS(10, 8, 1024, false, false, 256);
+      rep("same_bytes_U2B16", time_ms([&] { nstream<2, 16, true><<<mp / 2048, 256>>>(base, stride, n, out); }, 20), rb + wb);
+      rep("same_bytes_read_only", time_ms([&] { nstream<2, 16, false><<<mp / 2048, 256>>>(base, stride, n, out); }, 20), rb);
+    }
     const int64_t half = big / 2;
     rep("copy_float4",
         time_ms([&] { copy4<<<4096, 256>>>(base, base + half, half / 4); }, 20),
