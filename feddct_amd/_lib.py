@@ -39,6 +39,8 @@ FA_PLAN_TUNE_WAVE_CONTIG = 32
 FA_PLAN_TUNE_ST_PLAIN = 64
 FA_PLAN_TUNE_LD_PLAIN = 128
 FA_PLAN_TUNE_ST_SC1 = 0x10000
+FA_PLAN_TUNE_BATCH1 = 0x20000
+FA_PLAN_TUNE_BATCH4 = 0x40000
 
 
 def FA_PLAN_TUNE_BLOCKS_PER_CU(c):

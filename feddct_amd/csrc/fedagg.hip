@@ -111,6 +111,29 @@ __device__ __forceinline__ float cw(KArgs& a, int i) {
   return a.n <= kInline ? a.w[i] : a.tabw[i];
 }
 
+// Pointer source of the vector path.  TAB (the DEEP kernels, n >= 256): the
+// device table through a constant-address-space view (read-only for the
+// launch), so a uniform index is one scalar load: 2-10 % faster at 300
+// clients than generic loads (2 % slower at 200, hence only from 256 on).
+// Otherwise the runtime-selecting accessor above.  Measured
+// (tools/exp_ab.py, same box, one process): compiled this way the inline
+// kernel issues each client's U loads behind a vmcnt(0) wait and runs
+// 141-146 us on the cfg2 workload; reading a.c32[i] directly lets the
+// compiler issue the whole batch's loads back to back, which is 4-6 %
+// SLOWER (148-156 us) at every batch size tried (1, 4, 8, 16 clients).
+typedef const float* f32p;
+#define FA_CONST __attribute__((address_space(4)))
+template <bool TAB>
+__device__ __forceinline__ const float* vptr32(KArgs& a, int i) {
+  if constexpr (TAB) return ((const FA_CONST f32p*)a.tab32)[i];
+  else return cptr32(a, i);
+}
+template <bool TAB>
+__device__ __forceinline__ float vw(KArgs& a, int i) {
+  if constexpr (TAB) return ((const FA_CONST float*)a.tabw)[i];
+  else return cw(a, i);
+}
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr unsigned kWaveContig = 0x200u;  // internal a.flags bit (FA_PLAN_TUNE_WAVE_CONTIG)
@@ -227,7 +250,7 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t
   f4 x[NB][U];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const float* p = cptr32(a, b0 + b) + start;
+    const float* p = vptr32<DEEP>(a, b0 + b) + start;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
@@ -239,7 +262,7 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       f4 v = x[b][u];
-      if constexpr (WEIGHTED) v = mul4s(v, cw(a, b0 + b));
+      if constexpr (WEIGHTED) v = mul4s(v, vw<DEEP>(a, b0 + b));
       A.l0[u] = add4(A.l0[u], v);
     }
     promote<U, DEEP>(A, b0 + b + 1, lp, mask);
@@ -256,7 +279,7 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     if (b < nb) {
-      const float* p = cptr32(a, b0 + b) + start;
+      const float* p = vptr32<DEEP>(a, b0 + b) + start;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
@@ -270,7 +293,7 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         f4 v = x[b][u];
-        if constexpr (WEIGHTED) v = mul4s(v, cw(a, b0 + b));
+        if constexpr (WEIGHTED) v = mul4s(v, vw<DEEP>(a, b0 + b));
         A.l0[u] = add4(A.l0[u], v);
       }
       promote<U, DEEP>(A, b0 + b + 1, lp, mask);
@@ -320,7 +343,7 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
     st_out<POL>(a.out32, start, vi[u], r);
     if (a.flags & FA_F_BCAST) {
       for (int i = 0; i < n; ++i)
-        stg4<(POL & 2) != 0>(const_cast<float*>(cptr32(a, i)) + start, vi[u], r);
+        stg4<(POL & 2) != 0>(const_cast<float*>(vptr32<DEEP>(a, i)) + start, vi[u], r);
     }
   }
 }
@@ -342,24 +365,30 @@ struct SrcI64 {
 };
 
 // multi_row_sum over rows first, first+stride, ... (count rows), 1 column.
+// The four level accumulators are named variables (a runtime-indexed array
+// would live in scratch).
 template <class Src>
 __device__ float cascade_seq(const Src& src, int64_t e, int first, int stride,
                              int count) {
   const int lp = level_power(count);
   const int step = 1 << lp, mask = step - 1;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   int i = 0;
   for (; i + step <= count;) {
-    for (int j = 0; j < step; ++j, ++i) acc[0] = __fadd_rn(acc[0], src(first + i * stride, e));
-    for (int j = 1; j < 4; ++j) {
-      acc[j] = __fadd_rn(acc[j], acc[j - 1]);
-      acc[j - 1] = 0.f;
-      if (i & (mask << (j * lp))) break;
-    }
+    for (int j = 0; j < step; ++j, ++i) a0 = __fadd_rn(a0, src(first + i * stride, e));
+    a1 = __fadd_rn(a1, a0);
+    a0 = 0.f;
+    if (i & (mask << lp)) continue;
+    a2 = __fadd_rn(a2, a1);
+    a1 = 0.f;
+    if (i & (mask << (2 * lp))) continue;
+    a3 = __fadd_rn(a3, a2);
+    a2 = 0.f;
   }
-  for (; i < count; ++i) acc[0] = __fadd_rn(acc[0], src(first + i * stride, e));
-  for (int j = 1; j < 4; ++j) acc[0] = __fadd_rn(acc[0], acc[j]);
-  return acc[0];
+  for (; i < count; ++i) a0 = __fadd_rn(a0, src(first + i * stride, e));
+  a0 = __fadd_rn(a0, a1);
+  a0 = __fadd_rn(a0, a2);
+  return __fadd_rn(a0, a3);
 }
 
 // ATen row_sum: ILP-4 over rows first + k*stride (count rows).
@@ -367,11 +396,14 @@ template <class Src>
 __device__ float ilp4_seq(const Src& src, int64_t e, int first, int stride,
                           int count) {
   const int q = count / 4;
-  float p[4];
-  for (int k = 0; k < 4; ++k) p[k] = cascade_seq(src, e, first + k * stride, 4 * stride, q);
-  for (int i = 4 * q; i < count; ++i) p[0] = __fadd_rn(p[0], src(first + i * stride, e));
-  for (int k = 1; k < 4; ++k) p[0] = __fadd_rn(p[0], p[k]);
-  return p[0];
+  float p0 = cascade_seq(src, e, first, 4 * stride, q);
+  const float p1 = cascade_seq(src, e, first + stride, 4 * stride, q);
+  const float p2 = cascade_seq(src, e, first + 2 * stride, 4 * stride, q);
+  const float p3 = cascade_seq(src, e, first + 3 * stride, 4 * stride, q);
+  for (int i = 4 * q; i < count; ++i) p0 = __fadd_rn(p0, src(first + i * stride, e));
+  p0 = __fadd_rn(p0, p1);
+  p0 = __fadd_rn(p0, p2);
+  return __fadd_rn(p0, p3);
 }
 
 // ATen vectorized_inner_sum (M == 1, n >= 8): 8 lanes, each an ILP-4 over
@@ -387,7 +419,7 @@ __device__ float inner_seq(const Src& src, int64_t e, int n) {
 }
 
 template <bool WEIGHTED>
-__device__ void tile_scalar(KArgs& a, const Tile& t) {
+__device__ void tile_scalar(KArgs& a, Tile t) {
   const int j = threadIdx.x;
   if (j >= t.count) return;
   const int64_t e = t.start + j;
@@ -715,6 +747,7 @@ hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, int pol,
 
 hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pflags,
                          hipStream_t st) {
+  // DEEP (n >= 256): cascade levels 2-3 and the constant-space table loads
   const bool deep = a.n >= 256;
   const bool w = a.flags & 0x100u;  // internal: weighted
   int nt = (pflags & FA_PLAN_TUNE_NO_NT) ? 0 : 3;
@@ -722,17 +755,29 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   if (pflags & FA_PLAN_TUNE_LD_PLAIN) nt &= ~1;
   if (pflags & FA_PLAN_TUNE_ST_SC1) nt |= 4;
   const bool small = w || a.n < 16;
-  const int b_env = (pflags & FA_PLAN_TUNE_BATCH8) ? 8
+  const int b_env = (pflags & FA_PLAN_TUNE_BATCH1)    ? 1
+                    : (pflags & FA_PLAN_TUNE_BATCH4)  ? 4
+                    : (pflags & FA_PLAN_TUNE_BATCH8)  ? 8
                     : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (small ? 8 : 16);
   const unsigned cap = (pflags >> 8) & 0xFu;  // FA_PLAN_TUNE_BLOCKS_PER_CU(c)
   t_dyn_lds = cap ? (160u * 1024u / cap) & ~1023u : 0;
   t_grid_cap = 256 * (int)((pflags >> 12) & 0xFu);  // FA_PLAN_TUNE_PERSIST(k)
   switch (vec_u) {
-    case 1: return b_env == 16 ? launch_u<1, 16>(a, ntiles, deep, w, nt, st)
-                               : launch_u<1, 8>(a, ntiles, deep, w, nt, st);
+    case 1:
+      switch (b_env) {
+        case 1: return launch_u<1, 1>(a, ntiles, deep, w, nt, st);
+        case 4: return launch_u<1, 4>(a, ntiles, deep, w, nt, st);
+        case 16: return launch_u<1, 16>(a, ntiles, deep, w, nt, st);
+        default: return launch_u<1, 8>(a, ntiles, deep, w, nt, st);
+      }
     case 4: return launch_u<4, 8>(a, ntiles, deep, w, nt, st);
-    default: return b_env == 16 ? launch_u<2, 16>(a, ntiles, deep, w, nt, st)
-                                : launch_u<2, 8>(a, ntiles, deep, w, nt, st);
+    default:
+      switch (b_env) {
+        case 1: return launch_u<2, 1>(a, ntiles, deep, w, nt, st);
+        case 4: return launch_u<2, 4>(a, ntiles, deep, w, nt, st);
+        case 16: return launch_u<2, 16>(a, ntiles, deep, w, nt, st);
+        default: return launch_u<2, 8>(a, ntiles, deep, w, nt, st);
+      }
   }
 }
 

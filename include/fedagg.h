@@ -81,6 +81,8 @@ extern "C" {
 #define FA_PLAN_TUNE_ST_PLAIN 64u  /* tuning: plain (temporal) stores only     */
 #define FA_PLAN_TUNE_LD_PLAIN 128u /* tuning: plain (temporal) loads only      */
 #define FA_PLAN_TUNE_ST_SC1 0x10000u /* tuning: result stores with sc1         */
+#define FA_PLAN_TUNE_BATCH1 0x20000u /* tuning: 1 client per load batch         */
+#define FA_PLAN_TUNE_BATCH4 0x40000u /* tuning: 4 clients per load batch        */
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
 #define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
 /* tuning: persistent grid of 256*k workgroups striding over the tiles */

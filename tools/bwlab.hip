@@ -181,6 +181,46 @@ __global__ __launch_bounds__(TPB) void persist(const float* __restrict__ base, i
   }
 }
 
+// Rolling window: at most W clients' loads (W*U per lane) in flight; the load
+// of client b+W is issued right after client b is consumed.  SERIAL: the
+// old product shape (issue U loads, wait for them, add, next client).
+template <int U, int W>
+__global__ __launch_bounds__(256) void nstream_win(const float* __restrict__ base,
+                                                   int64_t stride, int n,
+                                                   float* __restrict__ out) {
+  const int64_t t0 = (int64_t)blockIdx.x * U * 1024;
+  f4 acc[U];
+  int64_t off[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    off[u] = t0 + 4 * (int64_t)(threadIdx.x + u * 256);
+    acc[u] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  f4 x[W][U];
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[w][u] = w < n ? ld(base + w * stride + off[u]) : f4{0, 0, 0, 0};
+  int b = 0;
+  for (; b + W <= n; b += W) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[u] += x[w][u];
+        if (b + w + W < n) x[w][u] = ld(base + (b + w + W) * stride + off[u]);
+      }
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    if (b + w < n)
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] += x[w][u];
+#pragma unroll
+  for (int u = 0; u < U; ++u) st(out + off[u], acc[u]);
+}
+
 __global__ __launch_bounds__(256) void copy4(const float* __restrict__ s, float* __restrict__ d,
                                              int64_t nv) {
   for (int64_t v = blockIdx.x * 256ll + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256)
@@ -243,26 +283,12 @@ int main(int argc, char** argv) {
       time_ms([&] { nstream_pol<2, 16, LA, SA><<<m / 2048, 256>>>(base, stride, n, out); }, \
               20),                                                                     \
       rbytes + wbytes)
-    {
-      const int64_t mp = 256ll * 10 * 4096;  // 10,485,760 floats: 10 sub-tiles per CU
-      const double rb = (double)n * mp * 4, wb = (double)mp * 4;
-#define PERS(S, NB, TPB, PARK, INTER, G)                                                   \
-  rep("persist_S" #S "_B" #NB "_T" #TPB "_park" #PARK "_inter" #INTER "_G" #G,              \
-      time_ms([&] { persist<S, NB, TPB, PARK, INTER><<<G, TPB>>>(base, stride, n, out); }, 20), \
-      rb + wb)
-      PERS(10, 8, 1024, true, false, 256);
-      PERS(10, 8, 1024, true, true, 256);
-      PERS(10, 16, 1024, true, false, 256);
-      PERS(10, 4, 1024, true, false, 256);
-      PERS(10, 8, 512, true, false, 512);
-      PERS(10, 8, 256, true, false, 1024);
-      PERS(20, 8, 512, true, false, 256);
-      PERS(20, 8, 512, true, true, 256);
-      PERS(5, 8, 1024, true, false, 512);
-      PERS(10, 8, 1024, false, false, 256);
-      rep("same_bytes_U2B16", time_ms([&] { nstream<2, 16, true><<<mp / 2048, 256>>>(base, stride, n, out); }, 20), rb + wb);
-      rep("same_bytes_read_only", time_ms([&] { nstream<2, 16, false><<<mp / 2048, 256>>>(base, stride, n, out); }, 20), rb);
-    }
+#define WIN(U, W)                                                                         \
+  rep("win_U" #U "_W" #W,                                                                 \
+      time_ms([&] { nstream_win<U, W><<<m / (U * 1024), 256>>>(base, stride, n, out); }, 20), \
+      rbytes + wbytes)
+    WIN(2, 1); WIN(2, 2); WIN(2, 3); WIN(2, 4); WIN(2, 6); WIN(2, 8); WIN(2, 16);
+    WIN(1, 1); WIN(1, 2); WIN(1, 4); WIN(1, 8); WIN(4, 1); WIN(4, 2);
     const int64_t half = big / 2;
     rep("copy_float4",
         time_ms([&] { copy4<<<4096, 256>>>(base, base + half, half / 4); }, 20),

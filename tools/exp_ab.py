@@ -1,6 +1,6 @@
 """A/B: the in-tree libfedagg.so against another build of the same ABI
 (e.g. the previous commit's, tools/libfedagg_ab.so) on the same workload,
-interleaved rounds in one process.  Usage: exp_ab.py OTHER.so LAYOUT N ROUNDS"""
+interleaved rounds in one process.  Usage: exp_ab.py OTHER.so[,OTHER2.so...] LAYOUT N ROUNDS"""
 import ctypes
 import json
 import os
@@ -24,7 +24,9 @@ def main():
     nbytes = lay.algorithmic_bytes(n)
     a32 = _lib.ptr_array([c[0].data_ptr() for c in clients])
     a64 = _lib.ptr_array([c[1].data_ptr() for c in clients])
-    libs = {"intree": _lib.lib, "other": ctypes.CDLL(os.path.abspath(other))}
+    libs = {"intree": _lib.lib}
+    for o in other.split(","):
+        libs[os.path.basename(o)] = ctypes.CDLL(os.path.abspath(o))
     runs = {}
     for name, L in libs.items():
         L.fa_plan_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
