@@ -95,9 +95,16 @@ class Comm:
         rank 0's id travels over the group."""
         import torch.distributed as dist
         world, rank = dist.get_world_size(group), dist.get_rank(group)
-        obj = [unique_id() if rank == 0 else None]
+        obj = [None]
+        if rank == 0:
+            try:
+                obj = [unique_id()]
+            except _lib.FedaggError as e:  # every rank must leave the broadcast
+                obj = [repr(e)]
         src = 0 if group is None else dist.get_global_rank(group, 0)
         dist.broadcast_object_list(obj, src=src, group=group)
+        if not isinstance(obj[0], bytes):
+            raise _lib.FedaggError(f"fa_comm_unique_id failed on rank 0: {obj[0]}")
         return cls(world, rank, obj[0])
 
     @classmethod
