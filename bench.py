@@ -282,6 +282,50 @@ def other_configs(dev, steps=20):
     return res
 
 
+def cfg5_sharded(dev, world, rank, group, steps):
+    """BASELINE config 5 on the N GPUs of this run: FedDCT sf4 C100, 24 slots
+    (main + proxy in one joint bucket), slots sharded contiguously over the
+    ranks (3 per GPU at N=8), global state to rank 0.  e1 (client shards +
+    chunked RCCL reduce) timed as a round; e2 (column stripes, P2P) timed and
+    its result checked bit-for-bit against the reference digests."""
+    from feddct_amd.dist import ShardedAggregator, StripedAggregator, shard_range
+    from feddct_amd.workload import joint_manifest
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        dig = json.load(f)
+    names = ("wrnsl16_8_sf4_c100_main", "wrnsl16_8_sf4_c100_proxy")
+    mans = [load_manifest(x) for x in names]
+    prefixes = ("0.", "1.")
+    lay = BucketLayout.from_manifest(joint_manifest(mans, prefixes))
+    n = 24
+    lo, hi = shard_range(n, world, rank)
+    cl = make_clients(lay, list(zip(mans, prefixes)), range(lo, hi), dev)
+    l32, l64 = [c[0] for c in cl], [c[1] for c in cl]
+    o32 = torch.zeros(max(lay.f32_numel, 64), dtype=torch.float32, device=dev)
+    o64 = torch.zeros(max(lay.i64_numel, 1), dtype=torch.int64, device=dev)
+    nbytes = lay.algorithmic_bytes(n)
+
+    def tmax(fn, k, w):
+        t, _ = timed_launches(fn, k, w, sync_group=group)
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+    agg = ShardedAggregator(lay, l32, l64, n, o32, o64, final="reduce")
+    t1 = tmax(agg.step, steps, 5)
+    s32, s64 = torch.zeros_like(o32), torch.zeros_like(o64)
+    sagg = StripedAggregator(lay, n, s32, s64, group=group, final="reduce")
+    t2 = tmax(lambda: sagg.step_device(l32, l64), max(3, steps // 10), 2)
+    out = {"slots": n, "slots_per_gpu": hi - lo, "algorithmic_bytes": nbytes,
+           "e1_ms": round(t1 * 1e3, 4), "e1_GBps": round(nbytes / t1 / 1e9, 2),
+           "e2_exact_ms": round(t2 * 1e3, 4), "e2_exact_GBps": round(nbytes / t2 / 1e9, 2)}
+    if rank == 0:
+        ok = all(digest_of(lay, s32, s64, pf) == dig[f"feddct/{nm}/n24"]
+                 for nm, pf in zip(names, prefixes))
+        out["e2_bit_exact_vs_reference_digest"] = bool(ok)
+        out["e1_max_abs_err_vs_exact"] = float((o32 - s32).abs().max())
+        out["e1_int64_bit_exact"] = bool(torch.equal(o64, s64))
+    return out
+
+
 def cfg1_host_resident(dev, reps=5):
     """BASELINE config 1's shape — FedAvg, 2 clients, wide_resnet16_8 C10,
     modules in HOST memory — through the drop-in server_aggregate (pinned
@@ -702,6 +746,12 @@ def main():
         t_step = e1[e1_best]
         extra["e1_implementations_ms"] = {k: round(v * 1e3, 4) for k, v in e1.items()}
         extra["e1_selected"] = e1_best
+        if not args.kernel_only:
+            try:
+                extra["cfg5_feddct_c100_n24_sharded"] = cfg5_sharded(dev, world, rank, group,
+                                                                      max(10, args.steps // 2))
+            except Exception as e:  # noqa: BLE001
+                extra["cfg5_feddct_c100_n24_sharded"] = {"error": repr(e)}
         # the exact (column-striped) mode on the same client placement
         striped = striped_host = None
         if not args.kernel_only and not args.no_exact:
