@@ -19,10 +19,20 @@ from __future__ import annotations
 
 from typing import Dict, List, Tuple
 
+from array import array
+
 import torch
 from torch.autograd.graph import increment_version
 
 from .layout import KIND_I64, KIND_PACKF, BucketLayout
+
+# The per-call checks and version bumps in C (csrc/shim.cpp, built by
+# build.py); the Python loops below define the same semantics and run when
+# the helper is absent (tests compare the two).
+try:
+    from . import _fa_shim
+except ImportError:  # not built
+    _fa_shim = None
 
 
 # Structure generation: bumped by torch's global registration hooks whenever
@@ -115,24 +125,35 @@ class ModuleArena:
         self.module_ref = module
         # tensors the kernel writes behind autograd's back (raw pointers)
         self._written = tuple(t for _, _, t, _ in self._checks)
+        self._v_dicts = tuple(d for d, _, _, _ in self._checks)
+        self._v_names = tuple(n for _, n, _, _ in self._checks)
+        self._v_ptrs = array("Q", [p for _, _, _, p in self._checks]).tobytes()
 
     def mark_written(self) -> None:
         """Bump the autograd version counter of every bucket-backed tensor,
         as the reference's ``load_state_dict`` (an in-place ``copy_``) does:
         a graph that saved the old values then fails loudly in backward
-        instead of using the overwritten ones.  One C++ call per arena."""
-        increment_version(self._written)
+        instead of using the overwritten ones."""
+        if _fa_shim is not None:
+            _fa_shim.bump_versions(self._written)
+        else:
+            increment_version(self._written)
 
-    def valid(self) -> bool:
+    def valid(self, use_shim: bool = True) -> bool:
         if self._gen != _STRUCT_GEN[0]:
             # something somewhere registered a tensor/module: is it ours?
             m = self.module_ref
             if list(state_owners(m).keys()) != self._keyset:
                 return False
             self._gen = _STRUCT_GEN[0]
-        for d, name, t, ptr in self._checks:
-            if d.get(name) is not t or t.data_ptr() != ptr:
+        if use_shim and _fa_shim is not None:
+            if not _fa_shim.valid_views(self._v_dicts, self._v_names, self._written,
+                                        self._v_ptrs):
                 return False
+        else:
+            for d, name, t, ptr in self._checks:
+                if d.get(name) is not t or t.data_ptr() != ptr:
+                    return False
         for d, name, t, _ in self._packed:
             if d.get(name) is not t:
                 return False
@@ -147,6 +168,8 @@ class ModuleArena:
     def unpack(self) -> None:
         """``copy_`` the f32 slot back into the key's own dtype (the
         load_state_dict semantics of train_fedavg.py:147)."""
+        if not self._packed:
+            return
         with torch.no_grad():
             for _, _, t, s in self._packed:
                 t.copy_(self.f32[s.offset:s.offset + s.numel].view(s.shape))

@@ -29,6 +29,36 @@ COMM_DEPS = [COMM_SRC, os.path.join(HERE, "csrc", "common.h"),
 COMM_OUT = os.path.join(HERE, "libfedagg_comm.so")
 
 
+# The drop-in's per-call host bookkeeping (arena checks, autograd version
+# bumps) as a small CPython extension against the running torch (g++; host
+# code only).
+SHIM_SRC = os.path.join(HERE, "csrc", "shim.cpp")
+
+
+def shim_path() -> str:
+    import sysconfig
+    return os.path.join(HERE, "_fa_shim" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_shim(force: bool = False) -> str:
+    import sysconfig
+
+    import torch
+    from torch.utils.cpp_extension import include_paths
+    out = shim_path()
+    if not force and not _stale(out, [SHIM_SRC]):
+        return out
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall",
+           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", *("-I" + p for p in include_paths()),
+           "-I" + sysconfig.get_paths()["include"], SHIM_SRC, "-o", out + ".tmp",
+           "-L" + tlib, "-ltorch_python", "-lc10", "-ltorch_cpu", "-Wl,-rpath," + tlib]
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def _stale(out, deps):
     return not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(d)
                                                                    for d in deps)
@@ -44,6 +74,7 @@ def build(force: bool = False, extra=()) -> str:
                "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,$ORIGIN"]
         subprocess.run(cmd, check=True)
         os.replace(COMM_OUT + ".tmp", COMM_OUT)
+    build_shim(force)
     return OUT
 
 

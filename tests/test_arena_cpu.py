@@ -137,3 +137,27 @@ def test_kernel_writes_bump_autograd_versions():
         y.backward()
     # a graph built after the write is fine
     (w * w).sum().backward()
+
+
+def test_c_helper_matches_python_checks():
+    """csrc/shim.cpp (valid_views / bump_versions) against the Python loops
+    that define them, on intact and tampered modules."""
+    from feddct_amd import arena as A
+    if A._fa_shim is None:
+        pytest.skip("_fa_shim not built")
+    m = net()
+    a = ModuleArena(m, BucketLayout.from_state_dict(m.state_dict()))
+    assert a.valid(use_shim=True) and a.valid(use_shim=False)
+    w = m[0].weight
+    old = w.data
+    w.data = torch.zeros_like(old)  # a .data swap (what model.to() does)
+    assert not a.valid(use_shim=True) and not a.valid(use_shim=False)
+    w.data = old
+    assert a.valid(use_shim=True)
+    m[1]._parameters["bias"] = torch.nn.Parameter(m[1].bias.detach().clone())  # replaced
+    assert not a.valid(use_shim=True) and not a.valid(use_shim=False)
+    v = [t._version for t in a._written]
+    A._fa_shim.bump_versions(a._written)
+    assert all(t._version > x for t, x in zip(a._written, v))
+    with pytest.raises(TypeError):
+        A._fa_shim.bump_versions((1,))
