@@ -27,6 +27,7 @@ are bound to pinned host buckets and staged through device buckets
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -127,20 +128,36 @@ class Engine:
             raise ValueError(f"{w.shape[0]} weights for {n} clients")
         return (ctypes.c_float * n)(*[float(x) for x in w])
 
-    def _launch(self, plan, layout, c32, c64, n, weights, out32, out64, flags, device):
-        a32 = _lib.ptr_array(c32)
-        a64 = _lib.ptr_array(c64)
+    def _launch(self, plan, a32, a64, n, weights, out32, out64, flags, device):
         stream = torch.cuda.current_stream(device).cuda_stream
+        if torch.cuda.current_device() == device.index:
+            _lib.check(_lib.lib.fa_reduce(plan.handle, a32, a64, n, weights, out32, out64,
+                                          flags, ctypes.c_void_p(stream)), "fa_reduce")
+            return
         with torch.cuda.device(device):
             _lib.check(_lib.lib.fa_reduce(plan.handle, a32, a64, n, weights, out32, out64,
                                           flags, ctypes.c_void_p(stream)), "fa_reduce")
+
+    def _ptr_arrays(self, cas: List[ModuleArena]):
+        """Client bucket pointer arrays, kept for the last client list (the
+        round loop passes the same slots every round; arenas never move)."""
+        key = tuple(map(id, cas))
+        hit = getattr(self, "_last_ptrs", None)
+        # weak references: the cache must not keep a dropped round's buckets alive
+        if hit is not None and hit[0] == key and all(r() is c for r, c in zip(hit[1], cas)):
+            return hit[2], hit[3]
+        a32 = _lib.ptr_array([c.ptr32 for c in cas])
+        a64 = _lib.ptr_array([c.ptr64 for c in cas])
+        self._last_ptrs = (key, tuple(weakref.ref(c) for c in cas), a32, a64)
+        return a32, a64
 
     def _reduce_device(self, layout, ga: ModuleArena, cas: List[ModuleArena], weights, fuse):
         n = len(cas)
         plan = self.plan(layout, ga.device)
         flags = _lib.FA_F_BCAST if fuse else 0
-        self._launch(plan, layout, [c.ptr32 for c in cas], [c.ptr64 for c in cas], n,
-                     self._weights_arg(weights, n), ga.ptr32, ga.ptr64, flags, ga.device)
+        a32, a64 = self._ptr_arrays(cas)
+        self._launch(plan, a32, a64, n, self._weights_arg(weights, n), ga.ptr32, ga.ptr64,
+                     flags, ga.device)
 
     def _reduce_host(self, layout, ga: ModuleArena, cas: List[ModuleArena], weights, fuse):
         """Host-resident state (the reference's CPU configuration): the
