@@ -139,6 +139,12 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
     # cfg1_host_resident_n2 drop-in timing)
     g2 = Holder()
     t_cfg1, reps_cfg1 = time_call(lambda: reference_loop(g2, mods[:2]), 5, budget_s * 0.1)
+    # BASELINE config 3's FedDCT round (train_feddct.py:34-56): the loop on
+    # the main-client models, then on the proxies, 5 slots
+    fd = _feddct_modules(torch.device("cuda", torch.cuda.current_device()), cpu=True)
+    t_fd, reps_fd = time_call(lambda: [reference_loop(g_, ms_) for _, _, g_, ms_ in fd], 3,
+                              budget_s * 0.2)
+    del fd
     # the same on one thread (SURVEY.md §8 d asks for both)
     torch.set_num_threads(1)
     t_loop1, reps1 = time_call(lambda: reference_loop(g, mods), 3, budget_s * 0.3)
@@ -156,6 +162,7 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
             "one_thread": {"loop_ms": round(t_loop1 * 1e3, 2), "core_ms": round(t_core1 * 1e3, 2),
                            "loop_GBps": round(nbytes / t_loop1 / 1e9, 3), "runs": reps1},
             "cfg1_n2": {"loop_ms": round(t_cfg1 * 1e3, 2), "runs": reps_cfg1},
+            "cfg3_feddct_n5": {"loop_ms": round(t_fd * 1e3, 2), "runs": reps_fd},
             "host_cpus": os.cpu_count(), "cpu": _cpu_model()}
 
 
@@ -590,6 +597,59 @@ def dropin_timing(layout, clients, dev, reps=20):
             "note": "median wall incl. Python shim, arena checks, fused reduce+broadcast, sync"}
 
 
+def _feddct_modules(dev, n=5, cpu=False):
+    """BASELINE config 3's slots as nn.Modules: n main-client + n proxy
+    modules (wrnsl16_8 sf4 C10 state_dicts) holding the synthetic states,
+    plus the two global models."""
+    names = ("wrnsl16_8_sf4_c10_main", "wrnsl16_8_sf4_c10_proxy")
+    out = []
+    for nm in names:
+        man = load_manifest(nm)
+        lay = BucketLayout.from_manifest(man)
+        Holder = _holder_class(lay)
+        mods = []
+        for f32, i64 in make_clients(lay, man, range(n), dev):
+            m = Holder() if cpu else Holder().to(dev)
+            sd = m.state_dict()
+            with torch.no_grad():
+                for sl in lay.slots:
+                    src = i64 if sl.kind == "i64" else f32
+                    sd[sl.key].copy_(src[sl.offset:sl.offset + sl.numel].view(sl.shape))
+            mods.append(m)
+        out.append((nm, lay, Holder() if cpu else Holder().to(dev), mods))
+    return out
+
+
+def dropin_feddct_timing(dev, reps=20):
+    """The FedDCT drop-in ``server_aggregate(g_main, g_proxy, mains, proxies)``
+    (train_feddct.py:34-56) on BASELINE config 3's shape, end to end: the
+    result is checked against the reference's digests, then timed."""
+    from feddct_amd.feddct import server_aggregate
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        dig = json.load(f)
+    (nm_m, lay_m, g_m, mains), (nm_p, lay_p, g_p, proxies) = _feddct_modules(dev)
+    server_aggregate(g_m, g_p, mains, proxies)
+    torch.cuda.synchronize()
+    import hashlib
+    ok = True
+    for nm, g in ((nm_m, g_m), (nm_p, g_p)):
+        h = hashlib.sha256()
+        for k, v in g.state_dict().items():
+            h.update(k.encode())
+            h.update(v.detach().cpu().numpy().tobytes())
+        ok &= h.hexdigest() == dig[f"feddct/{nm}/n5"]
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        server_aggregate(g_m, g_p, mains, proxies)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return {"server_aggregate_ms": round(ts[len(ts) // 2] * 1e3, 3),
+            "bit_exact_vs_reference_digest": bool(ok),
+            "note": "cfg3 shape: 5 slots x (main + proxy), median wall incl. sync"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -668,6 +728,10 @@ def main():
             tb, _ = timed_launches(fused, max(10, args.steps // 2), 3)
             extra["round_with_fused_broadcast_us"] = round(tb * 1e6, 1)
             extra["dropin"] = dropin_timing(layout, clients, dev)
+            try:
+                extra["dropin_feddct_cfg3"] = dropin_feddct_timing(dev)
+            except Exception as e:  # noqa: BLE001
+                extra["dropin_feddct_cfg3"] = {"error": repr(e)}
             extra["other_configs"] = other_configs(dev)
             try:
                 extra["next_rows"] = next_rows(dev)
