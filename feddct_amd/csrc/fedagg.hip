@@ -770,7 +770,12 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
         case 16: return launch_u<1, 16>(a, ntiles, deep, w, nt, st);
         default: return launch_u<1, 8>(a, ntiles, deep, w, nt, st);
       }
-    case 4: return launch_u<4, 8>(a, ntiles, deep, w, nt, st);
+    case 4:
+      switch (b_env) {
+        case 1: return launch_u<4, 1>(a, ntiles, deep, w, nt, st);
+        case 4: return launch_u<4, 4>(a, ntiles, deep, w, nt, st);
+        default: return launch_u<4, 8>(a, ntiles, deep, w, nt, st);
+      }
     default:
       switch (b_env) {
         case 1: return launch_u<2, 1>(a, ntiles, deep, w, nt, st);
