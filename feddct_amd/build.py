@@ -75,7 +75,25 @@ def build(force: bool = False, extra=()) -> str:
         subprocess.run(cmd, check=True)
         os.replace(COMM_OUT + ".tmp", COMM_OUT)
     build_shim(force)
+    build_example(force)
     return OUT
+
+
+# A native consumer of the C ABI (examples/c_abi_round.cpp): no Python, no
+# torch; run by tests/test_gpu_cabi.py.
+EXAMPLE_SRC = os.path.join(HERE, "..", "examples", "c_abi_round.cpp")
+EXAMPLE_OUT = os.path.join(HERE, "..", "examples", "c_abi_round")
+
+
+def build_example(force: bool = False) -> str:
+    if force or _stale(EXAMPLE_OUT, [EXAMPLE_SRC, OUT, os.path.join(HERE, "..", "include",
+                                                                     "fedagg.h")]):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-O2", "-std=c++17",
+               "-I" + os.path.join(HERE, "..", "include"), "-o", EXAMPLE_OUT + ".tmp",
+               EXAMPLE_SRC, "-L" + HERE, "-lfedagg", "-Wl,-rpath,$ORIGIN/../feddct_amd"]
+        subprocess.run(cmd, check=True)
+        os.replace(EXAMPLE_OUT + ".tmp", EXAMPLE_OUT)
+    return EXAMPLE_OUT
 
 
 if __name__ == "__main__":
