@@ -786,6 +786,7 @@ def main():
                 dist.all_reduce(tn, op=dist.ReduceOp.MAX)
                 nat[nch] = float(tn.item())
                 del nagg
+            ncomm.close()  # before torch's own teardown; nothing native runs after this
             best = min(nat, key=nat.get)
             extra["native_mode"] = {
                 "mode": "C ABI fa_reduce_sharded: client shards + chunked ncclReduce to rank 0",
