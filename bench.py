@@ -289,7 +289,7 @@ def other_configs(dev, steps=20):
     return res
 
 
-def cfg5_sharded(dev, world, rank, group, steps):
+def cfg5_sharded(dev, world, rank, group, steps, ncomm=None):
     """BASELINE config 5 on the N GPUs of this run: FedDCT sf4 C100, 24 slots
     (main + proxy in one joint bucket), slots sharded contiguously over the
     ranks (3 per GPU at N=8), global state to rank 0.  e1 (client shards +
@@ -320,14 +320,26 @@ def cfg5_sharded(dev, world, rank, group, steps):
     t1 = tmax(agg.step, steps, 5)
     s32, s64 = torch.zeros_like(o32), torch.zeros_like(o64)
     sagg = StripedAggregator(lay, n, s32, s64, group=group, final="reduce")
-    t2 = tmax(lambda: sagg.step_device(l32, l64), max(3, steps // 10), 2)
+    t2 = tmax(lambda: sagg.step_device(l32, l64), max(2, steps // 10), 1)
     out = {"slots": n, "slots_per_gpu": hi - lo, "algorithmic_bytes": nbytes,
            "e1_ms": round(t1 * 1e3, 4), "e1_GBps": round(nbytes / t1 / 1e9, 2),
            "e2_exact_ms": round(t2 * 1e3, 4), "e2_exact_GBps": round(nbytes / t2 / 1e9, 2)}
+    x32 = x64 = None
+    if ncomm is not None:  # the exact mode through the C ABI
+        from feddct_amd.comm import NativeStripedAggregator
+        x32, x64 = torch.zeros_like(o32), torch.zeros_like(o64)
+        xagg = NativeStripedAggregator(lay, l32, l64, n, x32, x64, ncomm, final="reduce")
+        t3 = tmax(xagg.step, max(2, steps // 4), 1)
+        out["e2_native_ms"] = round(t3 * 1e3, 4)
+        out["e2_native_GBps"] = round(nbytes / t3 / 1e9, 2)
     if rank == 0:
         ok = all(digest_of(lay, s32, s64, pf) == dig[f"feddct/{nm}/n24"]
                  for nm, pf in zip(names, prefixes))
         out["e2_bit_exact_vs_reference_digest"] = bool(ok)
+        if x32 is not None:
+            out["e2_native_bit_exact_vs_reference_digest"] = bool(all(
+                digest_of(lay, x32, x64, pf) == dig[f"feddct/{nm}/n24"]
+                for nm, pf in zip(names, prefixes)))
         out["e1_max_abs_err_vs_exact"] = float((o32 - s32).abs().max())
         out["e1_int64_bit_exact"] = bool(torch.equal(o64, s64))
     return out
@@ -378,7 +390,7 @@ def cfg1_host_resident(dev, reps=5):
 
 
 def exact_modes(layout, manifest, clients, out32, out64, world, group, dev, nbytes_rank,
-                steps):
+                steps, ncomm=None):
     """N>1: the exact column-striped mode (feddct_amd/dist.py),
     with device-resident client shards and with host ingress."""
     from feddct_amd.dist import StripedAggregator
@@ -398,6 +410,16 @@ def exact_modes(layout, manifest, clients, out32, out64, world, group, dev, nbyt
     striped = {"mode": "column-striped exact (grouped P2P stripe exchange over RCCL)",
                "ms_per_step": round(ts * 1e3, 3),
                "GBps": round(nbytes_rank * world / ts / 1e9, 2)}
+    x32 = x64 = None
+    if ncomm is not None:  # the same exact round through the C ABI (fa_reduce_striped)
+        from feddct_amd.comm import NativeStripedAggregator
+        x32, x64 = torch.zeros_like(out32), torch.zeros_like(out64)
+        xagg = NativeStripedAggregator(layout, lc32, lc64, n_total, x32, x64, ncomm,
+                                       final="reduce")
+        tx = timed_max(xagg.step, steps, 2)
+        striped["native"] = {"ms_per_step": round(tx * 1e3, 3),
+                             "GBps": round(nbytes_rank * world / tx / 1e9, 2)}
+        del xagg
     # host ingress (the north_star's CPU-tensor clients): each GPU uploads only
     # ITS column stripe of every client over its own PCIe link, reduces it
     # exactly, the stripes meet on the root
@@ -415,7 +437,7 @@ def exact_modes(layout, manifest, clients, out32, out64, world, group, dev, nbyt
                     "ms_per_step": round(th * 1e3, 3),
                     "GBps": round(nbytes_rank * world / th / 1e9, 2),
                     "H2D_bytes_per_gpu": int((hi - lo) * 4 * n_total)}
-    return striped, striped_host, (s32, s64, h32, h64)
+    return striped, striped_host, (s32, s64, h32, h64, x32, x64)
 
 
 def _holder_class(layout):
@@ -743,6 +765,7 @@ def main():
                 extra["cfg1_host_resident_n2"] = {"error": repr(e)}
     else:
         from feddct_amd.dist import ShardedAggregator
+        log(f"[rank {rank}] e1 torch.distributed")
         agg = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
                                 N_CLIENTS * world, out32, out64, nchunks=args.chunks,
                                 final="reduce")
@@ -770,7 +793,9 @@ def main():
         # several chunk counts; every variant is a complete round with the
         # global state on rank 0, timed like the headline (K steps, max over
         # ranks), and the headline takes the fastest implementation
+        log(f"[rank {rank}] e1 native")
         n32 = n64 = None
+        ncomm = None
         e1 = {f"torch.distributed/{args.chunks}chunks": None}
         try:
             from feddct_amd.comm import Comm, NativeShardedAggregator
@@ -786,7 +811,6 @@ def main():
                 dist.all_reduce(tn, op=dist.ReduceOp.MAX)
                 nat[nch] = float(tn.item())
                 del nagg
-            ncomm.close()  # before torch's own teardown; nothing native runs after this
             best = min(nat, key=nat.get)
             extra["native_mode"] = {
                 "mode": "C ABI fa_reduce_sharded: client shards + chunked ncclReduce to rank 0",
@@ -812,18 +836,21 @@ def main():
         extra["e1_implementations_ms"] = {k: round(v * 1e3, 4) for k, v in e1.items()}
         extra["e1_selected"] = e1_best
         if not args.kernel_only:
+            log(f"[rank {rank}] config 5 sharded")
             try:
                 extra["cfg5_feddct_c100_n24_sharded"] = cfg5_sharded(dev, world, rank, group,
-                                                                      max(10, args.steps // 2))
+                                                                      max(10, args.steps // 2),
+                                                                      ncomm)
             except Exception as e:  # noqa: BLE001
                 extra["cfg5_feddct_c100_n24_sharded"] = {"error": repr(e)}
         # the exact (column-striped) mode on the same client placement
         striped = striped_host = None
         if not args.kernel_only and not args.no_exact:
+            log(f"[rank {rank}] exact modes")
             try:
-                striped, striped_host, (s32, s64, h32, h64) = exact_modes(
+                striped, striped_host, (s32, s64, h32, h64, x32, x64) = exact_modes(
                     layout, manifest, clients, out32, out64, world, group, dev, nbytes_rank,
-                    max(3, min(5, args.steps // 10)))
+                    max(3, min(5, args.steps // 10)), ncomm)
             except Exception as e:  # noqa: BLE001
                 extra["exact_mode"] = {"error": repr(e)}
         if rank == 0 and not args.kernel_only:
@@ -843,6 +870,9 @@ def main():
                 extra["native_mode"]["int64_bit_exact"] = bool(torch.equal(n64, ex64))
             if striped is not None:
                 striped["bit_exact"] = bool(torch.equal(s32, ex32) and torch.equal(s64, ex64))
+                if x32 is not None:
+                    striped["native"]["bit_exact"] = bool(torch.equal(x32, ex32)
+                                                          and torch.equal(x64, ex64))
                 extra["exact_mode"] = striped
             if striped_host is not None:
                 striped_host["bit_exact"] = bool(torch.equal(h32, ex32) and torch.equal(h64, ex64))
@@ -885,6 +915,8 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        if ncomm is not None:
+            ncomm.close()  # the library's communicator before torch's teardown
         dist.barrier()
         dist.destroy_process_group()
 

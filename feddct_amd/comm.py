@@ -30,7 +30,8 @@ FA_COMM_UID_BYTES = 128
 
 COMM_EXPORTS = ["fa_comm_unique_id", "fa_comm_init_rank", "fa_comm_init", "fa_comm_destroy",
                 "fa_comm_info", "fa_shard_plan_create", "fa_shard_plan_destroy",
-                "fa_reduce_sharded"]
+                "fa_reduce_sharded", "fa_stripe_plan_create", "fa_stripe_plan_destroy",
+                "fa_reduce_striped"]
 
 _P, _I, _I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
 
@@ -55,6 +56,10 @@ def _load():
                                  ctypes.c_uint, ctypes.POINTER(_P)],
         "fa_shard_plan_destroy": [_P],
         "fa_reduce_sharded": [ctypes.POINTER(_P), _I, ctypes.POINTER(FaShardIO), _I],
+        "fa_stripe_plan_create": [_P, _P, _I, _I64, _P, _I, _I64, ctypes.POINTER(_I),
+                                  ctypes.c_uint, ctypes.POINTER(_P)],
+        "fa_stripe_plan_destroy": [_P],
+        "fa_reduce_striped": [ctypes.POINTER(_P), _I, ctypes.POINTER(FaShardIO), _I],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -196,3 +201,66 @@ class NativeShardedAggregator:
         self.io.stream = s
         _lib.check(lib().fa_reduce_sharded(self._plans, 1, ctypes.byref(self.io), self.root),
                    "fa_reduce_sharded")
+
+
+class StripePlan:
+    """This rank's exact-mode plan for a layout (its stripe's tiles, the
+    receive rows, int64 gather buffers)."""
+
+    def __init__(self, comm: Comm, layout: BucketLayout, counts: Sequence[int]):
+        a32, n32 = _lib.seg_array(layout.segs32 if len(layout.segs32)
+                                  else np.zeros((0, 2), np.int64))
+        a64, n64 = _lib.seg_array(layout.segs64 if len(layout.segs64)
+                                  else np.zeros((0, 2), np.int64))
+        c = (_I * len(counts))(*map(int, counts))
+        h = _P()
+        _lib.check(lib().fa_stripe_plan_create(comm.handle, a32, n32, int(layout.f32_numel), a64,
+                                               n64, int(layout.i64_numel), c,
+                                               _lib.FA_PLAN_GAPS_ARE_PADDING, ctypes.byref(h)),
+                   "fa_stripe_plan_create")
+        self.handle = h
+        self.comm = comm
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                lib().fa_stripe_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+class NativeStripedAggregator(NativeShardedAggregator):
+    """The exact cross-GPU round (dist.StripedAggregator's device-ingress
+    form) through the C ABI: ``step()`` is ONE fa_reduce_striped call; the
+    result is bit-identical to one GPU reducing all clients."""
+
+    def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
+                 local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
+                 out64: torch.Tensor, comm: Comm, final: str = "reduce", root: int = 0):
+        if final not in ("reduce", "allreduce"):
+            raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
+        world, rank, _ = comm.info()
+        counts = [b - a for a, b in (shard_range(n_total, world, r) for r in range(world))]
+        if len(local32) != counts[rank]:
+            raise ValueError(f"rank {rank} holds {len(local32)} clients, shard is {counts[rank]}")
+        self.plan = StripePlan(comm, layout, counts)
+        self.root = root if final == "reduce" else -1
+        self._a32 = _lib.ptr_array([t.data_ptr() for t in local32])
+        self._a64 = _lib.ptr_array([t.data_ptr() for t in local64])
+        self._w = None
+        self._plans = (_P * 1)(self.plan.handle.value)
+        self.io = FaShardIO()
+        self.io.c32 = ctypes.cast(self._a32, _P)
+        self.io.c64 = ctypes.cast(self._a64, _P) if layout.i64_numel else None
+        self.io.weights = None
+        self.io.out32 = out32.data_ptr()
+        self.io.out64 = out64.data_ptr() if layout.i64_numel else None
+        self._keep = (local32, local64, out32, out64)
+
+    def step(self, stream=None) -> None:
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self.io.stream = s
+        _lib.check(lib().fa_reduce_striped(self._plans, 1, ctypes.byref(self.io), self.root),
+                   "fa_reduce_striped")

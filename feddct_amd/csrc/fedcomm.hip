@@ -1,13 +1,18 @@
-// fedcomm.hip — libfedagg_comm.so: client-sharded aggregation across the GPUs
-// of one node over RCCL (include/fedagg_comm.h; SURVEY.md §8 b, e1).
+// fedcomm.hip — libfedagg_comm.so: aggregation across the GPUs of one node
+// over RCCL (include/fedagg_comm.h; SURVEY.md §8 b, e1, e2).
 //
 // Layering: this library uses only libfedagg.so's public ABI for the
 // arithmetic (fa_plan_build_host to enumerate the layout's tiles,
-// fa_plan_create_from_tiles for the per-chunk tile subsets, fa_reduce with
-// FA_F_SUM_ONLY for the per-rank partial sums, fa_div_f32 for the /N finish)
-// and adds the exchange: one ncclReduce / ncclAllReduce per column chunk on an
-// internal communication stream, issued as soon as the kernel over that chunk
-// is done, so the exchange of chunk c overlaps the reduction of chunk c+1.
+// fa_plan_create_from_tiles for tile subsets, fa_reduce for the reductions,
+// fa_div_f32 for the /N finish) and adds the exchanges:
+//   e1 (fa_reduce_sharded): one ncclReduce / ncclAllReduce per column chunk
+//      on an internal communication stream, issued as soon as the kernel
+//      over that chunk is done, so the exchange of chunk c overlaps the
+//      reduction of chunk c+1;
+//   e2 (fa_reduce_striped): grouped ncclSend/ncclRecv move every client's
+//      values for rank r's column stripe to rank r, which reduces its stripe
+//      over all clients in the exact order; the stripes then travel to the
+//      root (or to every rank).  Bit-identical to one GPU.
 // RCCL resolves to the librccl.so.1 torch has already loaded (same soname),
 // so a process holds one RCCL.
 
@@ -17,6 +22,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "../../include/fedagg_comm.h"
@@ -39,23 +45,12 @@ struct fa_comm {
   hipStream_t cs = nullptr;  // communication stream
 };
 
-struct fa_shard_plan {
-  fa_comm* comm = nullptr;
-  int64_t f32_numel = 0, i64_numel = 0;
-  int n_local = 0, n_total = 0, nmax = 0, lo_slot = 0;
-  std::vector<fa_plan*> chunk;               // tile subset per column chunk
-  std::vector<std::pair<int64_t, int64_t>> range;  // [lo, hi) of each chunk
-  fa_plan* plan64 = nullptr;                 // the int64 tiles
-  float* partial = nullptr;                  // f32_numel (library scratch)
-  int64_t* stack64 = nullptr;                // nmax rows of i64_numel
-  int64_t* gather64 = nullptr;               // nranks * nmax rows
-  std::vector<const int64_t*> rows64;        // n_total real rows, slot order
-  std::vector<hipEvent_t> ev;                // per chunk (+ int64, + done)
-};
-
 namespace {
 
-// Stack the rank's int64 buckets into contiguous rows for the all-gather.
+// ------------------------------------------------------------ int64 keys --
+// The int64 keys (num_batches_tracked) are a few bytes per client: every
+// rank's buckets are stacked into rows, all-gathered raw, and the result
+// ranks reduce all n_total rows exactly (slot order = rank order).
 constexpr int kStackPtrs = 64;
 struct StackArgs {
   const int64_t* src[kStackPtrs];
@@ -69,6 +64,99 @@ __global__ void stack_i64_kernel(StackArgs a) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < a.width;
        e += (int64_t)gridDim.x * blockDim.x)
     a.dst[r * a.width + e] = a.src[r][e];
+}
+
+struct I64Part {
+  fa_plan* plan = nullptr;  // the int64 tiles (nullptr: no int64 keys)
+  int64_t* stack = nullptr;   // nmax rows of width
+  int64_t* gather = nullptr;  // nranks * nmax rows
+  std::vector<const int64_t*> rows;  // the n_total real rows, slot order
+  int nmax = 0;
+  int64_t width = 0;
+
+  int init(const fa_comm* c, const std::vector<fa_tile_desc>& t64, const int* counts,
+           int64_t f32_numel, int64_t i64_numel, unsigned flags) {
+    if (t64.empty()) return FA_OK;
+    int rc = fa_plan_create_from_tiles(t64.data(), (int)t64.size(), f32_numel, i64_numel, 0,
+                                       flags, &plan);
+    if (rc) return rc;
+    width = i64_numel;
+    for (int r = 0; r < c->nranks; ++r) nmax = std::max(nmax, counts[r]);
+    const size_t row = (size_t)width * 8;
+    FA_HIP_TRY(hipMalloc(&stack, std::max<size_t>(1, (size_t)nmax * row)));
+    FA_HIP_TRY(hipMalloc(&gather, std::max<size_t>(1, (size_t)nmax * c->nranks * row)));
+    for (int r = 0; r < c->nranks; ++r)
+      for (int j = 0; j < counts[r]; ++j)
+        rows.push_back(gather + ((size_t)r * nmax + j) * width);
+    return FA_OK;
+  }
+  void release() {
+    fa_plan_destroy(plan);
+    if (stack) (void)hipFree(stack);
+    if (gather) (void)hipFree(gather);
+    plan = nullptr;
+    stack = gather = nullptr;
+  }
+  // stack this rank's n_local buckets on stream s
+  int stack_local(const int64_t* const* c64, int n_local, hipStream_t s) {
+    for (int j0 = 0; j0 < n_local; j0 += kStackPtrs) {
+      StackArgs a;
+      memset(&a, 0, sizeof a);
+      a.rows = std::min(kStackPtrs, n_local - j0);
+      for (int j = 0; j < a.rows; ++j) a.src[j] = c64[j0 + j];
+      a.dst = stack + (size_t)j0 * width;
+      a.width = width;
+      const int gx = (int)std::min<int64_t>(64, (width + 255) / 256);
+      hipLaunchKernelGGL(stack_i64_kernel, dim3(gx, a.rows), dim3(256), 0, s, a);
+      FA_HIP_TRY(hipGetLastError());
+    }
+    return FA_OK;
+  }
+};
+
+// ------------------------------------------------------------ tile cuts --
+// The layout's fp32 tiles sorted by start, and its int64 tiles.
+int layout_tiles(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_seg* seg64,
+                 int nseg64, int64_t i64_numel, unsigned flags, std::vector<fa_tile_desc>* t32,
+                 std::vector<fa_tile_desc>* t64) {
+  fa_plan_info info{};
+  int rc = fa_plan_build_host(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, 0, flags,
+                              nullptr, 0, &info);
+  if (rc) return rc;
+  std::vector<fa_tile_desc> tiles(std::max(1, info.ntiles));
+  rc = fa_plan_build_host(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, 0, flags,
+                          tiles.data(), info.ntiles, &info);
+  if (rc) return rc;
+  tiles.resize(info.ntiles);
+  for (const fa_tile_desc& t : tiles) (t.kind >= 4 ? t64 : t32)->push_back(t);
+  std::sort(t32->begin(), t32->end(),
+            [](const fa_tile_desc& a, const fa_tile_desc& b) { return a.start < b.start; });
+  return FA_OK;
+}
+
+// k contiguous groups of the sorted fp32 tiles with equal shares of the
+// elements, cut only before a vector tile on a 256-B boundary (so every
+// group's byte range starts aligned); exactly k groups, trailing ones may be
+// empty.  Group g = tiles [cut[g], cut[g+1]), byte range [lo[g], lo[g+1])
+// with lo[0] = 0 and lo[k] = f32_numel (the padding between tensors is
+// covered, FA_PLAN_GAPS_ARE_PADDING).
+void cut_tiles(const std::vector<fa_tile_desc>& t32, int k, int64_t f32_numel,
+               std::vector<size_t>* cut, std::vector<int64_t>* lo) {
+  int64_t total = 0;
+  for (const fa_tile_desc& t : t32) total += t.count;
+  cut->assign(1, 0);
+  int64_t acc = 0;
+  for (size_t i = 0; i < t32.size(); ++i) {
+    const int c = (int)cut->size();
+    if (c < k && i > 0 && acc >= total * c / k && t32[i].kind == 0 && t32[i].start % 64 == 0)
+      cut->push_back(i);
+    acc += t32[i].count;
+  }
+  while ((int)cut->size() < k + 1) cut->push_back(t32.size());
+  lo->assign(k + 1, f32_numel);
+  (*lo)[0] = 0;
+  for (int g = 1; g < k; ++g)
+    (*lo)[g] = (*cut)[g] < t32.size() ? t32[(*cut)[g]].start : f32_numel;
 }
 
 struct DeviceGuard {
@@ -99,19 +187,97 @@ int make_comm(ncclComm_t nc, int device, fa_comm** out) {
   return FA_OK;
 }
 
-void free_plan(fa_shard_plan* p) {
+int slot_layout(const fa_comm* comm, const int* counts, int* n_total, int* lo_slot,
+                const char* who) {
+  *n_total = 0;
+  *lo_slot = 0;
+  for (int r = 0; r < comm->nranks; ++r) {
+    if (counts[r] < 0) return set_err(FA_E_INVAL, "%s: counts[%d]=%d", who, r, counts[r]);
+    if (r < comm->rank) *lo_slot += counts[r];
+    *n_total += counts[r];
+  }
+  if (*n_total < 1 || *n_total > FA_MAX_CLIENTS)
+    return set_err(FA_E_RANGE, "%s: %d clients in total", who, *n_total);
+  return FA_OK;
+}
+
+int make_events(std::vector<hipEvent_t>* ev, size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    hipEvent_t e;
+    FA_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ev->push_back(e);
+  }
+  return FA_OK;
+}
+
+}  // namespace
+
+struct fa_shard_plan {
+  fa_comm* comm = nullptr;
+  int64_t f32_numel = 0, i64_numel = 0;
+  int n_local = 0, n_total = 0, lo_slot = 0;
+  std::vector<fa_plan*> chunk;                     // tile subset per column chunk
+  std::vector<std::pair<int64_t, int64_t>> range;  // [lo, hi) of each chunk
+  float* partial = nullptr;                        // f32_numel (library scratch)
+  I64Part i64;
+  std::vector<hipEvent_t> ev;  // per chunk (+ int64, + done)
+};
+
+struct fa_stripe_plan {
+  fa_comm* comm = nullptr;
+  int64_t f32_numel = 0, i64_numel = 0;
+  int n_local = 0, n_total = 0, lo_slot = 0;
+  std::vector<int> counts, first_slot;  // per rank
+  std::vector<int64_t> lo;              // nranks + 1 stripe bounds
+  fa_plan* stripe = nullptr;            // this rank's stripe tiles (nullptr: empty)
+  int64_t row = 0;                      // recv row stride (floats, 64-aligned)
+  float* recv = nullptr;                // n_total rows of the stripe
+  float* sbuf = nullptr;                // the reduced stripe
+  std::vector<const float*> ptrs;       // the n_total source pointers (see create)
+  I64Part i64;
+  std::vector<hipEvent_t> ev;  // start, int64, done
+};
+
+namespace {
+void free_shard(fa_shard_plan* p) {
   if (!p) return;
   DeviceGuard g;
   if (p->comm) (void)hipSetDevice(p->comm->device);
   for (fa_plan* c : p->chunk) fa_plan_destroy(c);
-  fa_plan_destroy(p->plan64);
   if (p->partial) (void)hipFree(p->partial);
-  if (p->stack64) (void)hipFree(p->stack64);
-  if (p->gather64) (void)hipFree(p->gather64);
+  p->i64.release();
+  for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+  delete p;
+}
+void free_stripe(fa_stripe_plan* p) {
+  if (!p) return;
+  DeviceGuard g;
+  if (p->comm) (void)hipSetDevice(p->comm->device);
+  fa_plan_destroy(p->stripe);
+  if (p->recv) (void)hipFree(p->recv);
+  if (p->sbuf) (void)hipFree(p->sbuf);
+  p->i64.release();
   for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
   delete p;
 }
 
+// int64 keys after the local buckets are stacked on stream s: all-gather
+// (grouped over the local GPUs by the caller) happens in run_i64_exchange.
+int i64_exchange(I64Part* const* parts, const fa_comm* const* comms, int nlocal) {
+  NCCL_TRY(ncclGroupStart());
+  for (int d = 0; d < nlocal; ++d) {
+    (void)hipSetDevice(comms[d]->device);
+    ncclResult_t r = ncclAllGather(parts[d]->stack, parts[d]->gather,
+                                   (size_t)parts[d]->nmax * parts[d]->width, ncclInt64,
+                                   comms[d]->nc, comms[d]->cs);
+    if (r != ncclSuccess) {
+      ncclGroupEnd();
+      return set_err(FA_E_COMM, "int64 all-gather: %s", ncclGetErrorString(r));
+    }
+  }
+  NCCL_TRY(ncclGroupEnd());
+  return FA_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -180,6 +346,7 @@ int fa_comm_info(const fa_comm* c, int* nranks, int* rank, int* device) {
   return FA_OK;
 }
 
+// ============================================================== e1 ========
 int fa_shard_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
                          const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
                          int nchunks, unsigned flags, fa_shard_plan** out) {
@@ -193,30 +360,14 @@ int fa_shard_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t
   if (nchunks == 0) nchunks = 8;
   if (nchunks < 1 || nchunks > FA_COMM_MAX_CHUNKS)
     return set_err(FA_E_INVAL, "fa_shard_plan_create: nchunks=%d", nchunks);
-  int n_total = 0, nmax = 0, lo_slot = 0;
-  for (int r = 0; r < comm->nranks; ++r) {
-    if (counts[r] < 0) return set_err(FA_E_INVAL, "counts[%d]=%d", r, counts[r]);
-    if (r < comm->rank) lo_slot += counts[r];
-    n_total += counts[r];
-    nmax = std::max(nmax, counts[r]);
-  }
-  if (n_total < 1 || n_total > FA_MAX_CLIENTS)
-    return set_err(FA_E_RANGE, "fa_shard_plan_create: %d clients in total", n_total);
+  int n_total = 0, lo_slot = 0;
+  int rc = slot_layout(comm, counts, &n_total, &lo_slot, "fa_shard_plan_create");
+  if (rc) return rc;
   DeviceGuard g;
   FA_HIP_TRY(hipSetDevice(comm->device));
-  fa_plan_info info{};
-  int rc = fa_plan_build_host(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, 0, flags,
-                              nullptr, 0, &info);
-  if (rc) return rc;
-  std::vector<fa_tile_desc> tiles(std::max(1, info.ntiles));
-  rc = fa_plan_build_host(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, 0, flags,
-                          tiles.data(), info.ntiles, &info);
-  if (rc) return rc;
-  tiles.resize(info.ntiles);
   std::vector<fa_tile_desc> t32, t64;
-  for (const fa_tile_desc& t : tiles) (t.kind >= 4 ? t64 : t32).push_back(t);
-  std::sort(t32.begin(), t32.end(),
-            [](const fa_tile_desc& a, const fa_tile_desc& b) { return a.start < b.start; });
+  rc = layout_tiles(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, flags, &t32, &t64);
+  if (rc) return rc;
 
   fa_shard_plan* p = new fa_shard_plan();
   p->comm = comm;
@@ -224,72 +375,44 @@ int fa_shard_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t
   p->i64_numel = i64_numel;
   p->n_local = counts[comm->rank];
   p->n_total = n_total;
-  p->nmax = nmax;
   p->lo_slot = lo_slot;
-  hipError_t e = hipSuccess;
-  // chunks: equal shares of the summed elements, cut only before a vector
-  // tile on a 256-B boundary so every exchange starts aligned
   if (!t32.empty()) {
-    int64_t total = 0;
-    for (const fa_tile_desc& t : t32) total += t.count;
-    std::vector<size_t> cuts{0};
-    int64_t acc = 0;
-    for (size_t i = 0; i < t32.size(); ++i) {
-      const int c = (int)cuts.size();
-      if (c < nchunks && i > 0 && acc >= total * c / nchunks && t32[i].kind == 0 &&
-          t32[i].start % 64 == 0)
-        cuts.push_back(i);
-      acc += t32[i].count;
-    }
-    cuts.push_back(t32.size());
-    for (size_t c = 0; c + 1 < cuts.size(); ++c) {
-      const int64_t lo = c == 0 ? 0 : t32[cuts[c]].start;
-      const int64_t hi = c + 2 == cuts.size() ? f32_numel : t32[cuts[c + 1]].start;
+    std::vector<size_t> cut;
+    std::vector<int64_t> lo;
+    cut_tiles(t32, nchunks, f32_numel, &cut, &lo);
+    for (int c = 0; c < nchunks; ++c) {
+      if (cut[c] == cut[c + 1]) continue;  // empty trailing group
       fa_plan* sub = nullptr;
-      rc = fa_plan_create_from_tiles(t32.data() + cuts[c], (int)(cuts[c + 1] - cuts[c]),
+      rc = fa_plan_create_from_tiles(t32.data() + cut[c], (int)(cut[c + 1] - cut[c]),
                                      f32_numel, i64_numel, 0, flags, &sub);
       if (rc) {
-        free_plan(p);
+        free_shard(p);
         return rc;
       }
       p->chunk.push_back(sub);
-      p->range.emplace_back(lo, hi);
+      // the last non-empty chunk's exchange runs to the end of the bucket
+      p->range.emplace_back(lo[c], lo[c + 1]);
     }
-    e = hipMalloc(&p->partial, (size_t)f32_numel * 4);
+    p->range.back().second = f32_numel;
+    hipError_t e = hipMalloc(&p->partial, (size_t)f32_numel * 4);
     if (e == hipSuccess) e = hipMemset(p->partial, 0, (size_t)f32_numel * 4);
-  }
-  if (e == hipSuccess && !t64.empty()) {
-    rc = fa_plan_create_from_tiles(t64.data(), (int)t64.size(), f32_numel, i64_numel, 0, flags,
-                                   &p->plan64);
-    if (rc) {
-      free_plan(p);
-      return rc;
-    }
-    const size_t row = (size_t)i64_numel * 8;
-    e = hipMalloc(&p->stack64, std::max<size_t>(1, (size_t)nmax * row));
-    if (e == hipSuccess)
-      e = hipMalloc(&p->gather64, std::max<size_t>(1, (size_t)nmax * comm->nranks * row));
-    if (e == hipSuccess) {
-      for (int r = 0; r < comm->nranks; ++r)
-        for (int j = 0; j < counts[r]; ++j)
-          p->rows64.push_back(p->gather64 + ((size_t)r * nmax + j) * i64_numel);
+    if (e != hipSuccess) {
+      free_shard(p);
+      return set_err(FA_E_HIP, "fa_shard_plan_create: %s", hipGetErrorString(e));
     }
   }
-  for (size_t i = 0; e == hipSuccess && i < p->chunk.size() + 2; ++i) {
-    hipEvent_t ev;
-    e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (e == hipSuccess) p->ev.push_back(ev);
-  }
-  if (e != hipSuccess) {
-    free_plan(p);
-    return set_err(FA_E_HIP, "fa_shard_plan_create: %s", hipGetErrorString(e));
+  rc = p->i64.init(comm, t64, counts, f32_numel, i64_numel, flags);
+  if (!rc) rc = make_events(&p->ev, p->chunk.size() + 2);
+  if (rc) {
+    free_shard(p);
+    return rc;
   }
   *out = p;
   return FA_OK;
 }
 
 int fa_shard_plan_destroy(fa_shard_plan* p) {
-  free_plan(p);
+  free_shard(p);
   return FA_OK;
 }
 
@@ -305,9 +428,9 @@ int fa_reduce_sharded(fa_shard_plan* const* plans, int nlocal, const fa_shard_io
     const bool result = root < 0 || root == p->comm->rank;
     if (p->n_local > 0 && !p->chunk.empty() && !io[d].c32)
       return set_err(FA_E_INVAL, "fa_reduce_sharded: fp32 buckets required (GPU %d)", d);
-    if (p->n_local > 0 && p->plan64 && !io[d].c64)
+    if (p->n_local > 0 && p->i64.plan && !io[d].c64)
       return set_err(FA_E_INVAL, "fa_reduce_sharded: int64 buckets required (GPU %d)", d);
-    if (result && ((!p->chunk.empty() && !io[d].out32) || (p->plan64 && !io[d].out64)))
+    if (result && ((!p->chunk.empty() && !io[d].out32) || (p->i64.plan && !io[d].out64)))
       return set_err(FA_E_INVAL, "fa_reduce_sharded: result buckets required on rank %d",
                      p->comm->rank);
     if (p->chunk.size() != plans[0]->chunk.size())
@@ -359,44 +482,28 @@ int fa_reduce_sharded(fa_shard_plan* const* plans, int nlocal, const fa_shard_io
       }
     }
   }
-  if (plans[0]->plan64) {
-    const size_t k64 = nch;  // event slot of the int64 stack
+  if (plans[0]->i64.plan) {
+    std::vector<I64Part*> parts;
+    std::vector<const fa_comm*> comms;
     for (int d = 0; d < nlocal; ++d) {
       fa_shard_plan* p = plans[d];
       hipStream_t s = (hipStream_t)io[d].stream;
       FA_HIP_TRY(hipSetDevice(p->comm->device));
-      for (int j0 = 0; j0 < p->n_local; j0 += kStackPtrs) {
-        StackArgs a;
-        memset(&a, 0, sizeof a);
-        a.rows = std::min(kStackPtrs, p->n_local - j0);
-        for (int j = 0; j < a.rows; ++j) a.src[j] = io[d].c64[j0 + j];
-        a.dst = p->stack64 + (size_t)j0 * p->i64_numel;
-        a.width = p->i64_numel;
-        const int gx = (int)std::min<int64_t>(64, (p->i64_numel + 255) / 256);
-        hipLaunchKernelGGL(stack_i64_kernel, dim3(gx, a.rows), dim3(256), 0, s, a);
-        FA_HIP_TRY(hipGetLastError());
-      }
-      FA_HIP_TRY(hipEventRecord(p->ev[k64], s));
-      FA_HIP_TRY(hipStreamWaitEvent(p->comm->cs, p->ev[k64], 0));
+      int rc = p->i64.stack_local(io[d].c64, p->n_local, s);
+      if (rc) return rc;
+      FA_HIP_TRY(hipEventRecord(p->ev[nch], s));
+      FA_HIP_TRY(hipStreamWaitEvent(p->comm->cs, p->ev[nch], 0));
+      parts.push_back(&p->i64);
+      comms.push_back(p->comm);
     }
-    NCCL_TRY(ncclGroupStart());
-    for (int d = 0; d < nlocal; ++d) {
-      fa_shard_plan* p = plans[d];
-      (void)hipSetDevice(p->comm->device);
-      ncclResult_t r = ncclAllGather(p->stack64, p->gather64, (size_t)p->nmax * p->i64_numel,
-                                     ncclInt64, p->comm->nc, p->comm->cs);
-      if (r != ncclSuccess) {
-        ncclGroupEnd();
-        return set_err(FA_E_COMM, "int64 all-gather: %s", ncclGetErrorString(r));
-      }
-    }
-    NCCL_TRY(ncclGroupEnd());
+    int rc = i64_exchange(parts.data(), comms.data(), nlocal);
+    if (rc) return rc;
     for (int d = 0; d < nlocal; ++d) {
       fa_shard_plan* p = plans[d];
       if (!(root < 0 || root == p->comm->rank)) continue;
       FA_HIP_TRY(hipSetDevice(p->comm->device));
-      const int rc = fa_reduce(p->plan64, nullptr, p->rows64.data(), p->n_total, nullptr,
-                               nullptr, io[d].out64, 0, p->comm->cs);
+      rc = fa_reduce(p->i64.plan, nullptr, p->i64.rows.data(), p->n_total, nullptr, nullptr,
+                     io[d].out64, 0, p->comm->cs);
       if (rc) return rc;
     }
   }
@@ -407,6 +514,205 @@ int fa_reduce_sharded(fa_shard_plan* const* plans, int nlocal, const fa_shard_io
     hipEvent_t done = p->ev[nch + 1];
     FA_HIP_TRY(hipEventRecord(done, p->comm->cs));
     FA_HIP_TRY(hipStreamWaitEvent((hipStream_t)io[d].stream, done, 0));
+  }
+  return FA_OK;
+}
+
+// ============================================================== e2 ========
+int fa_stripe_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
+                          const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
+                          unsigned flags, fa_stripe_plan** out) {
+  if (!out) return set_err(FA_E_INVAL, "fa_stripe_plan_create: out is NULL");
+  *out = nullptr;
+  if (!comm || !counts) return set_err(FA_E_INVAL, "fa_stripe_plan_create: NULL comm/counts");
+  if (!(flags & FA_PLAN_GAPS_ARE_PADDING))
+    return set_err(FA_E_INVAL,
+                   "fa_stripe_plan_create: the layout must allow writes to its padding "
+                   "(FA_PLAN_GAPS_ARE_PADDING): stripe exchanges span it");
+  int n_total = 0, lo_slot = 0;
+  int rc = slot_layout(comm, counts, &n_total, &lo_slot, "fa_stripe_plan_create");
+  if (rc) return rc;
+  DeviceGuard g;
+  FA_HIP_TRY(hipSetDevice(comm->device));
+  std::vector<fa_tile_desc> t32, t64;
+  rc = layout_tiles(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, flags, &t32, &t64);
+  if (rc) return rc;
+
+  fa_stripe_plan* p = new fa_stripe_plan();
+  p->comm = comm;
+  p->f32_numel = f32_numel;
+  p->i64_numel = i64_numel;
+  p->n_local = counts[comm->rank];
+  p->n_total = n_total;
+  p->lo_slot = lo_slot;
+  p->counts.assign(counts, counts + comm->nranks);
+  int s0 = 0;
+  for (int r = 0; r < comm->nranks; ++r) {
+    p->first_slot.push_back(s0);
+    s0 += counts[r];
+  }
+  std::vector<size_t> cut;
+  cut_tiles(t32, comm->nranks, f32_numel, &cut, &p->lo);
+  const int me = comm->rank;
+  const int64_t L = p->lo[me + 1] - p->lo[me];
+  hipError_t e = hipSuccess;
+  if (cut[me] < cut[me + 1]) {
+    rc = fa_plan_create_from_tiles(t32.data() + cut[me], (int)(cut[me + 1] - cut[me]),
+                                   f32_numel, i64_numel, 0, flags, &p->stripe);
+    if (rc) {
+      free_stripe(p);
+      return rc;
+    }
+    // one row per client slot (local rows unused), 256-B aligned rows; the
+    // stripe starts on a 64-float boundary, so (row - lo) stays aligned
+    p->row = (L + 63) / 64 * 64;
+    e = hipMalloc(&p->recv, (size_t)n_total * p->row * 4);
+    if (e == hipSuccess) e = hipMalloc(&p->sbuf, (size_t)p->row * 4);
+    if (e == hipSuccess) e = hipMemset(p->sbuf, 0, (size_t)p->row * 4);
+    for (int k = 0; e == hipSuccess && k < n_total; ++k)
+      p->ptrs.push_back(p->recv + (size_t)k * p->row - p->lo[me]);  // element e at [e - lo]
+  }
+  if (e != hipSuccess) {
+    free_stripe(p);
+    return set_err(FA_E_HIP, "fa_stripe_plan_create: %s", hipGetErrorString(e));
+  }
+  rc = p->i64.init(comm, t64, counts, f32_numel, i64_numel, flags);
+  if (!rc) rc = make_events(&p->ev, 3);
+  if (rc) {
+    free_stripe(p);
+    return rc;
+  }
+  *out = p;
+  return FA_OK;
+}
+
+int fa_stripe_plan_destroy(fa_stripe_plan* p) {
+  free_stripe(p);
+  return FA_OK;
+}
+
+int fa_reduce_striped(fa_stripe_plan* const* plans, int nlocal, const fa_shard_io* io,
+                      int root) {
+  if (nlocal < 1 || !plans || !io) return set_err(FA_E_INVAL, "fa_reduce_striped: bad arguments");
+  for (int d = 0; d < nlocal; ++d) {
+    const fa_stripe_plan* p = plans[d];
+    if (!p) return set_err(FA_E_INVAL, "fa_reduce_striped: plan %d is NULL", d);
+    if (root >= p->comm->nranks) return set_err(FA_E_INVAL, "fa_reduce_striped: root=%d", root);
+    if (io[d].weights)
+      return set_err(FA_E_INVAL, "fa_reduce_striped: the exact mode takes no weights");
+    const bool result = root < 0 || root == p->comm->rank;
+    if (p->n_local > 0 && !io[d].c32)
+      return set_err(FA_E_INVAL, "fa_reduce_striped: fp32 buckets required (GPU %d)", d);
+    if (p->n_local > 0 && p->i64.plan && !io[d].c64)
+      return set_err(FA_E_INVAL, "fa_reduce_striped: int64 buckets required (GPU %d)", d);
+    if (result && (!io[d].out32 || (p->i64.plan && !io[d].out64)))
+      return set_err(FA_E_INVAL, "fa_reduce_striped: result buckets required on rank %d",
+                     p->comm->rank);
+  }
+  DeviceGuard g;
+  // the inputs are ready on the caller's streams
+  for (int d = 0; d < nlocal; ++d) {
+    fa_stripe_plan* p = plans[d];
+    FA_HIP_TRY(hipSetDevice(p->comm->device));
+    FA_HIP_TRY(hipEventRecord(p->ev[0], (hipStream_t)io[d].stream));
+    FA_HIP_TRY(hipStreamWaitEvent(p->comm->cs, p->ev[0], 0));
+  }
+  // 1. every client's values for stripe r go to rank r
+  NCCL_TRY(ncclGroupStart());
+  for (int d = 0; d < nlocal; ++d) {
+    fa_stripe_plan* p = plans[d];
+    (void)hipSetDevice(p->comm->device);
+    const int me = p->comm->rank;
+    const int64_t Lme = p->lo[me + 1] - p->lo[me];
+    for (int r = 0; r < p->comm->nranks; ++r) {
+      if (r == me) continue;
+      const int64_t Lr = p->lo[r + 1] - p->lo[r];
+      ncclResult_t x = ncclSuccess;
+      for (int j = 0; x == ncclSuccess && Lr > 0 && j < p->n_local; ++j)
+        x = ncclSend(io[d].c32[j] + p->lo[r], (size_t)Lr, ncclFloat32, r, p->comm->nc,
+                     p->comm->cs);
+      for (int k = 0; x == ncclSuccess && Lme > 0 && k < p->counts[r]; ++k)
+        x = ncclRecv(p->recv + (size_t)(p->first_slot[r] + k) * p->row, (size_t)Lme,
+                     ncclFloat32, r, p->comm->nc, p->comm->cs);
+      if (x != ncclSuccess) {
+        ncclGroupEnd();
+        return set_err(FA_E_COMM, "stripe exchange: %s", ncclGetErrorString(x));
+      }
+    }
+  }
+  NCCL_TRY(ncclGroupEnd());
+  // 2. each rank reduces its stripe over all n_total clients, exact order
+  for (int d = 0; d < nlocal; ++d) {
+    fa_stripe_plan* p = plans[d];
+    if (!p->stripe) continue;
+    FA_HIP_TRY(hipSetDevice(p->comm->device));
+    std::vector<const float*> src(p->ptrs);
+    for (int j = 0; j < p->n_local; ++j) src[p->lo_slot + j] = io[d].c32[j];
+    const int rc = fa_reduce(p->stripe, src.data(), nullptr, p->n_total, nullptr,
+                             p->sbuf - p->lo[p->comm->rank], nullptr, 0, p->comm->cs);
+    if (rc) return rc;
+  }
+  // 3. the stripes to the result ranks
+  NCCL_TRY(ncclGroupStart());
+  for (int d = 0; d < nlocal; ++d) {
+    fa_stripe_plan* p = plans[d];
+    (void)hipSetDevice(p->comm->device);
+    const int me = p->comm->rank;
+    const bool result = root < 0 || root == me;
+    const int64_t Lme = p->lo[me + 1] - p->lo[me];
+    ncclResult_t x = ncclSuccess;
+    for (int r = 0; x == ncclSuccess && r < p->comm->nranks; ++r) {
+      if (r == me) continue;
+      const int64_t Lr = p->lo[r + 1] - p->lo[r];
+      if (Lme > 0 && (root < 0 || r == root))
+        x = ncclSend(p->sbuf, (size_t)Lme, ncclFloat32, r, p->comm->nc, p->comm->cs);
+      if (x == ncclSuccess && Lr > 0 && result)
+        x = ncclRecv(io[d].out32 + p->lo[r], (size_t)Lr, ncclFloat32, r, p->comm->nc,
+                     p->comm->cs);
+    }
+    if (x != ncclSuccess) {
+      ncclGroupEnd();
+      return set_err(FA_E_COMM, "stripe gather: %s", ncclGetErrorString(x));
+    }
+  }
+  NCCL_TRY(ncclGroupEnd());
+  for (int d = 0; d < nlocal; ++d) {
+    fa_stripe_plan* p = plans[d];
+    const int me = p->comm->rank;
+    const int64_t Lme = p->lo[me + 1] - p->lo[me];
+    if (!(root < 0 || root == me) || Lme == 0) continue;
+    FA_HIP_TRY(hipSetDevice(p->comm->device));
+    FA_HIP_TRY(hipMemcpyAsync(io[d].out32 + p->lo[me], p->sbuf, (size_t)Lme * 4,
+                              hipMemcpyDeviceToDevice, p->comm->cs));
+  }
+  // 4. int64 keys as in e1
+  if (plans[0]->i64.plan) {
+    std::vector<I64Part*> parts;
+    std::vector<const fa_comm*> comms;
+    for (int d = 0; d < nlocal; ++d) {
+      fa_stripe_plan* p = plans[d];
+      FA_HIP_TRY(hipSetDevice(p->comm->device));
+      int rc = p->i64.stack_local(io[d].c64, p->n_local, p->comm->cs);
+      if (rc) return rc;
+      parts.push_back(&p->i64);
+      comms.push_back(p->comm);
+    }
+    int rc = i64_exchange(parts.data(), comms.data(), nlocal);
+    if (rc) return rc;
+    for (int d = 0; d < nlocal; ++d) {
+      fa_stripe_plan* p = plans[d];
+      if (!(root < 0 || root == p->comm->rank)) continue;
+      FA_HIP_TRY(hipSetDevice(p->comm->device));
+      rc = fa_reduce(p->i64.plan, nullptr, p->i64.rows.data(), p->n_total, nullptr, nullptr,
+                     io[d].out64, 0, p->comm->cs);
+      if (rc) return rc;
+    }
+  }
+  for (int d = 0; d < nlocal; ++d) {
+    fa_stripe_plan* p = plans[d];
+    FA_HIP_TRY(hipSetDevice(p->comm->device));
+    FA_HIP_TRY(hipEventRecord(p->ev[2], p->comm->cs));
+    FA_HIP_TRY(hipStreamWaitEvent((hipStream_t)io[d].stream, p->ev[2], 0));
   }
   return FA_OK;
 }

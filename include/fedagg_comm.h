@@ -1,7 +1,7 @@
 /*
  * fedagg_comm.h — C ABI of libfedagg_comm.so: the multi-GPU form of the
  * server-side aggregation (SURVEY.md §8 b "fa_comm_init / fa_mean_f32_multi",
- * §8 e1), natively over RCCL (xGMI inside one node).
+ * §8 e1 and e2), natively over RCCL (xGMI inside one node).
  *
  * Reference: the round loops aggregate every client of a round into one
  * global model (train_fedavg.py:138-149, train_feddct.py:34-56); when the
@@ -20,8 +20,8 @@
  *   over all N_total clients, so they match the single-GPU result bit for bit.
  *
  * The cross-rank sum re-associates fp32: the fp32 result is NOT bit-identical
- * to the single-process reference (the exact element-striped mode lives in
- * feddct_amd/dist.py StripedAggregator).  With one rank it is bit-identical.
+ * to the single-process reference (the exact column-striped mode is
+ * fa_reduce_striped, below).  With one rank it is bit-identical.
  *
  * Process models:
  *   - one process per GPU (the product's): rank 0 calls fa_comm_unique_id,
@@ -93,6 +93,29 @@ typedef struct fa_shard_io {
  * clients of fp32(x_i * w_i) (no division); int64 keys always take the
  * mean-and-truncate path. */
 int fa_reduce_sharded(fa_shard_plan *const *plans, int nlocal,
+                      const fa_shard_io *io, int root);
+
+/* ---- exact mode: column stripes ----------------------
+ * Rank r owns a contiguous column stripe [lo_r, lo_{r+1}) of the bucket (cut
+ * before 256-B aligned vector tiles, equal shares of the elements).  A round
+ * (fa_reduce_striped):
+ *   1. grouped ncclSend/ncclRecv move every client's values for stripe r to
+ *      rank r (n_local * (W-1)/W of a bucket out per rank: the price of
+ *      exactness on device-resident inputs);
+ *   2. each rank reduces its stripe over all n_total clients in the exact
+ *      torch order (every tile keeps its column's order);
+ *   3. the finished stripes travel to the root (root >= 0) or to every rank;
+ *   int64 keys as in e1.  The result is bit-identical to one GPU's
+ *   fa_reduce over all clients.  Unweighted only (io.weights must be NULL).
+ * Same counts / io conventions as the sharded plan; the plan owns a receive
+ * buffer of n_total stripe rows. */
+typedef struct fa_stripe_plan fa_stripe_plan;
+int fa_stripe_plan_create(fa_comm *comm, const fa_seg *seg32, int nseg32,
+                          int64_t f32_numel, const fa_seg *seg64, int nseg64,
+                          int64_t i64_numel, const int *counts, unsigned flags,
+                          fa_stripe_plan **out);
+int fa_stripe_plan_destroy(fa_stripe_plan *plan);
+int fa_reduce_striped(fa_stripe_plan *const *plans, int nlocal,
                       const fa_shard_io *io, int root);
 
 #ifdef __cplusplus

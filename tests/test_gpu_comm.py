@@ -134,3 +134,46 @@ def test_native_errors(comm):
         agg.step()
     with pytest.raises(_lib.FedaggError, match="clients in total"):
         ShardPlan(comm, layout, [0])
+
+
+@pytest.mark.parametrize("lay", ["wrn16_8_c10", "wrnsl16_8_sf4_c10_proxy",
+                                 "wrnsl16_8_sf4_c10_main"])
+@pytest.mark.parametrize("final", ["reduce", "allreduce"])
+def test_native_striped_one_rank_is_bit_exact(comm, lay, final):
+    """The exact mode (fa_reduce_striped): with one rank the stripe is the
+    whole bucket and the exchanges are empty — the tile subset, the receive
+    pointer arithmetic for local clients, the stripe gather copy and the
+    int64 path must reproduce the single-GPU result bit for bit."""
+    from feddct_amd.comm import NativeStripedAggregator
+    man = load_manifest(lay)
+    layout = BucketLayout.from_manifest(man)
+    n = 20
+    clients = make_clients(layout, man, range(n), DEV, mode=synth.MODE_ADVERSARIAL)
+    want32, want64 = _single_gpu(layout, clients)
+    out32 = torch.full_like(clients[0][0], float("nan"))
+    out64 = torch.full_like(clients[0][1], -7)
+    agg = NativeStripedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], n,
+                                  out32, out64, comm, final=final)
+    for _ in range(2):
+        agg.step()
+    torch.cuda.synchronize()
+    mask = _layout_pad_mask(layout)
+    nan = torch.isnan(want32[mask])
+    assert torch.equal(torch.isnan(out32[mask]), nan)
+    assert torch.equal(out32[mask].view(torch.int32)[~nan], want32[mask].view(torch.int32)[~nan])
+    assert torch.equal(out64, want64)
+
+
+def test_native_striped_refuses_weights(comm):
+    from feddct_amd import _lib
+    from feddct_amd.comm import NativeStripedAggregator
+    man = load_manifest("wrnsl16_8_sf4_c10_main")
+    layout = BucketLayout.from_manifest(man)
+    clients = make_clients(layout, man, range(3), DEV)
+    o32, o64 = torch.zeros_like(clients[0][0]), torch.zeros_like(clients[0][1])
+    agg = NativeStripedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], 3,
+                                  o32, o64, comm)
+    w = (ctypes.c_float * 3)(1, 1, 1)
+    agg.io.weights = ctypes.cast(w, ctypes.c_void_p)
+    with pytest.raises(_lib.FedaggError, match="no weights"):
+        agg.step()
