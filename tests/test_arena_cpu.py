@@ -1,5 +1,4 @@
 """Arena binding and the shim's host-side checks (no GPU needed)."""
-import numpy as np
 import pytest
 import torch
 
