@@ -30,8 +30,8 @@ FA_COMM_UID_BYTES = 128
 
 COMM_EXPORTS = ["fa_comm_unique_id", "fa_comm_init_rank", "fa_comm_init", "fa_comm_destroy",
                 "fa_comm_info", "fa_shard_plan_create", "fa_shard_plan_destroy",
-                "fa_reduce_sharded", "fa_stripe_plan_create", "fa_stripe_plan_destroy",
-                "fa_reduce_striped"]
+                "fa_reduce_sharded", "fa_mean_f32_multi", "fa_stripe_plan_create",
+                "fa_stripe_plan_destroy", "fa_reduce_striped"]
 
 _P, _I, _I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
 
@@ -56,6 +56,7 @@ def _load():
                                  ctypes.c_uint, ctypes.POINTER(_P)],
         "fa_shard_plan_destroy": [_P],
         "fa_reduce_sharded": [ctypes.POINTER(_P), _I, ctypes.POINTER(FaShardIO), _I],
+        "fa_mean_f32_multi": [_P, _P, ctypes.POINTER(_I), _I64, _P, _P, _I, _I, _P],
         "fa_stripe_plan_create": [_P, _P, _I, _I64, _P, _I, _I64, ctypes.POINTER(_I),
                                   ctypes.c_uint, ctypes.POINTER(_P)],
         "fa_stripe_plan_destroy": [_P],

@@ -22,6 +22,9 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -280,6 +283,13 @@ int i64_exchange(I64Part* const* parts, const fa_comm* const* comms, int nlocal)
 }
 }  // namespace
 
+// fa_mean_f32_multi's shard plans, by (communicator, layout, counts); a
+// communicator's entries go with it (fa_comm_destroy).
+namespace {
+std::mutex g_multi_mu;
+std::map<std::string, fa_shard_plan*> g_multi;
+}  // namespace
+
 extern "C" {
 
 int fa_comm_unique_id(unsigned char* id, int len) {
@@ -329,6 +339,17 @@ int fa_comm_init(int ndev, const int* devs, fa_comm** comms) {
 
 int fa_comm_destroy(fa_comm* c) {
   if (!c) return FA_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    for (auto it = g_multi.begin(); it != g_multi.end();) {
+      if (it->second->comm == c) {
+        free_shard(it->second);
+        it = g_multi.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
   DeviceGuard g;
   (void)hipSetDevice(c->device);
   if (c->cs) (void)hipStreamDestroy(c->cs);
@@ -516,6 +537,37 @@ int fa_reduce_sharded(fa_shard_plan* const* plans, int nlocal, const fa_shard_io
     FA_HIP_TRY(hipStreamWaitEvent((hipStream_t)io[d].stream, done, 0));
   }
   return FA_OK;
+}
+
+// Stateless form (SURVEY.md §8 b's fa_mean_f32_multi): fp32 segments only,
+// shard plans cached per (communicator, layout, counts); 8 chunks.
+int fa_mean_f32_multi(fa_comm* comm, const float* const* clients, const int* counts,
+                      int64_t numel, float* out, const fa_seg* segs, int nseg, int root,
+                      void* stream) {
+  if (!comm || !counts) return set_err(FA_E_INVAL, "fa_mean_f32_multi: NULL comm/counts");
+  if (nseg < 0 || (nseg > 0 && !segs)) return set_err(FA_E_INVAL, "fa_mean_f32_multi: segs");
+  std::string key((const char*)&comm, sizeof comm);
+  key.append((const char*)&numel, sizeof numel);
+  key.append((const char*)counts, sizeof(int) * comm->nranks);
+  if (nseg > 0) key.append((const char*)segs, sizeof(fa_seg) * nseg);
+  fa_shard_plan* plan = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    auto it = g_multi.find(key);
+    if (it != g_multi.end()) {
+      plan = it->second;
+    } else {
+      const int rc = fa_shard_plan_create(comm, segs, nseg, numel, nullptr, 0, 0, counts, 8,
+                                          FA_PLAN_GAPS_ARE_PADDING, &plan);
+      if (rc) return rc;
+      g_multi[key] = plan;
+    }
+  }
+  fa_shard_io io{};
+  io.c32 = clients;
+  io.out32 = out;
+  io.stream = stream;
+  return fa_reduce_sharded(&plan, 1, &io, root);
 }
 
 // ============================================================== e2 ========

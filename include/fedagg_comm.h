@@ -95,6 +95,16 @@ typedef struct fa_shard_io {
 int fa_reduce_sharded(fa_shard_plan *const *plans, int nlocal,
                       const fa_shard_io *io, int root);
 
+/* Stateless form of the sharded round for fp32 keys (SURVEY.md §8 b's
+ * fa_mean_f32_multi): `clients` = this rank's counts[rank] buckets of numel
+ * floats laid out by segs (as fa_mean_f32; gaps are treated as padding);
+ * out = the mean over all ranks' clients on `root` (root < 0: every rank).
+ * The shard plan is cached per (comm, layout, counts) and released with the
+ * communicator (fa_comm_destroy). */
+int fa_mean_f32_multi(fa_comm *comm, const float *const *clients,
+                      const int *counts, int64_t numel, float *out,
+                      const fa_seg *segs, int nseg, int root, void *stream);
+
 /* ---- exact mode: column stripes ----------------------
  * Rank r owns a contiguous column stripe [lo_r, lo_{r+1}) of the bucket (cut
  * before 256-B aligned vector tiles, equal shares of the elements).  A round

@@ -177,3 +177,31 @@ def test_native_striped_refuses_weights(comm):
     agg.io.weights = ctypes.cast(w, ctypes.c_void_p)
     with pytest.raises(_lib.FedaggError, match="no weights"):
         agg.step()
+
+
+def test_stateless_mean_f32_multi():
+    """fa_mean_f32_multi (SURVEY.md §8 b's stateless form) on a one-rank
+    communicator: the fp32 mean equals the single-GPU fa_mean_f32; its cached
+    plan goes away with the communicator."""
+    from feddct_amd import _lib
+    from feddct_amd import comm as C
+    torch.cuda.set_device(DEV)
+    c = C.Comm.single()
+    man = load_manifest("wrn16_8_c10")
+    layout = BucketLayout.from_manifest(man)
+    clients = make_clients(layout, man, range(6), DEV, mode=synth.MODE_ADVERSARIAL)
+    ptrs = _lib.ptr_array([x[0].data_ptr() for x in clients])
+    segs, nseg = _lib.seg_array(layout.segs32)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    want = torch.zeros_like(clients[0][0])
+    _lib.check(_lib.lib.fa_mean_f32(ptrs, 6, layout.f32_numel, want.data_ptr(), segs, nseg, st))
+    got = torch.zeros_like(want)
+    counts = (ctypes.c_int * 1)(6)
+    for _ in range(2):  # the second call takes the cached plan
+        _lib.check(C.lib().fa_mean_f32_multi(c.handle, ptrs, counts, layout.f32_numel,
+                                             got.data_ptr(), segs, nseg, 0, st),
+                   "fa_mean_f32_multi")
+    torch.cuda.synchronize()
+    mask = _layout_pad_mask(layout)
+    assert torch.equal(got[mask], want[mask])
+    c.close()
