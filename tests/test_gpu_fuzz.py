@@ -32,10 +32,13 @@ def _case(seed):
         off += m + gap
     numel = off + 64
     n = int(rng.choice([1, 2, 3, 5, 8, 15, 16, 17, 20, 33, 40, 129, 140]))
-    nseg64 = int(rng.integers(0, 3))
-    segs64 = [(j, 1) for j in range(nseg64)]
+    segs64, o64 = [], 0
+    for _ in range(int(rng.integers(0, 4))):  # int64 keys: scalars and longer ones
+        m = int(rng.choice([1, 1, 2, 5, 33, 100]))
+        segs64.append((o64, m))
+        o64 += m
     return dict(segs=np.array(segs, np.int64).reshape(-1, 2), numel=numel, n=n,
-                segs64=np.array(segs64, np.int64).reshape(-1, 2), numel64=max(1, nseg64),
+                segs64=np.array(segs64, np.int64).reshape(-1, 2), numel64=max(1, o64),
                 tile=int(rng.choice([1024, 2048, 4096])),
                 gaps_pad=bool(rng.random() < 0.5), weighted=bool(rng.random() < 0.3),
                 flags=int(rng.choice([0, 0, 1, 2])), rng=rng)
