@@ -96,6 +96,24 @@ def ulp_dist(a: torch.Tensor, b: torch.Tensor) -> int:
     return int((ia - ib).abs().max().item())
 
 
+ULP_BUCKETS = ((0, 0), (1, 1), (2, 2), (3, 4), (5, 8), (9, 16), (17, None))
+
+
+def ulp_hist(a: torch.Tensor, b: torch.Tensor) -> dict:
+    """Histogram of per-element ULP distances (SURVEY.md §8 e1 asks for one:
+    the client-sharded sum is re-associated, so it is not bit-exact)."""
+    ia = a.view(torch.int32).to(torch.int64)
+    ib = b.view(torch.int32).to(torch.int64)
+    ia = torch.where(ia < 0, -(ia & 0x7FFFFFFF), ia)
+    ib = torch.where(ib < 0, -(ib & 0x7FFFFFFF), ib)
+    d = (ia - ib).abs()
+    out = {}
+    for lo, hi in ULP_BUCKETS:
+        m = d >= lo if hi is None else (d >= lo) & (d <= hi)
+        out[f"{lo}+" if hi is None else (str(lo) if lo == hi else f"{lo}-{hi}")] = int(m.sum().item())
+    return out
+
+
 def pmc_traffic(n_gpus):
     """HBM bytes per launch of the reduce kernel from the committed rocprofv3
     PMC summary (profiles/*pmc*.json written by tools/pmc_summary.py)."""
@@ -862,11 +880,13 @@ def main():
             torch.cuda.synchronize()
             extra["parity"] = {"vs": f"exact single-GPU torch order over {N_CLIENTS * world} clients",
                                "max_ulp_fp32": ulp_dist(out32, ex32),
+                               "ulp_histogram_fp32": ulp_hist(out32, ex32),
                                "max_abs_err_fp32": float((out32 - ex32).abs().max()),
                                "int64_bit_exact": bool(torch.equal(out64, ex64)),
                                "allreduce_mode_same_as_reduce_mode": bool(torch.equal(a32, out32))}
             if n32 is not None and "error" not in extra.get("native_mode", {}):
                 extra["native_mode"]["max_ulp_fp32_vs_exact"] = ulp_dist(n32, ex32)
+                extra["native_mode"]["ulp_histogram_fp32"] = ulp_hist(n32, ex32)
                 extra["native_mode"]["int64_bit_exact"] = bool(torch.equal(n64, ex64))
             if striped is not None:
                 striped["bit_exact"] = bool(torch.equal(s32, ex32) and torch.equal(s64, ex64))
