@@ -816,6 +816,10 @@ def main():
         ncomm = None
         e1 = {f"torch.distributed/{args.chunks}chunks": None}
         try:
+            if args.same_device:
+                # RCCL cannot place two ranks on one GPU; the rehearsal skips
+                # the native communicator (a real N>1 run never sets this)
+                raise RuntimeError("native comm skipped: --same-device rehearsal")
             from feddct_amd.comm import Comm, NativeShardedAggregator
             ncomm = Comm.from_process_group(group)
             n32, n64 = torch.zeros_like(out32), torch.zeros_like(out64)
