@@ -139,11 +139,12 @@ __global__ __launch_bounds__(kFinBlk) void prox_finish(const int* __restrict__ s
                                                        const float* __restrict__ partials,
                                                        float* __restrict__ norms,
                                                        float* __restrict__ total) {
-  extern __shared__ float dyn[];  // [nchunks partials][nseg + 1 boundaries]
-  __shared__ float red[kFinWaves];
+  // [nchunks partials][nseg + 1 boundaries][nseg norms]
+  extern __shared__ float dyn[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const float* P = partials;
   const int* F = seg_first;
+  float* NL = norms;  // where the norms are summed from
   if constexpr (LDS) {
     float* sp = dyn;
     int* sf = reinterpret_cast<int*>(dyn + nchunks);
@@ -164,23 +165,25 @@ __global__ __launch_bounds__(kFinBlk) void prox_finish(const int* __restrict__ s
     __syncthreads();
     P = sp;
     F = sf;
+    NL = reinterpret_cast<float*>(sf + nseg + 1);
   }
   for (int k = wave; k < nseg; k += kFinWaves) {
     float sq = 0.f;
     for (int i = F[k] + lane; i < F[k + 1]; i += 64) sq += P[i];
     sq = wave_sum(sq);
-    if (lane == 0) norms[k] = sqrtf(sq);
+    if (lane == 0) {
+      const float n = sqrtf(sq);
+      norms[k] = n;
+      if constexpr (LDS) NL[k] = n;
+    }
   }
-  __syncthreads();  // norms[] (global) written by this workgroup's waves
-  float t = 0.f;
-  for (int k = threadIdx.x; k < nseg; k += kFinBlk) t += norms[k];
-  t = wave_sum(t);
-  if (lane == 0) red[wave] = t;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float r = 0.f;
-    for (int i = 0; i < kFinWaves; ++i) r += red[i];
-    *total = r;
+  __syncthreads();  // NL[] written by this workgroup's waves
+  // the norms (a few hundred) summed by wave 0 alone: no second barrier
+  if (wave == 0) {
+    float t = 0.f;
+    for (int k = lane; k < nseg; k += 64) t += NL[k];
+    t = wave_sum(t);
+    if (lane == 0) *total = t;
   }
 }
 constexpr size_t kFinLdsMax = 64 * 1024;  // the default dynamic-LDS limit
@@ -298,7 +301,7 @@ int fa_prox_norms(const fa_norm_plan* p, const float* a, const float* b, float* 
                        p->d_partials);
     FA_HIP_TRY(hipGetLastError());
   }
-  const size_t lds = (size_t)(p->nchunks + p->nseg + 1) * 4;
+  const size_t lds = (size_t)(p->nchunks + 2 * p->nseg + 1) * 4;
   if (lds <= kFinLdsMax)
     hipLaunchKernelGGL(prox_finish<true>, dim3(1), dim3(kFinBlk), lds, st, p->d_seg_first,
                        p->nseg, p->nchunks, p->d_partials, norms, total);
