@@ -200,7 +200,9 @@ def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
     serial:    H2D of N·B, one kernel, D2H of B, one stream;
     pipelined: feddct_amd/pipeline.py (8 column chunks, H2D / reduce / D2H
                overlapped on two copy streams), result to the global only,
-               and with the broadcast (D2H into all N client buckets too)."""
+               and with the broadcast (D2H into all N client buckets too);
+    serial_pageable: the serial round from ordinary (pageable) host tensors
+               and into a pageable result (SURVEY.md §8 d asks for both)."""
     from feddct_amd.pipeline import HostPipeline
     n = len(clients)
     host = [(c[0].cpu().pin_memory(), c[1].cpu().pin_memory()) for c in clients]
@@ -215,6 +217,19 @@ def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
         reducer_dev()
         out_h32.copy_(out32, non_blocking=True)
         out_h64.copy_(out64, non_blocking=True)
+        torch.cuda.synchronize()
+
+    pageable = [(c[0].cpu(), c[1].cpu()) for c in clients]
+    out_p32 = torch.empty_like(out32, device="cpu")
+    out_p64 = torch.empty_like(out64, device="cpu")
+
+    def serial_pageable():
+        for (h32, h64), (d32, d64) in zip(pageable, clients):
+            d32.copy_(h32, non_blocking=True)
+            d64.copy_(h64, non_blocking=True)
+        reducer_dev()
+        out_p32.copy_(out32, non_blocking=True)
+        out_p64.copy_(out64, non_blocking=True)
         torch.cuda.synchronize()
 
     pipe = HostPipeline(layout, n, out32.device)
@@ -234,14 +249,17 @@ def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
     piped()
     res["pipelined_bit_exact"] = bool(torch.equal(out_h32, out32.cpu()) and
                                       torch.equal(out_h64, out64.cpu()))
-    for name, fn in (("serial", serial), ("pipelined", piped),
-                     ("pipelined_with_broadcast", piped_bcast)):
+    for name, fn in (("serial", serial), ("serial_pageable", serial_pageable),
+                     ("pipelined", piped), ("pipelined_with_broadcast", piped_bcast)):
         fn()
         t0 = time.perf_counter()
         for _ in range(reps):
             fn()
         t = (time.perf_counter() - t0) / reps
         res[name] = {"ms": round(t * 1e3, 3), "GBps": round(nbytes / t / 1e9, 2)}
+    res["serial_pageable"]["bit_exact"] = bool(torch.equal(out_p32, out32.cpu()) and
+                                               torch.equal(out_p64, out64.cpu()))
+    del pageable
     return res
 
 
