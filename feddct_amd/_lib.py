@@ -41,6 +41,7 @@ FA_PLAN_TUNE_LD_PLAIN = 128
 FA_PLAN_TUNE_ST_SC1 = 0x10000
 FA_PLAN_TUNE_BATCH1 = 0x20000
 FA_PLAN_TUNE_BATCH4 = 0x40000
+FA_PLAN_TUNE_FUSED_BCAST = 0x80000
 
 
 def FA_PLAN_TUNE_BLOCKS_PER_CU(c):

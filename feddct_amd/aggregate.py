@@ -19,8 +19,8 @@ client carrying keys the global model lacks (after the global is updated).
 
 Where the work runs: client state is bound once into flat device buckets
 (arena.py) and the whole state_dict — every fp32 key, every int64 key — is
-reduced by ONE launch of the HIP kernel (csrc/fedagg.hip) that also writes the
-broadcast.  Modules living in host memory (the reference's CPU configuration)
+reduced by ONE launch of the HIP kernel (csrc/fedagg.hip), and the broadcast
+is a second launch over the same tile table (FA_F_BCAST).  Modules living in host memory (the reference's CPU configuration)
 are bound to pinned host buckets and staged through device buckets
 (host-inclusive path).  There is no CPU arithmetic fallback.
 """
@@ -194,7 +194,8 @@ def server_aggregate(global_model, client_models):
 class _Pair(torch.nn.Module):
     """A FedDCT client slot as one module: (main client, proxy) under the
     keys "0." and "1.".  Binding a pair puts both halves' state in ONE bucket,
-    so a round is one launch; the per-key arithmetic is unchanged."""
+    so a round is one reduce launch (+ its broadcast launch); the per-key
+    arithmetic is unchanged."""
 
     def __init__(self, a, b):
         super().__init__()
@@ -217,7 +218,7 @@ def server_aggregate_split(global_model_a, global_model_b, models_a, models_b):
     (or client and server) halves reduced and broadcast independently.
 
     When every slot has both halves, each slot's pair is bound to one bucket
-    and both reductions + both broadcasts run as ONE launch.  Anything the
+    and both reductions run as ONE launch, both broadcasts as one more.  Anything the
     joint path would report differently from the reference (a missing or
     mismatched key, extra keys) takes the two-call path, which reproduces the
     reference's errors and their order exactly."""

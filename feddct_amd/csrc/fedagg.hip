@@ -500,6 +500,36 @@ __global__ void div_trunc_i64_kernel(const float* __restrict__ x, float d,
     out[j] = (int64_t)__fdiv_rn(x[j], d);
 }
 
+// The round's broadcast (train_fedavg.py:148-149) after the reduce, over the
+// same tile table: every tile's result range copied into every client bucket
+// (only segment elements are written, as the fused form).  A pure write
+// stream after a pure read stream: 4 % faster than writing the client buckets
+// from inside the reduce (tools/exp_bcast.py: 300.6 vs 313.2 us for the cfg2
+// round), where the interleaved read and write streams pay bus turnarounds.
+__global__ __launch_bounds__(kBlock) void bcast_tiles_kernel(ReduceArgs args) {
+  (void)args;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  for (int ti = blockIdx.x; ti < a.ntiles; ti += gridDim.x) {
+    const Tile t = a.tiles[ti];
+    if (t.kind == K_F32_VEC) {
+      const uint32_t nv = (uint32_t)t.count / 4;
+      for (uint32_t v = threadIdx.x; v < nv; v += kBlock) {
+        const f4 r = ldg4<true>(a.out32 + t.start, v);
+        for (int i = 0; i < a.n; ++i) stg4<true>(const_cast<float*>(cptr32(a, i)) + t.start, v, r);
+      }
+    } else if ((int)threadIdx.x < t.count) {
+      const int64_t e = t.start + threadIdx.x;
+      if (t.kind <= K_F32_INNER) {
+        const float r = a.out32[e];
+        for (int i = 0; i < a.n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
+      } else {
+        const int64_t r = a.out64[e];
+        for (int i = 0; i < a.n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
+      }
+    }
+  }
+}
+
 struct BcastArgs {
   const float* src;
   int n;
@@ -1038,7 +1068,10 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
   }
   int ntiles = in.ntiles, vec_u = plan->vec_u;
   a.nscalar = in.ntiles_tail;
-  if (plan->d_tiles_alt && !weights && n >= 64) {
+  // 1024-float tiles for unweighted N >= 64, and for the fused broadcast
+  // (tuning form) at any N (cfg2 round: 313 vs 318 us, tools/exp_bcast.py)
+  if (plan->d_tiles_alt && !weights &&
+      (n >= 64 || ((flags & FA_F_BCAST) && (plan->flags & FA_PLAN_TUNE_FUSED_BCAST)))) {
     a.tiles = plan->d_tiles_alt;
     ntiles = plan->ntiles_alt;
     a.nscalar = plan->nscalar_alt;
@@ -1046,7 +1079,14 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
   }
   a.ntiles = ntiles;
   a.xcd_swz = (plan->flags & FA_PLAN_TUNE_XCD) ? 1 : 0;
+  const bool split_bcast = (flags & FA_F_BCAST) && !(plan->flags & FA_PLAN_TUNE_FUSED_BCAST);
+  if (split_bcast) a.flags &= ~FA_F_BCAST;
   hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st);
+  if (e == hipSuccess && split_bcast) {
+    a.flags |= FA_F_BCAST;
+    hipLaunchKernelGGL(bcast_tiles_kernel, dim3(ntiles), dim3(kBlock), 0, st, a);
+    e = hipGetLastError();
+  }
   if (table) {
     hipError_t e2 = hipFreeAsync(table, st);
     if (e == hipSuccess) e = e2;

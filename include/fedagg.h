@@ -22,7 +22,7 @@
  *
  *   fa_reduce            stack(...).mean(0) for every key at once, over flat
  *                        per-client buckets (all fp32 keys + all int64 keys),
- *                        optionally fused with the :148-149 broadcast.
+ *                        optionally followed by the :148-149 broadcast.
  *   fa_mean_f32          the same for fp32 keys only, stateless form.
  *   fa_weighted_f32      client-size-weighted extension.
  *   fa_mean_i64_trunc    int64 keys: .float() -> mean -> copy_ into int64
@@ -83,6 +83,7 @@ extern "C" {
 #define FA_PLAN_TUNE_ST_SC1 0x10000u /* tuning: result stores with sc1         */
 #define FA_PLAN_TUNE_BATCH1 0x20000u /* tuning: 1 client per load batch         */
 #define FA_PLAN_TUNE_BATCH4 0x40000u /* tuning: 4 clients per load batch        */
+#define FA_PLAN_TUNE_FUSED_BCAST 0x80000u /* tuning: FA_F_BCAST inside the reduce */
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
 #define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
 /* tuning: persistent grid of 256*k workgroups striding over the tiles */
@@ -141,7 +142,8 @@ int fa_plan_create_from_tiles(const fa_tile_desc *tiles, int ntiles,
                               int64_t f32_numel, int64_t i64_numel,
                               int tile_elems, unsigned flags, fa_plan **out);
 
-/* The hot path: every key of N client buckets -> global bucket, one launch.
+/* The hot path: every key of N client buckets -> global bucket, one launch
+ * (FA_F_BCAST: plus one broadcast launch over the same tiles).
  *   c32[i] / c64[i]  : client i's fp32 / int64 bucket (slot order 0..n-1)
  *   weights          : NULL -> mean (sum / n);  else fp32 w[i], result =
  *                      ordered sum of fp32(x_i * w_i) (no division)

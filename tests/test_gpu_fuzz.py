@@ -51,6 +51,8 @@ def test_random_layouts_bit_exact(seed):
     c = _case(seed)
     rng, n, numel = c["rng"], c["n"], c["numel"]
     flags = _lib.FA_PLAN_GAPS_ARE_PADDING if c["gaps_pad"] else 0
+    if seed % 2:  # FA_F_BCAST cases alternate the split (default) and fused forms
+        flags |= _lib.FA_PLAN_TUNE_FUSED_BCAST
     plan = _lib.Plan(c["segs"], numel, c["segs64"], c["numel64"], tile_elems=c["tile"],
                      flags=flags)
     # adversarial-range values, exact small integers for the int64 keys
@@ -91,5 +93,7 @@ def test_random_layouts_bit_exact(seed):
     if not c["gaps_pad"]:
         assert (got32[~inside] == np.float32(7.25)).all(), "wrote outside the segments"
     if c["flags"] & _lib.FA_F_BCAST:
-        for t in b32:
+        for i, t in enumerate(b32):
             assert bits_equal(t.cpu().numpy()[inside], got32[inside]), "broadcast"
+            if not c["gaps_pad"]:
+                assert bits_equal(t.cpu().numpy()[~inside], x32[i][~inside]), "broadcast gaps"
