@@ -781,10 +781,12 @@ def main():
                            weights=w, plan=reducer.plan)
             tw, _ = timed_launches(wred, max(10, args.steps // 2), 3)
             extra["weighted_GBps"] = round(nbytes_rank / tw / 1e9, 1)
-            fused = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
-                            flags=_lib.FA_F_BCAST, plan=reducer.plan)
-            tb, _ = timed_launches(fused, max(10, args.steps // 2), 3)
-            extra["round_with_fused_broadcast_us"] = round(tb * 1e6, 1)
+            # the round with its broadcast (FA_F_BCAST: reduce launch + broadcast
+            # launch over the same tiles), N*B read + (N+1)*B written
+            bred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
+                           flags=_lib.FA_F_BCAST, plan=reducer.plan)
+            tb, _ = timed_launches(bred, max(10, args.steps // 2), 3)
+            extra["round_with_broadcast_us"] = round(tb * 1e6, 1)
             extra["dropin"] = dropin_timing(layout, clients, dev)
             try:
                 extra["dropin_feddct_cfg3"] = dropin_feddct_timing(dev)
