@@ -652,7 +652,7 @@ def dropin_timing(layout, clients, dev, reps=20):
     ts.sort()
     t = ts[len(ts) // 2]
     return {"server_aggregate_ms": round(t * 1e3, 3),
-            "note": "median wall incl. Python shim, arena checks, fused reduce+broadcast, sync"}
+            "note": "median wall incl. Python shim, arena checks, reduce + broadcast launches, sync"}
 
 
 def _feddct_modules(dev, n=5, cpu=False):
