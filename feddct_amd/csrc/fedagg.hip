@@ -512,10 +512,19 @@ __global__ __launch_bounds__(kBlock) void bcast_tiles_kernel(ReduceArgs args) {
   for (int ti = blockIdx.x; ti < a.ntiles; ti += gridDim.x) {
     const Tile t = a.tiles[ti];
     if (t.kind == K_F32_VEC) {
+      // two vectors per lane per pass (a 2048-float tile in one pass): both
+      // loads issue before the 2N stores
       const uint32_t nv = (uint32_t)t.count / 4;
-      for (uint32_t v = threadIdx.x; v < nv; v += kBlock) {
+      for (uint32_t v = threadIdx.x; v < nv; v += 2 * kBlock) {
+        const uint32_t v2 = v + kBlock;
+        const bool two = v2 < nv;
         const f4 r = ldg4<true>(a.out32 + t.start, v);
-        for (int i = 0; i < a.n; ++i) stg4<true>(const_cast<float*>(cptr32(a, i)) + t.start, v, r);
+        const f4 r2 = two ? ldg4<true>(a.out32 + t.start, v2) : r;
+        for (int i = 0; i < a.n; ++i) {
+          float* d = const_cast<float*>(cptr32(a, i)) + t.start;
+          stg4<true>(d, v, r);
+          if (two) stg4<true>(d, v2, r2);
+        }
       }
     } else if ((int)threadIdx.x < t.count) {
       const int64_t e = t.start + threadIdx.x;
