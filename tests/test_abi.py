@@ -121,3 +121,18 @@ def test_comm_library_exports_every_declared_symbol():
     assert so.fa_shard_plan_create(None, None, 0, 0, None, 0, 0, None, 0, 1,
                                    ctypes.byref(h)) == _lib.FA_E_INVAL
     assert b"NULL" in _lib.lib.fa_last_error()  # one error channel for both libraries
+
+
+def test_header_constants_match_binding():
+    """Every plain FA_* integer macro of include/fedagg.h that the Python
+    binding also names has the same value there."""
+    src = open(os.path.join(ROOT, "include", "fedagg.h")).read()
+    macros = dict(re.findall(r"#define\s+(FA_[A-Z0-9_]+)\s+\(?(-?(?:0x[0-9a-fA-F]+|\d+))u?\)?",
+                             src))
+    checked = 0
+    for name, val in macros.items():
+        if hasattr(_lib, name) and isinstance(getattr(_lib, name), int):
+            assert getattr(_lib, name) == int(val, 0), name
+            checked += 1
+    assert checked >= 10
+    assert _lib.FA_PLAN_TUNE_FUSED_BCAST == 0x80000
