@@ -727,6 +727,11 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        # diagnosis only: a multi-rank run that stalls leaves every rank's
+        # Python stack on stderr (nothing is interrupted)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ.get("FA_BENCH_STACK_DUMP_S", "480")))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
