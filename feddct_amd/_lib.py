@@ -59,7 +59,7 @@ EXPORTS = [
     "fa_mean_i64_trunc", "fa_div_f32", "fa_div_trunc_i64", "fa_broadcast_f32",
     "fa_synth_fill_f32", "fa_synth_fill_i64", "fa_copy_f32",
     "fa_norm_plan_create", "fa_norm_plan_destroy", "fa_prox_norms", "fa_prox_grad",
-    "fa_read_probe_f32",
+    "fa_read_probe_f32", "fa_chain_levels", "fa_reduce_chain",
 ]
 
 
@@ -76,6 +76,11 @@ class FaPlanInfo(ctypes.Structure):
 
 class FaTileDesc(ctypes.Structure):
     _fields_ = [("start", ctypes.c_int64), ("count", ctypes.c_int32), ("kind", ctypes.c_int32)]
+
+
+class FaChain(ctypes.Structure):
+    _fields_ = [("row0", ctypes.c_int), ("n_total", ctypes.c_int), ("state_in", ctypes.c_void_p),
+                ("state_out", ctypes.c_void_p), ("plane", ctypes.c_int64)]
 
 
 class FedaggError(RuntimeError):
@@ -115,6 +120,8 @@ def _load():
         "fa_synth_fill_i64": (_I, [_P, _I64, _I, _I, _I, _P]),
         "fa_copy_f32": (_I, [_P, _P, _I64, _P]),
         "fa_read_probe_f32": (_I, [_P, _I64, _P, _I, _P]),
+        "fa_chain_levels": (ctypes.c_uint, [_I, _I]),
+        "fa_reduce_chain": (_I, [_P, _P, _I, _P, ctypes.POINTER(FaChain), _P, ctypes.c_uint, _P]),
         "fa_norm_plan_create": (_I, [_P, _I, _I64, ctypes.POINTER(_P)]),
         "fa_norm_plan_destroy": (_I, [_P]),
         "fa_prox_norms": (_I, [_P, _P, _P, _P, _P, _P]),

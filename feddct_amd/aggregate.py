@@ -85,7 +85,9 @@ class Engine:
         layout = self.layout_of(global_model)
         ga = get_arena(global_model, layout)
         cas = [get_arena(c, layout) for c in client_models]
-        dev = ga.device
+        # torch.stack (train_fedavg.py:145) needs the clients on one device;
+        # the global may live elsewhere (load_state_dict at :147 copies across)
+        dev = cas[0].device
         for c in cas:
             if c.device != dev:
                 raise RuntimeError(
@@ -99,7 +101,13 @@ class Engine:
         for c in cas:
             c.pack()
         if dev.type == "cuda":
-            self._reduce_device(layout, ga, cas, weights, fuse_bcast)
+            if ga.device == dev:
+                self._reduce_device(layout, ga.f32, ga.i64, cas, weights, fuse_bcast)
+            else:
+                o32, o64 = self._stage(layout, dev)
+                self._reduce_device(layout, o32, o64, cas, weights, fuse_bcast)
+                ga.f32.copy_(o32)
+                ga.i64.copy_(o64)
         else:
             self._reduce_host(layout, ga, cas, weights, fuse_bcast)
         ga.unpack()
@@ -113,11 +121,11 @@ class Engine:
                         + ", ".join(f'"{k}"' for k in c.extra_keys) + ". ")
                 c.f32.copy_(ga.f32)
                 c.i64.copy_(ga.i64)
-                c.unpack()
+                c.unpack(ga)
                 c.mark_written()
         elif fuse_bcast:
             for c in cas:
-                c.unpack()
+                c.unpack(ga)
                 c.mark_written()
 
     def _weights_arg(self, weights, n):
@@ -151,13 +159,25 @@ class Engine:
         self._last_ptrs = (key, tuple(weakref.ref(c) for c in cas), a32, a64)
         return a32, a64
 
-    def _reduce_device(self, layout, ga: ModuleArena, cas: List[ModuleArena], weights, fuse):
+    def _stage(self, layout, device: torch.device):
+        """Result buckets on the clients' device for a global model that
+        lives on another device (cached per layout and device)."""
+        key = ("stage", layout.signature, device.index)
+        st = self._pipes.get(key)
+        if st is None:
+            from .arena import alloc_buckets
+            st = self._pipes[key] = alloc_buckets(layout, device)
+        return st
+
+    def _reduce_device(self, layout, out32: torch.Tensor, out64: torch.Tensor,
+                       cas: List[ModuleArena], weights, fuse):
         n = len(cas)
-        plan = self.plan(layout, ga.device)
+        dev = cas[0].device
+        plan = self.plan(layout, dev)
         flags = _lib.FA_F_BCAST if fuse else 0
         a32, a64 = self._ptr_arrays(cas)
-        self._launch(plan, a32, a64, n, self._weights_arg(weights, n), ga.ptr32, ga.ptr64,
-                     flags, ga.device)
+        self._launch(plan, a32, a64, n, self._weights_arg(weights, n), out32.data_ptr(),
+                     out64.data_ptr(), flags, dev)
 
     def _reduce_host(self, layout, ga: ModuleArena, cas: List[ModuleArena], weights, fuse):
         """Host-resident state (the reference's CPU configuration): the
@@ -165,7 +185,8 @@ class Engine:
         pinned arenas; the broadcast is part of the D2H stream."""
         from .pipeline import HostPipeline
         n = len(cas)
-        dev = torch.device("cuda", torch.cuda.current_device())
+        dev = (ga.device if ga.device.type == "cuda"
+               else torch.device("cuda", torch.cuda.current_device()))
         key = (layout.signature, dev.index, n)
         pipe = self._pipes.get(key)
         if pipe is None:
@@ -195,7 +216,11 @@ class _Pair(torch.nn.Module):
     """A FedDCT client slot as one module: (main client, proxy) under the
     keys "0." and "1.".  Binding a pair puts both halves' state in ONE bucket,
     so a round is one reduce launch (+ its broadcast launch); the per-key
-    arithmetic is unchanged."""
+    arithmetic is unchanged.  Each half's tensors still sit in a storage
+    object of their own (arena._part_bases), so saving one model's
+    state_dict writes only that model's bytes."""
+
+    _fa_storage_parts = ("0.", "1.")
 
     def __init__(self, a, b):
         super().__init__()

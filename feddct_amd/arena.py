@@ -97,27 +97,60 @@ class ModuleArena:
                 raise RuntimeError(
                     f"stack expects each tensor to be equal size, but got {list(s.shape)} "
                     f"(global) and {list(t.shape)} for key {s.key!r}")
-            if t.dtype != s.dtype:
+            if t.dtype != s.dtype and (t.dtype.is_complex or (
+                    s.kind == KIND_I64 and t.dtype.is_floating_point)):
+                # a float value in an integer key: .float() keeps its fraction,
+                # the int64 bucket cannot (the reference's .float() at
+                # train_fedavg.py:145 takes every other dtype, see _packed)
                 raise TypeError(
-                    f"state_dict key {s.key!r}: module dtype {t.dtype} differs from the "
-                    f"global model's {s.dtype} (mixed-dtype client slots are not supported)")
+                    f"state_dict key {s.key!r}: module dtype {t.dtype} cannot be staged in "
+                    f"the global model's {s.dtype} slot")
+            if s.alias_of is not None:
+                a = tensors[s.alias_of]
+                if (t.data_ptr() != a.data_ptr() or t.stride() != a.stride()
+                        or t.dtype != a.dtype):
+                    # the layout says this key shares the other's storage (tied
+                    # weights in the global model); binding an untied module
+                    # to it would silently tie its parameters
+                    raise RuntimeError(
+                        f"state_dict key {s.key!r} is tied to {s.alias_of!r} in the global "
+                        "model but not in this module")
         # keys the module has beyond the layout: the reference's broadcast
         # load_state_dict(strict=True) rejects such a client (train_fedavg.py:149)
         self.extra_keys = [k for k in tensors if k not in layout.by_key]
         self._keyset = list(tensors.keys())
         self._gen = _STRUCT_GEN[0]
         self.f32, self.i64 = alloc_buckets(layout, self.device, pinned)
+        bases = _part_bases(layout, self.f32, self.i64,
+                            getattr(module, "_fa_storage_parts", None))
         self._checks: List[tuple] = []
         self._packed: List[tuple] = []
+        self._packed_keys: List[str] = []
+        self._via_global = set()
         with torch.no_grad():
             for s in layout.slots:
                 d, name = owners[s.key]
                 t = d[name]
-                if s.kind == KIND_PACKF:
-                    self._packed.append((d, name, t, s))
-                    continue
                 bucket = self.i64 if s.kind == KIND_I64 else self.f32
+                if s.kind == KIND_PACKF or t.dtype != s.dtype:
+                    # staged per call: the key's own dtype differs from its
+                    # bucket's (a packed dtype, or a client whose dtype differs
+                    # from the global's — the reference's .float() takes both)
+                    self._packed.append((d, name, t, bucket[s.offset:s.offset + s.numel]
+                                         .view(s.shape)))
+                    self._packed_keys.append(s.key)
+                    if s.kind == KIND_PACKF and t.dtype != s.dtype:
+                        # the reference broadcasts the global's value in the
+                        # global's dtype (train_fedavg.py:148-149): this key
+                        # gets C(G(mean)), not C(mean)
+                        self._via_global.add(s.key)
+                    continue
                 view = bucket[s.offset:s.offset + s.numel].view(s.shape)
+                part = bases.get((s.kind == KIND_I64, _part_of(s.key, bases)))
+                if part is not None:
+                    # same memory, seen through the part's own storage object
+                    pb, plo = part
+                    view = pb[s.offset - plo:s.offset - plo + s.numel].view(s.shape)
                 if s.alias_of is None:
                     view.copy_(t)
                 t.data = view
@@ -161,18 +194,31 @@ class ModuleArena:
 
     # -- keys stored in another dtype: staged through the f32 bucket -------
     def pack(self) -> None:
-        """``.float()`` every non-fp32/int64 key into its f32 slot."""
-        for _, _, t, s in self._packed:
-            self.f32[s.offset:s.offset + s.numel].view(s.shape).copy_(t)
-
-    def unpack(self) -> None:
-        """``copy_`` the f32 slot back into the key's own dtype (the
-        load_state_dict semantics of train_fedavg.py:147)."""
+        """``.float()`` every staged key into its bucket slot (fp32 slots; an
+        integer key into an int64 slot, which is exact)."""
         if not self._packed:
             return
         with torch.no_grad():
-            for _, _, t, s in self._packed:
-                t.copy_(self.f32[s.offset:s.offset + s.numel].view(s.shape))
+            for _, _, t, view in self._packed:
+                view.copy_(t)
+
+    def unpack(self, glob: "ModuleArena" = None) -> None:
+        """``copy_`` the slot back into the key's own dtype (the
+        load_state_dict semantics of train_fedavg.py:147).  ``glob``: the
+        global model's arena, already unpacked, for a broadcast target whose
+        key dtype differs from the global's packed dtype."""
+        if not self._packed:
+            return
+        with torch.no_grad():
+            for key, (_, _, t, view) in zip(self._packed_keys, self._packed):
+                if glob is not None and key in self._via_global:
+                    t.copy_(glob.staged(key))
+                else:
+                    t.copy_(view)
+
+    def staged(self, key: str) -> torch.Tensor:
+        """The module's own tensor of a staged key."""
+        return self._packed[self._packed_keys.index(key)][2]
 
     @property
     def ptr32(self) -> int:
@@ -181,6 +227,41 @@ class ModuleArena:
     @property
     def ptr64(self) -> int:
         return self.i64.data_ptr()
+
+
+def _part_of(key: str, bases) -> str:
+    for (_, pre) in bases:
+        if key.startswith(pre):
+            return pre
+    return ""
+
+
+def _part_bases(layout: BucketLayout, f32: torch.Tensor, i64: torch.Tensor, parts):
+    """Per key-prefix views of the buckets through their OWN storage objects
+    (slices of the bucket storage, which keep it alive).  A FedDCT slot binds
+    its main-client and proxy models as one bucket (one launch per round), but
+    each model's tensors must stay in a storage of their own: torch.save
+    writes whole storages, and the reference saves the two models to separate
+    files (train_feddct.py:455,463 via utils/metric.py:16-32)."""
+    out = {}
+    if not parts:
+        return out
+    for pre in parts:
+        for is64, bucket in ((False, f32), (True, i64)):
+            sl = [s for s in layout.slots if s.key.startswith(pre) and s.alias_of is None
+                  and (s.kind == KIND_I64) == is64]
+            if not sl:
+                continue
+            lo = min(s.offset for s in sl)
+            hi = max(s.offset + s.numel for s in sl)
+            if not is64:
+                hi = min(-(-hi // 64) * 64, bucket.numel())
+            es = bucket.element_size()
+            st = bucket.untyped_storage()[lo * es:hi * es]
+            base = torch.empty(0, dtype=bucket.dtype, device=bucket.device).set_(
+                st, 0, (hi - lo,))
+            out[(is64, pre)] = (base, lo)
+    return out
 
 
 def get_arena(module: torch.nn.Module, layout: BucketLayout) -> ModuleArena:

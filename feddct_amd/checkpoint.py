@@ -98,6 +98,13 @@ def save_checkpoint_proxy_clients(state: dict, is_best: bool, model_dir: str) ->
         save_checkpoint(state, False, model_dir, "proxy_clients_best.pth.tar")
 
 
+def _in_slot(t, s, first32) -> bool:
+    return (isinstance(t, torch.Tensor) and t.dtype == torch.float32
+            and t.untyped_storage().data_ptr() == first32.untyped_storage().data_ptr()
+            and t.storage_offset() == s.offset and tuple(t.shape) == s.shape
+            and t.is_contiguous())
+
+
 def load_into(module: torch.nn.Module, state_dict) -> None:
     """``module.load_state_dict(state_dict)`` (strict); when the module is
     bound and the checkpoint's tensors are views of one bucket-shaped
@@ -111,9 +118,11 @@ def load_into(module: torch.nn.Module, state_dict) -> None:
         module.load_state_dict(state_dict)  # raises like the reference would
         return
     first32 = next((state_dict[s.key] for s in a.layout.slots if s.kind == "f32"), None)
+    # one copy only when every fp32 tensor sits exactly where the bucket
+    # layout puts it (offset, shape, dtype, dense): a file packed any other
+    # way with the same total size takes load_state_dict's checked path
     whole = (first32 is not None and first32.untyped_storage().nbytes() == a.f32.numel() * 4
-             and all(state_dict[s.key].untyped_storage().data_ptr() ==
-                     first32.untyped_storage().data_ptr()
+             and all(_in_slot(state_dict[s.key], s, first32)
                      for s in a.layout.slots if s.kind == "f32"))
     if whole:
         src = torch.empty(0, dtype=torch.float32, device=first32.device)

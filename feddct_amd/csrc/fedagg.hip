@@ -86,6 +86,18 @@ struct ReduceArgs {
   int ntiles;   // tiles in the table (== grid)
   int nscalar;  // leading scalar tiles
   int xcd_swz;  // tuning: give each XCD a contiguous range of vector tiles
+  // The cascade's position (fa_reduce_chain; a plain reduction is row0 = 0,
+  // n_total = n): these clients are rows row0 .. row0+n-1 of an n_total-row
+  // reduction.  The level accumulators start from st_in's planes (bit l of
+  // lev_in: plane l at st_in + l*plane; others +0) and, with st_out, end
+  // there (bit l of lev_out) instead of being finished into out32.
+  int n_total;
+  int row0;
+  int lev_in;
+  int lev_out;
+  const float* st_in;
+  float* st_out;
+  int64_t plane;
   const float* const* tab32;
   const int64_t* const* tab64;
   const float* tabw;
@@ -243,14 +255,14 @@ __device__ __forceinline__ void promote(Acc<U, DEEP>& A, int ii, int lp, int mas
 
 // One batch of NB clients starting at b0.  FULL: every lane's U vectors are
 // inside the tile (no per-lane predicate).
-template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL>
+template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool TAB>
 __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t start,
                                       const uint32_t (&vi)[U], const bool (&ok)[U],
-                                      int lp, int mask) {
+                                      int lp, int mask, int r0) {
   f4 x[NB][U];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const float* p = vptr32<DEEP>(a, b0 + b) + start;
+    const float* p = vptr32<TAB>(a, b0 + b) + start;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
@@ -262,24 +274,24 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       f4 v = x[b][u];
-      if constexpr (WEIGHTED) v = mul4s(v, vw<DEEP>(a, b0 + b));
+      if constexpr (WEIGHTED) v = mul4s(v, vw<TAB>(a, b0 + b));
       A.l0[u] = add4(A.l0[u], v);
     }
-    promote<U, DEEP>(A, b0 + b + 1, lp, mask);
+    promote<U, DEEP>(A, r0 + b0 + b + 1, lp, mask);
   }
 }
 
 // The last, partial batch (nb < NB clients): same issue-all-then-add shape,
 // every step guarded by a uniform (scalar) branch.
-template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL>
+template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool TAB>
 __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, int nb,
                                            int64_t start, const uint32_t (&vi)[U],
-                                           const bool (&ok)[U], int lp, int mask) {
+                                           const bool (&ok)[U], int lp, int mask, int r0) {
   f4 x[NB][U];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     if (b < nb) {
-      const float* p = vptr32<DEEP>(a, b0 + b) + start;
+      const float* p = vptr32<TAB>(a, b0 + b) + start;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
@@ -293,19 +305,25 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         f4 v = x[b][u];
-        if constexpr (WEIGHTED) v = mul4s(v, vw<DEEP>(a, b0 + b));
+        if constexpr (WEIGHTED) v = mul4s(v, vw<TAB>(a, b0 + b));
         A.l0[u] = add4(A.l0[u], v);
       }
-      promote<U, DEEP>(A, b0 + b + 1, lp, mask);
+      promote<U, DEEP>(A, r0 + b0 + b + 1, lp, mask);
     }
   }
 }
 
-template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, int POL>
+template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool CHAIN>
 __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
                                          int count) {
+  // TAB: the DEEP kernels' constant-space pointer table; a chain segment may
+  // be DEEP (n_total >= 256) with few local clients, so it takes the
+  // runtime-selected pointer source instead
+  constexpr bool TAB = DEEP && !CHAIN;
   const int n = a.n;
-  const int lp = level_power(n);
+  const int nt = CHAIN ? a.n_total : n;
+  const int r0 = CHAIN ? a.row0 : 0;
+  const int lp = level_power(nt);
   const int mask = (1 << lp) - 1;
   Acc<U, DEEP> A;
   uint32_t vi[U];
@@ -321,14 +339,48 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
     ok[u] = FULL || 4 * v < count;
     A.l0[u] = A.l1[u] = A.l2[u] = A.l3[u] = f4{0.f, 0.f, 0.f, 0.f};
   }
+  if constexpr (CHAIN) {
+    // the state after rows 0..row0-1 (levels outside lev_in are +0, exactly
+    // what the cascade holds there after its promotions)
+    if (a.st_in) {
+      const int li = a.lev_in;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        if (li & 1) A.l0[u] = ldg4<true>(a.st_in + start, vi[u]);
+        if (li & 2) A.l1[u] = ldg4<true>(a.st_in + a.plane + start, vi[u]);
+        if constexpr (DEEP) {
+          if (li & 4) A.l2[u] = ldg4<true>(a.st_in + 2 * a.plane + start, vi[u]);
+          if (li & 8) A.l3[u] = ldg4<true>(a.st_in + 3 * a.plane + start, vi[u]);
+        }
+      }
+    }
+  }
   int b0 = 0;
   for (; b0 + B <= n; b0 += B)
-    batch<U, B, FULL, DEEP, WEIGHTED, POL>(a, A, b0, start, vi, ok, lp, mask);
+    batch<U, B, FULL, DEEP, WEIGHTED, POL, TAB>(a, A, b0, start, vi, ok, lp, mask, r0);
   if (b0 < n)
-    batch_tail<U, B, FULL, DEEP, WEIGHTED, POL>(a, A, b0, n - b0, start, vi, ok, lp, mask);
+    batch_tail<U, B, FULL, DEEP, WEIGHTED, POL, TAB>(a, A, b0, n - b0, start, vi, ok, lp, mask,
+                                                     r0);
+  if constexpr (CHAIN) {
+    if (a.st_out) {
+      const int lo = a.lev_out;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        if (lo & 1) stg4<true>(a.st_out + start, vi[u], A.l0[u]);
+        if (lo & 2) stg4<true>(a.st_out + a.plane + start, vi[u], A.l1[u]);
+        if constexpr (DEEP) {
+          if (lo & 4) stg4<true>(a.st_out + 2 * a.plane + start, vi[u], A.l2[u]);
+          if (lo & 8) stg4<true>(a.st_out + 3 * a.plane + start, vi[u], A.l3[u]);
+        }
+      }
+      return;
+    }
+  }
 
   const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
-  const float fn = (float)n;
+  const float fn = (float)nt;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (!ok[u]) continue;
@@ -341,9 +393,9 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
     }
     const f4 r = sum_only ? s : div4s(s, fn);
     st_out<POL>(a.out32, start, vi[u], r);
-    if (a.flags & FA_F_BCAST) {
+    if (!CHAIN && (a.flags & FA_F_BCAST)) {
       for (int i = 0; i < n; ++i)
-        stg4<(POL & 2) != 0>(const_cast<float*>(vptr32<DEEP>(a, i)) + start, vi[u], r);
+        stg4<(POL & 2) != 0>(const_cast<float*>(vptr32<TAB>(a, i)) + start, vi[u], r);
     }
   }
 }
@@ -452,7 +504,7 @@ __device__ void tile_scalar(KArgs& a, Tile t) {
   }
 }
 
-template <int U, int B, bool DEEP, bool WEIGHTED, int POL>
+template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN>
 __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
   if (a.xcd_swz && ti >= a.nscalar) {
     // bijective: blocks i and i+8 share an XCD (round-robin dispatch); XCD x
@@ -463,24 +515,26 @@ __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
   }
   const Tile t = a.tiles[ti];
   if (t.kind == K_F32_VEC) {
-    if (t.count == 4 * U * kBlock) tile_vec<U, B, true, DEEP, WEIGHTED, POL>(a, t.start, t.count);
-    else tile_vec<U, B, false, DEEP, WEIGHTED, POL>(a, t.start, t.count);
-  } else {
+    if (t.count == 4 * U * kBlock)
+      tile_vec<U, B, true, DEEP, WEIGHTED, POL, CHAIN>(a, t.start, t.count);
+    else
+      tile_vec<U, B, false, DEEP, WEIGHTED, POL, CHAIN>(a, t.start, t.count);
+  } else if (!CHAIN) {
     tile_scalar<WEIGHTED>(a, t);
   }
 }
 
 // One workgroup per tile (default), or a persistent grid walking the table
 // with stride gridDim.x (tuning: FA_PLAN_TUNE_PERSIST).
-template <int U, int B, bool DEEP, bool WEIGHTED, int POL>
+template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN = false>
 __global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs args) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   if ((int)gridDim.x >= a.ntiles) {
-    run_tile<U, B, DEEP, WEIGHTED, POL>(a, blockIdx.x);
+    run_tile<U, B, DEEP, WEIGHTED, POL, CHAIN>(a, blockIdx.x);
   } else {
     for (int ti = blockIdx.x; ti < a.ntiles; ti += gridDim.x) {
-      run_tile<U, B, DEEP, WEIGHTED, POL>(a, ti);
+      run_tile<U, B, DEEP, WEIGHTED, POL, CHAIN>(a, ti);
       __syncthreads();  // scalar tiles exit threads early; keep the block in step
     }
   }
@@ -686,6 +740,21 @@ int check_segs(const fa_seg* s, int ns, int64_t numel, const char* what,
   return FA_OK;
 }
 
+// Every element belongs to at most one tile: two tiles over one element would
+// race two summation orders (and two stores) into the same output.
+int check_disjoint(std::vector<Tile> t, const char* who) {
+  std::sort(t.begin(), t.end(), [](const Tile& x, const Tile& y) {
+    const bool x64 = x.kind >= K_I64_CASC, y64 = y.kind >= K_I64_CASC;
+    return x64 != y64 ? y64 : x.start < y.start;
+  });
+  for (size_t i = 1; i < t.size(); ++i)
+    if ((t[i - 1].kind >= K_I64_CASC) == (t[i].kind >= K_I64_CASC) &&
+        t[i - 1].start + t[i - 1].count > t[i].start)
+      return set_err(FA_E_INVAL, "%s: tiles overlap at %s element %lld", who,
+                     t[i].kind >= K_I64_CASC ? "int64" : "fp32", (long long)t[i].start);
+  return FA_OK;
+}
+
 void push_scalar(std::vector<Tile>* t, int64_t start, int64_t count, int kind) {
   for (int64_t c = 0; c < count; c += kBlock)
     t->push_back(Tile{start + c, (int32_t)std::min<int64_t>(kBlock, count - c), kind});
@@ -707,6 +776,9 @@ int build_tiles(const std::vector<fa_seg>& s32, const std::vector<fa_seg>& s64, 
     const int64_t M = g.numel;
     if (M == 0) continue;
     if (M == 1) {
+      // the scalar breaks the run: a later aligned segment must not extend
+      // the open vector run across this element (it would be covered twice)
+      flush();
       push_scalar(&tail, g.offset, 1, K_F32_INNER);
       info->tail_elems += 1;
       continue;
@@ -740,6 +812,10 @@ int build_tiles(const std::vector<fa_seg>& s32, const std::vector<fa_seg>& s64, 
     if (b) push_scalar(&tail, g.offset, b, K_I64_CASC);
     if (b < M) push_scalar(&tail, g.offset + b, M - b, K_I64_ILP4);
   }
+  std::vector<Tile> all(vec);
+  all.insert(all.end(), tail.begin(), tail.end());
+  const int rc = check_disjoint(all, "tile planner");
+  if (rc) return rc;
   // Scalar tiles first: their few long-latency workgroups start early and
   // finish under the vector stream instead of trailing it.
   out->clear();
@@ -757,12 +833,32 @@ thread_local size_t t_dyn_lds = 0;  // tuning: occupancy cap through dynamic LDS
 
 thread_local int t_grid_cap = 0;     // tuning: persistent grid size
 
-template <int U, int B, bool DEEP, bool W, int POL>
+template <int U, int B, bool DEEP, bool W, int POL, bool CHAIN = false>
 hipError_t launch_one(const ReduceArgs& a, int ntiles, hipStream_t st) {
   const int grid = (t_grid_cap > 0 && t_grid_cap < ntiles) ? t_grid_cap : ntiles;
-  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, POL>), dim3(grid), dim3(kBlock), t_dyn_lds,
-                     st, a);
+  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, POL, CHAIN>), dim3(grid), dim3(kBlock),
+                     t_dyn_lds, st, a);
   return hipGetLastError();
+}
+
+// Chain segments (fa_reduce_chain): default cache policy, the plan's tile
+// width, 16-client batches for unweighted segments of >= 16 clients.
+template <int U, int B>
+hipError_t launch_chain_ub(const ReduceArgs& a, int ntiles, bool deep, bool w, hipStream_t st) {
+  if (deep) return w ? launch_one<U, B, true, true, 3, true>(a, ntiles, st)
+                     : launch_one<U, B, true, false, 3, true>(a, ntiles, st);
+  return w ? launch_one<U, B, false, true, 3, true>(a, ntiles, st)
+           : launch_one<U, B, false, false, 3, true>(a, ntiles, st);
+}
+hipError_t launch_chain(const ReduceArgs& a, int ntiles, int vec_u, hipStream_t st) {
+  const bool deep = a.n_total >= 256;
+  const bool w = a.flags & 0x100u;
+  t_dyn_lds = 0;
+  t_grid_cap = 0;
+  if (vec_u == 1) return launch_chain_ub<1, 8>(a, ntiles, deep, w, st);
+  if (vec_u == 4) return launch_chain_ub<4, 8>(a, ntiles, deep, w, st);
+  if (w || a.n < 16) return launch_chain_ub<2, 8>(a, ntiles, deep, w, st);
+  return launch_chain_ub<2, 16>(a, ntiles, deep, w, st);
 }
 
 
@@ -880,11 +976,19 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   p->vec_u = tile_elems / (4 * kBlock);
   p->flags = flags;
   std::vector<Tile> tiles, alt;
-  build_tiles(s32, s64, tile_elems, flags, &tiles, &p->info);
+  rc = build_tiles(s32, s64, tile_elems, flags, &tiles, &p->info);
+  if (rc) {
+    delete p;
+    return rc;
+  }
   set_kinds(p, tiles);
   if (autosel) {
     fa_plan_info ia{};
-    build_tiles(s32, s64, 4 * kBlock, flags, &alt, &ia);
+    rc = build_tiles(s32, s64, 4 * kBlock, flags, &alt, &ia);
+    if (rc) {
+      delete p;
+      return rc;
+    }
     p->ntiles_alt = (int)alt.size();
     p->nscalar_alt = ia.ntiles_tail;
   }
@@ -926,7 +1030,8 @@ int fa_plan_build_host(const fa_seg* seg32, int nseg32, int64_t f32_numel, const
   in.i64_numel = i64_numel;
   in.tile_elems = tile_elems;
   std::vector<Tile> t;
-  build_tiles(s32, s64, tile_elems, flags, &t, &in);
+  rc = build_tiles(s32, s64, tile_elems, flags, &t, &in);
+  if (rc) return rc;
   *info = in;
   if (tiles) {
     if (cap < (int)t.size())
@@ -975,6 +1080,8 @@ int fa_plan_create_from_tiles(const fa_tile_desc* tiles, int ntiles, int64_t f32
   t.clear();
   t.insert(t.end(), sc.begin(), sc.end());
   t.insert(t.end(), vec.begin(), vec.end());
+  const int rc = check_disjoint(t, "fa_plan_create_from_tiles");
+  if (rc) return rc;
   in.ntiles = (int32_t)t.size();
   in.ntiles_cascade = (int32_t)vec.size();
   in.ntiles_tail = (int32_t)sc.size();
@@ -1028,6 +1135,7 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
   a.out32 = out32;
   a.out64 = out64;
   a.n = n;
+  a.n_total = n;
   a.flags = flags | (weights ? 0x100u : 0u) |
             ((plan->flags & FA_PLAN_TUNE_WAVE_CONTIG) ? kWaveContig : 0u);
   const bool need32 = plan->has32, need64 = plan->has64;
@@ -1101,6 +1209,108 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
     if (e == hipSuccess) e = e2;
   }
   if (e != hipSuccess) return set_err(FA_E_HIP, "reduce launch: %s", hipGetErrorString(e));
+  return FA_OK;
+}
+
+unsigned fa_chain_levels(int rows, int n_total) {
+  if (rows <= 0 || n_total < 1) return 0;
+  const int lp = level_power(n_total);
+  const int step = 1 << lp;
+  unsigned m = 0;
+  if (rows % step) m |= 1u;                     // the open block
+  if ((rows >> lp) % step) m |= 2u;             // completed blocks since the last promotion
+  if (n_total >= 256) {                         // levels 2-3 exist (DEEP kernels)
+    if ((rows >> (2 * lp)) % step) m |= 4u;
+    if (rows >> (3 * lp)) m |= 8u;              // level 3 only accumulates
+  }
+  return m;
+}
+
+int fa_reduce_chain(const fa_plan* plan, const float* const* c32, int n, const float* weights,
+                    const fa_chain* ch, float* out32, unsigned flags, void* stream) {
+  if (!plan || !ch) return set_err(FA_E_INVAL, "fa_reduce_chain: plan/chain is NULL");
+  if (flags & ~FA_F_SUM_ONLY) return set_err(FA_E_INVAL, "fa_reduce_chain: bad flags");
+  const int nt = ch->n_total;
+  if (nt < 1 || nt > FA_MAX_CLIENTS)
+    return set_err(FA_E_RANGE, "fa_reduce_chain: n_total=%d outside 1..%d", nt, FA_MAX_CLIENTS);
+  if (n < 1 || ch->row0 < 0 || ch->row0 + n > nt)
+    return set_err(FA_E_INVAL, "fa_reduce_chain: rows [%d,+%d) outside the %d-row reduction",
+                   ch->row0, n, nt);
+  if (plan->has64 || plan->info.ntiles_tail > 0)
+    return set_err(FA_E_INVAL,
+                   "fa_reduce_chain: the plan holds scalar tiles (tails, M==1, int64); chain "
+                   "plans carry vector tiles only (scalar columns travel raw, fedagg_comm.h)");
+  const unsigned lin = fa_chain_levels(ch->row0, nt);
+  const unsigned lout = fa_chain_levels(ch->row0 + n, nt);
+  if (lin && !ch->state_in)
+    return set_err(FA_E_INVAL, "fa_reduce_chain: rows 0..%d-1 leave a state: state_in required",
+                   ch->row0);
+  if (!ch->state_out && !out32)
+    return set_err(FA_E_INVAL, "fa_reduce_chain: need state_out or out32");
+  if (ch->state_out && ch->row0 + n == nt)
+    return set_err(FA_E_INVAL, "fa_reduce_chain: the last segment finishes (state_out NULL)");
+  if (!ch->state_out && ch->row0 + n != nt)
+    return set_err(FA_E_INVAL, "fa_reduce_chain: only the last segment (rows ..%d) finishes",
+                   nt - 1);
+  const bool st = ch->state_in || ch->state_out;
+  if (st && (ch->plane < plan->info.f32_numel || ch->plane % 4))
+    return set_err(FA_E_INVAL, "fa_reduce_chain: plane=%lld must be >= %lld and a multiple of 4",
+                   (long long)ch->plane, (long long)plan->info.f32_numel);
+  if ((ch->state_in && !aligned16(ch->state_in)) || (ch->state_out && !aligned16(ch->state_out)) ||
+      (out32 && !aligned16(out32)))
+    return set_err(FA_E_ALIGN, "fa_reduce_chain: state/out buffers not 16-B aligned");
+  if (plan->info.ntiles == 0) return FA_OK;
+  if (!c32) return set_err(FA_E_INVAL, "fa_reduce_chain: fp32 buckets required");
+  for (int i = 0; i < n; ++i)
+    if (!c32[i] || !aligned16(c32[i]))
+      return set_err(FA_E_ALIGN, "fa_reduce_chain: client %d bucket NULL or not 16-B aligned", i);
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev != plan->device)
+    return set_err(FA_E_INVAL, "fa_reduce_chain: plan built on device %d, current device %d",
+                   plan->device, dev);
+  ReduceArgs a;
+  memset(&a, 0, sizeof a);
+  a.tiles = plan->d_tiles;
+  a.out32 = out32;
+  a.n = n;
+  a.n_total = nt;
+  a.row0 = ch->row0;
+  a.st_in = lin ? ch->state_in : nullptr;
+  a.st_out = ch->state_out;
+  a.lev_in = (int)lin;
+  a.lev_out = (int)lout;
+  a.plane = ch->plane;
+  a.flags = flags | (weights ? 0x100u : 0u);
+  a.ntiles = plan->info.ntiles;
+  hipStream_t s = (hipStream_t)stream;
+  void* table = nullptr;
+  if (n <= kInline) {
+    for (int i = 0; i < n; ++i) {
+      a.c32[i] = c32[i];
+      if (weights) a.w[i] = weights[i];
+    }
+  } else {
+    std::vector<char> host((size_t)n * 20);
+    const void** h32 = (const void**)host.data();
+    float* hw = (float*)(h32 + 2 * n);
+    for (int i = 0; i < n; ++i) {
+      h32[i] = c32[i];
+      h32[n + i] = nullptr;
+      hw[i] = weights ? weights[i] : 0.f;
+    }
+    HIP_TRY(hipMallocAsync(&table, host.size(), s));
+    HIP_TRY(hipMemcpyAsync(table, host.data(), host.size(), hipMemcpyHostToDevice, s));
+    a.tab32 = (const float* const*)table;
+    a.tab64 = (const int64_t* const*)((const void**)table + n);
+    a.tabw = (const float*)((const void**)table + 2 * n);
+  }
+  hipError_t e = launch_chain(a, a.ntiles, plan->vec_u, s);
+  if (table) {
+    hipError_t e2 = hipFreeAsync(table, s);
+    if (e == hipSuccess) e = e2;
+  }
+  if (e != hipSuccess) return set_err(FA_E_HIP, "chain launch: %s", hipGetErrorString(e));
   return FA_OK;
 }
 

@@ -93,7 +93,9 @@ class BucketLayout:
         self.segs64 = np.array([(s.offset, s.numel) for s in own if s.kind == KIND_I64],
                                np.int64).reshape(-1, 2)
         self.packed = [s for s in own if s.kind == KIND_PACKF]
-        self.signature = tuple((s.key, s.shape, str(s.dtype)) for s in self.slots)
+        # the alias map is part of the identity: a tied and an untied layout
+        # with the same keys bind modules differently (arena.py)
+        self.signature = tuple((s.key, s.shape, str(s.dtype), s.alias_of) for s in self.slots)
         self.keys = [s.key for s in self.slots]
 
     # ---------------------------------------------------------- builders --

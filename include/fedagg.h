@@ -154,6 +154,37 @@ int fa_reduce(const fa_plan *plan, const float *const *c32,
               const int64_t *const *c64, int n, const float *weights,
               float *out32, int64_t *out64, unsigned flags, void *stream);
 
+/* ---- chained segments: client shards reduced in the exact order ----------
+ * The cascade walks the N clients in slot order with four
+ * level accumulators; its state after rows 0..k-1 is those accumulators.
+ * fa_reduce_chain reduces rows row0..row0+n-1 of an n_total-row reduction:
+ * it starts from state_in (the state after rows 0..row0-1) and either writes
+ * the state after its last row to state_out, or — for the last segment —
+ * finishes into out32 (sum, then /n_total unless weighted or FA_F_SUM_ONLY).
+ * Segments chained in slot order reproduce fa_reduce over all n_total
+ * clients bit for bit, whatever the cut points (the state-carrying exact
+ * form of the client-sharded multi-GPU round, fedagg_comm.h).
+ *   state planes : level l lives at state + l*plane (element e at [e]);
+ *                  only the levels fa_chain_levels() reports are read or
+ *                  written — the others are +0 at that point of the order.
+ *                  state_in may equal state_out (in place).
+ *   plan         : vector (cascade) tiles only; the ILP-4 tail, M==1 and
+ *                  int64 columns of a layout are reduced by fa_reduce over
+ *                  all clients' raw values (they are a few hundred bytes).
+ * Equal weights as in fa_reduce (per local client, fp32). */
+typedef struct fa_chain {
+  int row0;              /* slot index of c32[0] in the whole reduction      */
+  int n_total;           /* clients in the whole reduction                   */
+  const float *state_in; /* state after rows 0..row0-1 (NULL when row0 == 0) */
+  float *state_out;      /* NULL: this is the last segment, finish to out32  */
+  int64_t plane;         /* floats per state plane (>= the plan's f32_numel) */
+} fa_chain;
+/* Bit l set: state plane l may be nonzero after `rows` of n_total rows. */
+unsigned fa_chain_levels(int rows, int n_total);
+int fa_reduce_chain(const fa_plan *plan, const float *const *c32, int n,
+                    const float *weights, const fa_chain *chain, float *out32,
+                    unsigned flags, void *stream);
+
 /* Stateless fp32 mean over segments (plan cached internally by layout). */
 int fa_mean_f32(const float *const *clients, int n, int64_t numel, float *out,
                 const fa_seg *segs, int nseg, void *stream);

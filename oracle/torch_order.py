@@ -82,6 +82,58 @@ def cascade(rows) -> np.ndarray:
     return acc[0]
 
 
+def cascade_state(rows, row0: int, n_total: int, acc=None):
+    """The cascade's four level accumulators after rows row0..row0+len-1 of
+    an ``n_total``-row ``multi_row_sum`` (``acc``: the state after rows
+    0..row0-1; None = the start, all +0).  Promotions happen after every
+    ``step``-th row of the WHOLE reduction, so chaining segments in slot order
+    and finishing with ``cascade_finish`` is ``cascade`` over all rows — the
+    order fa_reduce_chain reproduces (feddct_amd/csrc/fedagg.hip)."""
+    lp = level_power(n_total)
+    step = 1 << lp
+    mask = step - 1
+    shape = np.shape(rows[0]) if len(rows) else np.shape(acc[0])
+    acc = [np.zeros(shape, F32) for _ in range(4)] if acc is None else [a.copy() for a in acc]
+    for j in range(len(rows)):
+        i = row0 + j + 1
+        acc[0] = (acc[0] + rows[j]).astype(F32)
+        if i & mask:
+            continue
+        for lev in range(1, 4):
+            acc[lev] = (acc[lev] + acc[lev - 1]).astype(F32)
+            acc[lev - 1] = np.zeros(shape, F32)
+            if i & (mask << (lev * lp)):
+                break
+    return acc
+
+
+def cascade_finish(acc) -> np.ndarray:
+    out = acc[0]
+    for j in range(1, 4):
+        out = (out + acc[j]).astype(F32)
+    return out
+
+
+def chain_levels(rows: int, n_total: int) -> int:
+    """Bit l: level l of ``cascade_state`` may be nonzero after ``rows`` rows
+    (restates fa_chain_levels)."""
+    if rows <= 0:
+        return 0
+    lp = level_power(n_total)
+    step = 1 << lp
+    m = 0
+    if rows % step:
+        m |= 1
+    if (rows >> lp) % step:
+        m |= 2
+    if n_total >= 256:
+        if (rows >> (2 * lp)) % step:
+            m |= 4
+        if rows >> (3 * lp):
+            m |= 8
+    return m
+
+
 def ilp4(rows) -> np.ndarray:
     """ATen row_sum: rows viewed as (-1, 4); 4 interleaved cascades."""
     n = len(rows)

@@ -94,6 +94,35 @@ def test_stateless_plans_never_cover_gaps():
     assert np.array_equal(covered, want)
 
 
+def test_unit_tensor_between_vector_runs_is_covered_once():
+    """A 1-element fp32 key between two aligned keys (a scalar nn.Parameter,
+    PReLU's weight): with padding-gaps planning the vector run must stop
+    before it, or the element gets both the cascade and the inner order."""
+    lay = BucketLayout([("w", (64,), "float32"), ("s", (), "float32"),
+                        ("w2", (64,), "float32"), ("t", (37,), "float32"),
+                        ("u", (1,), "float32"), ("w3", (4, 32), "float32")])
+    info, tiles = _lib.build_tiles_host(lay.segs32, lay.f32_numel)
+    cover = np.zeros(lay.f32_numel, np.int64)
+    for s, c, k in tiles:
+        cover[s:s + c] += 1
+    assert cover.max() == 1
+    for o, M in lay.segs32:
+        assert (cover[o:o + M] == 1).all()
+    s_off = lay.by_key["s"].offset
+    kinds = [k for s, c, k in tiles if s <= s_off < s + c]
+    assert kinds == [3]
+
+
+def test_overlapping_tile_subsets_are_refused():
+    L = _lib.lib
+    arr = (_lib.FaTileDesc * 2)()
+    arr[0].start, arr[0].count, arr[0].kind = 0, 64, 0
+    arr[1].start, arr[1].count, arr[1].kind = 60, 1, 3
+    h = ctypes.c_void_p()
+    assert L.fa_plan_create_from_tiles(arr, 2, 128, 0, 0, 1, ctypes.byref(h)) == _lib.FA_E_INVAL
+    assert b"overlap" in L.fa_last_error()
+
+
 def test_norm_plan_host_errors():
     L = _lib.lib
     h = ctypes.c_void_p()

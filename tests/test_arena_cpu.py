@@ -57,9 +57,20 @@ def test_arena_errors_like_reference():
     with pytest.raises(RuntimeError, match="equal size"):
         ModuleArena(wrong, L)
     assert wrong[0].weight.data_ptr() == w0, "a failed bind must not touch the module"
+    # a client whose key dtype differs from the global's is staged like the
+    # reference's .float() (train_fedavg.py:145) instead of refused ...
     half = net().half()
-    with pytest.raises(TypeError):
-        ModuleArena(half, L)
+    ha = ModuleArena(half, L)
+    assert len(ha._packed) == 8   # every float key; the int64 one binds in place
+    ha.pack()
+    s = L.by_key["0.weight"]
+    assert torch.equal(ha.f32[s.offset:s.offset + s.numel].view(s.shape), half[0].weight.float())
+    # ... except a fractional value in an int64 key, which the int64 bucket
+    # cannot hold
+    fl = net()
+    fl[1].num_batches_tracked = torch.tensor(2.5)
+    with pytest.raises(TypeError, match="cannot be staged"):
+        ModuleArena(fl, L)
     bigger = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8),
                                  torch.nn.Linear(5, 2), torch.nn.Linear(2, 2))
     a = ModuleArena(bigger, L)
@@ -160,3 +171,58 @@ def test_c_helper_matches_python_checks():
     assert all(t._version > x for t, x in zip(a._written, v))
     with pytest.raises(TypeError):
         A._fa_shim.bump_versions((1,))
+
+
+def test_tied_layout_refuses_untied_client():
+    """the alias map is part of a layout's identity, and a client
+    whose tensors are not tied where the global's are is refused instead of
+    being silently tied."""
+    def tied():
+        m = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.Linear(4, 4))
+        m[1].weight = m[0].weight
+        return m
+    untied = torch.nn.Sequential(torch.nn.Linear(4, 4), torch.nn.Linear(4, 4))
+    Lt = BucketLayout.from_state_dict(tied().state_dict())
+    Lu = BucketLayout.from_state_dict(untied.state_dict())
+    assert Lt.by_key["1.weight"].alias_of == "0.weight"
+    assert Lt != Lu and Lt.signature != Lu.signature
+    w1 = untied[1].weight.detach().clone()
+    with pytest.raises(RuntimeError, match="tied"):
+        ModuleArena(untied, Lt)
+    assert torch.equal(untied[1].weight.detach(), w1)
+    t = tied()
+    a = ModuleArena(t, Lt)
+    assert t[0].weight is t[1].weight and a.valid()
+
+
+def test_pair_halves_keep_their_own_storage(tmp_path):
+    """a FedDCT slot (main + proxy) shares one bucket for the
+    launch, but each model's tensors sit in a storage of its own, so saving
+    one model's state_dict (train_feddct.py:455,463) writes only its bytes."""
+    import io
+    from feddct_amd.aggregate import _Pair
+    main = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 3), torch.nn.BatchNorm2d(4))
+    proxy = torch.nn.Sequential(torch.nn.Linear(300, 200), torch.nn.BatchNorm1d(200))
+    ref_main = {k: v.clone() for k, v in main.state_dict().items()}
+    pair = _Pair(main, proxy)
+    L = BucketLayout.from_state_dict(pair.state_dict())
+    a = ModuleArena(pair, L)
+    for m, pre in ((main, "0."), (proxy, "1.")):
+        own = BucketLayout.from_state_dict(m.state_dict())
+        stores = {(t.untyped_storage().data_ptr(), t.untyped_storage().nbytes())
+                  for t in m.state_dict().values()}
+        assert len(stores) == 2          # one fp32 + one int64 storage
+        assert sum(nb for _, nb in stores) <= 4 * own.f32_numel + 8 * own.i64_numel
+        for k, v in m.state_dict().items():   # still the pair bucket's memory
+            s = L.by_key[pre + k]
+            b = a.i64 if s.kind == "i64" else a.f32
+            assert v.data_ptr() == b[s.offset:].data_ptr()
+    for k, v in main.state_dict().items():
+        assert torch.equal(v, ref_main[k])
+    bm, bp = io.BytesIO(), io.BytesIO()
+    torch.save(main.state_dict(), bm)
+    torch.save(proxy.state_dict(), bp)
+    assert len(bm.getvalue()) < 8192 < len(bp.getvalue())
+    # writes through the pair bucket are seen by the halves
+    a.f32.fill_(1.5)
+    assert float(main[0].weight.detach().view(-1)[0]) == 1.5

@@ -54,3 +54,27 @@ def test_unbound_and_feddct_helpers(tmp_path):
     other = net(4)
     load_into(other, m.state_dict())
     assert torch.equal(other[0].weight, m[0].weight)
+
+
+def test_load_into_checks_slot_placement():
+    """a checkpoint whose fp32 tensors share one storage of the
+    bucket's size but are packed in another order must not be copied in
+    bulk (that would scramble the weights); load_state_dict's path takes it."""
+    m = net(5)
+    L = BucketLayout.from_state_dict(m.state_dict())
+    get_arena(m, L)
+    want = {k: v.clone() for k, v in net(6).state_dict().items()}
+    flat = torch.zeros(L.f32_numel)
+    sd, off = {}, 0
+    for s in reversed(L.slots):      # same total size, other placement
+        if s.kind == "f32":
+            flat[off:off + s.numel] = want[s.key].reshape(-1)
+            sd[s.key] = flat[off:off + s.numel].view(s.shape)
+            off += -(-s.numel // 64) * 64
+        else:
+            sd[s.key] = want[s.key]
+    sd = {k: sd[k] for k in L.keys}
+    assert sd[L.keys[0]].untyped_storage().nbytes() == L.f32_numel * 4
+    load_into(m, sd)
+    for k, v in want.items():
+        assert torch.equal(m.state_dict()[k], v), k

@@ -693,3 +693,26 @@ def test_shim_empty_and_unit_tensors():
         want = cpu[0].state_dict()[k].clone()
         want.copy_(ref)
         assert v.shape == want.shape and torch.equal(v.cpu(), want), k
+
+
+def test_unit_key_between_aligned_keys_n9():
+    """a 1-element fp32 key between two aligned keys (a scalar
+    nn.Parameter or PReLU weight) gets the inner order only, never also the
+    cascade of a vector run planned across it; n=9 makes the two orders
+    differ.  Through the shim against the reference's own expression."""
+    from feddct_amd.fedavg import server_aggregate
+    man = {"keys": [{"key": "w", "shape": [37], "dtype": "float32"},
+                    {"key": "s", "shape": [], "dtype": "float32"},
+                    {"key": "w2", "shape": [37], "dtype": "float32"},
+                    {"key": "a", "shape": [64], "dtype": "float32"},
+                    {"key": "p", "shape": [1], "dtype": "float32"},
+                    {"key": "b", "shape": [128], "dtype": "float32"}]}
+    n = 9
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    for rep in range(3):   # tile scheduling varies between launches
+        g = StateModule(man).to(DEV)
+        clients = _modules(man, states)
+        server_aggregate(g, clients)
+        torch.cuda.synchronize()
+        for (k, want), (k2, v) in zip(O.aggregate_state(states), g.state_dict().items()):
+            assert k == k2 and bits_equal(v.cpu().numpy(), want), (rep, k)

@@ -13,7 +13,7 @@ from conftest import ROOT
 LLVM = "/opt/rocm/lib/llvm/bin"
 LIBS = [os.path.join(ROOT, "feddct_amd", "libfedagg.so"),
         os.path.join(ROOT, "feddct_amd", "libfedagg_comm.so")]
-HOT = "_ZN12_GLOBAL__N_113reduce_kernelILi2ELi16ELb0ELb0ELi3EEEvNS_10ReduceArgsE"
+HOT = "_ZN12_GLOBAL__N_113reduce_kernelILi2ELi16ELb0ELb0ELi3ELb0EEEvNS_10ReduceArgsE"
 
 
 def _have_tools():
