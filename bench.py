@@ -52,25 +52,44 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def timed_launches(fn, steps, warmup, sync_group=None):
+def timed_launches(fn, steps, warmup, sync_group=None, per_launch=None):
+    """W untimed steps, then exactly K timed steps between two barriers and
+    device syncs; HIP events on the current stream bracket the K steps.
+    ``per_launch`` (a list): also an event between consecutive steps, so the
+    K per-step durations (which sum to the total) are reported — a clock ramp
+    shows up as a trend in them."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
     if sync_group is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
+    ev = [torch.cuda.Event(enable_timing=True)
+          for _ in range(steps + 1 if per_launch is not None else 2)]
     t0 = time.perf_counter()
-    e0.record()
-    for _ in range(steps):
+    ev[0].record()
+    for i in range(steps):
         fn()
-    e1.record()
+        if per_launch is not None:
+            ev[i + 1].record()
+    ev[-1].record()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     if sync_group is not None:
         dist.barrier()
-    return e0.elapsed_time(e1) / 1e3 / steps, wall / steps
+    if per_launch is not None:
+        per_launch[:] = [ev[i].elapsed_time(ev[i + 1]) / 1e3 for i in range(steps)]
+    return ev[0].elapsed_time(ev[-1]) / 1e3 / steps, wall / steps
+
+
+def launch_stats(ts):
+    """min / median / max / first / last of per-step seconds, in µs."""
+    if not ts:
+        return None
+    s = sorted(ts)
+    return {"min_us": round(s[0] * 1e6, 2), "median_us": round(s[len(s) // 2] * 1e6, 2),
+            "max_us": round(s[-1] * 1e6, 2), "first_us": round(ts[0] * 1e6, 2),
+            "last_us": round(ts[-1] * 1e6, 2), "n": len(ts)}
 
 
 def digest_of(layout, out32, out64, prefix=""):
@@ -133,7 +152,12 @@ def pmc_traffic(n_gpus):
 def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
     from oracle.torch_mirror import arithmetic_core, reference_loop, time_call
 
-    threads = min(16, os.cpu_count() or 1)
+    # every host core this process may run on, and the box's CPU share
+    # (OMP_NUM_THREADS, 16 per GPU on the pool); the faster is the baseline
+    all_cores = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", all_cores) or all_cores)
+    counts = sorted({max(1, min(share, all_cores)), all_cores})
+    threads = counts[0]
     torch.set_num_threads(threads)
 
     Holder = _holder_class(layout)
@@ -150,7 +174,14 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
 
     mods = [to_module(f, i) for f, i in clients]
     g = Holder()
-    t_loop, reps = time_call(lambda: reference_loop(g, mods), 5, budget_s * 0.5)
+    by_threads = {}
+    for th in counts:
+        torch.set_num_threads(th)
+        tl, rp = time_call(lambda: reference_loop(g, mods), 5, budget_s * 0.5 / len(counts))
+        by_threads[th] = (tl, rp)
+    threads = min(by_threads, key=lambda k: by_threads[k][0])
+    t_loop, reps = by_threads[threads]
+    torch.set_num_threads(threads)
     states = [m.state_dict() for m in mods]
     t_core, _ = time_call(lambda: arithmetic_core(states), 3, budget_s * 0.1)
     # BASELINE config 1's shape: the loop over 2 clients (beside bench's
@@ -181,7 +212,10 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
                            "loop_GBps": round(nbytes / t_loop1 / 1e9, 3), "runs": reps1},
             "cfg1_n2": {"loop_ms": round(t_cfg1 * 1e3, 2), "runs": reps_cfg1},
             "cfg3_feddct_n5": {"loop_ms": round(t_fd * 1e3, 2), "runs": reps_fd},
-            "host_cpus": os.cpu_count(), "cpu": _cpu_model()}
+            "loop_ms_by_threads": {str(k): round(v[0] * 1e3, 2) for k, v in by_threads.items()},
+            "threads_note": (f"torch intra-op threads: all {all_cores} cores of this process's "
+                             f"affinity and the box's CPU share ({share}); value = the faster"),
+            "host_cpus": os.cpu_count(), "affinity_cpus": all_cores, "cpu": _cpu_model()}
 
 
 def _cpu_model():
@@ -307,8 +341,13 @@ def other_configs(dev, steps=20):
             ok = True
             for names, prefixes, lay, n, _, o32, o64 in sets[0]:
                 for nm, pf in zip(names, prefixes):
-                    ok &= digest_of(lay, o32, o64, pf) == dig[digests[nm]]
-            out["bit_exact_vs_reference_digest"] = bool(ok)
+                    if digests[nm].startswith("weighted/"):
+                        ok &= weighted_digest_check(digests[nm][9:], lay, o32, o64)["bit_exact"]
+                    else:
+                        ok &= digest_of(lay, o32, o64, pf) == dig[digests[nm]]
+            out["bit_exact_vs_reference_digest" if not any(
+                d.startswith("weighted/") for d in digests.values())
+                else "bit_exact_vs_weighted_definition_digest"] = bool(ok)
         res[name] = out
 
     run("cfg3_feddct_c10_n5", [(("wrnsl16_8_sf4_c10_main", "wrnsl16_8_sf4_c10_proxy"), 5, None)], 2,
@@ -317,7 +356,7 @@ def other_configs(dev, steps=20):
     from feddct_amd.aggregate import client_weights as weights_from_sizes
     sizes = [2500 + 97 * ((7 * i) % 11) for i in range(20)]  # quantity-skewed shards
     run("cfg4_fedprox_c100_n20_weighted", [(("wrn16_8_c100",), 20, weights_from_sizes(sizes))],
-        1, {})
+        1, {"wrn16_8_c100": "weighted/wrn16_8_c100/n20/cfg4_sizes"})
     run("cfg5_feddct_c100_n24_one_gpu", [(("wrnsl16_8_sf4_c100_main", "wrnsl16_8_sf4_c100_proxy"),
                                           24, None)], 1,
         {"wrnsl16_8_sf4_c100_main": "feddct/wrnsl16_8_sf4_c100_main/n24",
@@ -325,13 +364,15 @@ def other_configs(dev, steps=20):
     return res
 
 
-def cfg5_sharded(dev, world, rank, group, steps, ncomm=None):
+def cfg5_sharded(dev, world, rank, group, steps, ncomm=None, chain_chunks=16):
     """BASELINE config 5 on the N GPUs of this run: FedDCT sf4 C100, 24 slots
     (main + proxy in one joint bucket), slots sharded contiguously over the
-    ranks (3 per GPU at N=8), global state to rank 0.  e1 (client shards +
-    chunked RCCL reduce) timed as a round; e2 (column stripes, P2P) timed and
-    its result checked bit-for-bit against the reference digests."""
-    from feddct_amd.dist import ShardedAggregator, StripedAggregator, shard_range
+    ranks (3 per GPU at N=8).  Timed as rounds: the chained exact round
+    (native and torch.distributed; result on the last rank), the striped
+    exact round (result on rank 0) and e1 (re-associated; rank 0).  Every
+    exact result is checked bit-for-bit against the reference's digests on
+    the rank that holds it."""
+    from feddct_amd.dist import ChainAggregator, ShardedAggregator, StripedAggregator, shard_range
     from feddct_amd.workload import joint_manifest
     with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
         dig = json.load(f)
@@ -346,38 +387,55 @@ def cfg5_sharded(dev, world, rank, group, steps, ncomm=None):
     o32 = torch.zeros(max(lay.f32_numel, 64), dtype=torch.float32, device=dev)
     o64 = torch.zeros(max(lay.i64_numel, 1), dtype=torch.int64, device=dev)
     nbytes = lay.algorithmic_bytes(n)
+    last = world - 1
 
     def tmax(fn, k, w):
         t, _ = timed_launches(fn, k, w, sync_group=group)
         tt = torch.tensor([t], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt.item())
-    agg = ShardedAggregator(lay, l32, l64, n, o32, o64, final="reduce")
-    t1 = tmax(agg.step, steps, 5)
-    s32, s64 = torch.zeros_like(o32), torch.zeros_like(o64)
-    sagg = StripedAggregator(lay, n, s32, s64, group=group, final="reduce")
-    t2 = tmax(lambda: sagg.step_device(l32, l64), max(2, steps // 10), 1)
-    out = {"slots": n, "slots_per_gpu": hi - lo, "algorithmic_bytes": nbytes,
-           "e1_ms": round(t1 * 1e3, 4), "e1_GBps": round(nbytes / t1 / 1e9, 2),
-           "e2_exact_ms": round(t2 * 1e3, 4), "e2_exact_GBps": round(nbytes / t2 / 1e9, 2)}
-    x32 = x64 = None
-    if ncomm is not None:  # the exact mode through the C ABI
-        from feddct_amd.comm import NativeStripedAggregator
-        x32, x64 = torch.zeros_like(o32), torch.zeros_like(o64)
-        xagg = NativeStripedAggregator(lay, l32, l64, n, x32, x64, ncomm, final="reduce")
-        t3 = tmax(xagg.step, max(2, steps // 4), 1)
-        out["e2_native_ms"] = round(t3 * 1e3, 4)
-        out["e2_native_GBps"] = round(nbytes / t3 / 1e9, 2)
-    if rank == 0:
-        ok = all(digest_of(lay, s32, s64, pf) == dig[f"feddct/{nm}/n24"]
-                 for nm, pf in zip(names, prefixes))
-        out["e2_bit_exact_vs_reference_digest"] = bool(ok)
-        if x32 is not None:
-            out["e2_native_bit_exact_vs_reference_digest"] = bool(all(
-                digest_of(lay, x32, x64, pf) == dig[f"feddct/{nm}/n24"]
-                for nm, pf in zip(names, prefixes)))
-        out["e1_max_abs_err_vs_exact"] = float((o32 - s32).abs().max())
-        out["e1_int64_bit_exact"] = bool(torch.equal(o64, s64))
+
+    def exact_on(r, b32, b64):
+        ok = [False]
+        if rank == r:
+            ok = [all(digest_of(lay, b32, b64, pf) == dig[f"feddct/{nm}/n24"]
+                      for nm, pf in zip(names, prefixes))]
+        dist.broadcast_object_list(ok, src=r, group=group)
+        return bool(ok[0])
+
+    out = {"slots": n, "slots_per_gpu": hi - lo, "algorithmic_bytes": nbytes}
+
+    def mode(name, make, root, k, exact):
+        try:
+            b32, b64 = torch.zeros_like(o32), torch.zeros_like(o64)
+            t = tmax(make(b32, b64), k, 2)
+            r = {"ms": round(t * 1e3, 4), "GBps": round(nbytes / t / 1e9, 2),
+                 "result_on": f"rank {root}"}
+            if exact:
+                r["bit_exact_vs_reference_digest"] = exact_on(root, b32, b64)
+            out[name] = r
+            return b32, b64
+        except Exception as e:  # noqa: BLE001
+            out[name] = {"error": repr(e)}
+            return None
+    if ncomm is not None:
+        from feddct_amd.comm import NativeChainedAggregator, NativeStripedAggregator
+        mode("chained_native", lambda b32, b64: NativeChainedAggregator(
+            lay, l32, l64, n, b32, b64, ncomm, nchunks=chain_chunks, final="reduce",
+            root=last).step, last, steps, True)
+        mode("e2_native", lambda b32, b64: NativeStripedAggregator(
+            lay, l32, l64, n, b32, b64, ncomm, final="reduce").step, 0, max(2, steps // 4), True)
+    mode("chained_torch_distributed", lambda b32, b64: (lambda a: lambda: a.step(l32, l64))(
+        ChainAggregator(lay, n, b32, b64, group=group, final="reduce", root=last,
+                        nchunks=chain_chunks)), last, max(2, steps // 2), True)
+    e2 = mode("e2_torch_distributed", lambda b32, b64: (lambda a: lambda: a.step_device(
+        l32, l64))(StripedAggregator(lay, n, b32, b64, group=group, final="reduce")), 0,
+        max(2, steps // 10), True)
+    e1 = mode("e1_torch_distributed", lambda b32, b64: ShardedAggregator(
+        lay, l32, l64, n, b32, b64, final="reduce").step, 0, steps, False)
+    if rank == 0 and e1 is not None and e2 is not None:
+        out["e1_torch_distributed"]["max_abs_err_vs_exact"] = float((e1[0] - e2[0]).abs().max())
+        out["e1_torch_distributed"]["int64_bit_exact"] = bool(torch.equal(e1[1], e2[1]))
     return out
 
 
@@ -708,12 +766,174 @@ def dropin_feddct_timing(dev, reps=20):
             "note": "cfg3 shape: 5 slots x (main + proxy), median wall incl. sync"}
 
 
+
+def weighted_digest_check(case, layout, o32, o64):
+    """The weighted launch's result against the committed digest of the
+    build's weighted definition (tests/golden/weighted_digests.json, made by
+    tests/golden/make_weighted_digests.py; the reference has no weights)."""
+    with open(os.path.join(ROOT, "tests", "golden", "weighted_digests.json")) as f:
+        want = json.load(f)[f"weighted/{case}"]["digest"]
+    return {"vs": "weighted definition digest (tests/golden/weighted_digests.json)",
+            "bit_exact": digest_of(layout, o32, o64) == want}
+
+
+def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, out64, reducer,
+              nbytes_rank, extra):
+    """N>1 (weak scaling: 20 client slots per GPU, slot order = rank order).
+    Every round form is timed over the same K steps (max over ranks):
+
+    * chained (exact client shards; native fa_reduce_chained and the
+      torch.distributed ChainAggregator): the shards stay put, the cascade
+      state hops rank to rank — the north_star's client-sharded partitioning
+      with the reference's bits; the global state lands on the last rank (the
+      chain's end; root = W-1: no extra transfer);
+    * striped e2 (exact column stripes; native and torch.distributed);
+    * sharded e1 (partial sums + RCCL reduce or reduce-scatter + gather to
+      rank 0; re-associated, NOT bit-exact: ULP histogram reported).
+
+    Every mode's result is compared with the exact single-GPU reduction of all
+    N·20 clients on rank 0; ``value`` is the fastest BIT-EXACT mode."""
+    from feddct_amd.dist import ChainAggregator, ShardedAggregator
+    n_total = N_CLIENTS * world
+    l32, l64 = [c[0] for c in clients], [c[1] for c in clients]
+    last = world - 1
+    modes = {}      # name -> {"t": s, "root": rank or -1, "out": (o32, o64), "exact_class": bool}
+
+    def tmax(fn, k, w):
+        t, _ = timed_launches(fn, k, w, sync_group=group)
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    def run_mode(name, make, root, exact_class, steps=None, warm=None):
+        log(f"[rank {rank}] {name}")
+        try:
+            o32, o64 = torch.full_like(out32, float("nan")), torch.zeros_like(out64)
+            fn = make(o32, o64)
+            t = tmax(fn, steps or args.steps, args.warmup if warm is None else warm)
+            modes[name] = {"t": t, "root": root, "out": (o32, o64), "exact_class": exact_class}
+        except Exception as e:  # noqa: BLE001  (reported in the line, every rank alike)
+            modes[name] = {"error": repr(e)}
+
+    ncomm = None
+    if not args.same_device:
+        try:
+            from feddct_amd.comm import Comm
+            ncomm = Comm.from_process_group(group)
+        except Exception as e:  # noqa: BLE001
+            extra["native_comm_error"] = repr(e)
+    if ncomm is not None:
+        from feddct_amd.comm import (FA_XCHG_RS_GATHER, NativeChainedAggregator,
+                                     NativeShardedAggregator, NativeStripedAggregator)
+        run_mode("chained/native", lambda o32, o64: NativeChainedAggregator(
+            layout, l32, l64, n_total, o32, o64, ncomm, nchunks=args.chain_chunks,
+            final="reduce", root=last).step, last, True)
+        run_mode("chained/native/allreduce", lambda o32, o64: NativeChainedAggregator(
+            layout, l32, l64, n_total, o32, o64, ncomm, nchunks=args.chain_chunks,
+            final="allreduce").step, -1, True, steps=max(5, args.steps // 2))
+        run_mode("e1/native/reduce", lambda o32, o64: NativeShardedAggregator(
+            layout, l32, l64, n_total, o32, o64, ncomm, nchunks=args.chunks,
+            final="reduce").step, 0, False)
+        run_mode("e1/native/rs_gather", lambda o32, o64: NativeShardedAggregator(
+            layout, l32, l64, n_total, o32, o64, ncomm, nchunks=args.chunks, final="reduce",
+            exchange=FA_XCHG_RS_GATHER).step, 0, False)
+        if not args.no_exact:
+            run_mode("e2/native", lambda o32, o64: NativeStripedAggregator(
+                layout, l32, l64, n_total, o32, o64, ncomm, final="reduce").step, 0, True,
+                steps=max(5, args.steps // 2))
+    run_mode("chained/torch.distributed", lambda o32, o64: (lambda a: lambda: a.step(l32, l64))(
+        ChainAggregator(layout, n_total, o32, o64, group=group, final="reduce", root=last,
+                        nchunks=args.chain_chunks)), last, True, steps=max(5, args.steps // 2))
+    run_mode("e1/torch.distributed", lambda o32, o64: ShardedAggregator(
+        layout, l32, l64, n_total, o32, o64, nchunks=args.chunks, final="reduce").step, 0, False)
+    striped_host = None
+    if not args.no_exact and not args.kernel_only:
+        try:
+            striped, striped_host, hbufs = exact_modes(
+                layout, manifest, clients, out32, out64, world, group, dev, nbytes_rank,
+                max(3, min(5, args.steps // 10)))
+            modes["e2/torch.distributed"] = {"t": striped["ms_per_step"] / 1e3, "root": 0,
+                                             "out": hbufs[0:2], "exact_class": True}
+        except Exception as e:  # noqa: BLE001
+            modes["e2/torch.distributed"] = {"error": repr(e)}
+    # kernel-only launch time for the roofline: this rank's 20-client reduce
+    kred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
+                   flags=_lib.FA_F_SUM_ONLY, plan=reducer.plan)
+    t_kernel, _ = timed_launches(kred, max(10, args.steps // 2), 3)
+
+    # parity of every mode on rank 0 (results on another rank travel there)
+    ex32 = ex64 = None
+    if rank == 0:
+        allc = make_clients(layout, manifest, range(n_total), dev)
+        ex32, ex64 = torch.zeros_like(out32), torch.zeros_like(out64)
+        Reducer(layout, allc, ex32, ex64)()
+        torch.cuda.synchronize()
+        del allc
+    report = {}
+    for name in sorted(modes):
+        m = modes[name]
+        if "error" in m:
+            report[name] = {"error": m["error"]}
+            continue
+        o32, o64 = m["out"]
+        src = 0 if m["root"] < 0 else m["root"]
+        if src != 0:
+            if rank == src:
+                dist.send(o32, 0, group=group)
+                dist.send(o64, 0, group=group)
+            elif rank == 0:
+                dist.recv(o32, src, group=group)
+                dist.recv(o64, src, group=group)
+        r = {"ms_per_step": round(m["t"] * 1e3, 4),
+             "GBps": round(nbytes_rank * world / m["t"] / 1e9, 2),
+             "result_on": "every rank" if m["root"] < 0 else f"rank {m['root']}"}
+        if rank == 0:
+            same = bool(torch.equal(o32.view(torch.int32), ex32.view(torch.int32))
+                        and torch.equal(o64, ex64))
+            r["bit_exact"] = same
+            if not same:
+                r["max_ulp_fp32"] = ulp_dist(o32, ex32)
+                r["ulp_histogram_fp32"] = ulp_hist(o32, ex32)
+                r["int64_bit_exact"] = bool(torch.equal(o64, ex64))
+        report[name] = r
+    # the headline: the fastest mode whose result is the reference's bits
+    # (decided on rank 0, shared so every rank agrees)
+    best_t, best = float("inf"), ""
+    if rank == 0:
+        for name, r in report.items():
+            if r.get("bit_exact") and modes[name]["t"] < best_t:
+                best_t, best = modes[name]["t"], name
+    sel = [best, best_t]
+    dist.broadcast_object_list(sel, src=0, group=group)
+    best, best_t = sel
+    if not best:   # no exact mode ran: report the exact class's fastest, flagged
+        cands = [n for n, m in modes.items() if "t" in m and m["exact_class"]]
+        best = min(cands, key=lambda n: modes[n]["t"]) if cands else min(
+            (n for n in modes if "t" in modes[n]), key=lambda n: modes[n]["t"])
+        best_t = modes[best]["t"]
+        extra["headline_not_verified_exact"] = True
+    extra["modes"] = report
+    extra["selected_mode"] = best
+    if striped_host is not None:
+        extra["exact_mode_host_ingress"] = striped_host
+    if not args.kernel_only:
+        log(f"[rank {rank}] config 5 sharded")
+        try:
+            extra["cfg5_feddct_c100_n24_sharded"] = cfg5_sharded(dev, world, rank, group,
+                                                                  max(10, args.steps // 2),
+                                                                  ncomm, args.chain_chunks)
+        except Exception as e:  # noqa: BLE001
+            extra["cfg5_feddct_c100_n24_sharded"] = {"error": repr(e)}
+    return best_t, t_kernel, ncomm
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--chunks", type=int, default=8)
+    ap.add_argument("--chain-chunks", type=int, default=16,
+                    help="N>1: column chunks of the chained round's state hops")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exact", action="store_true",
                     help="N>1: skip timing the column-striped exact mode")
@@ -759,16 +979,13 @@ def main():
     torch.cuda.synchronize()
 
     extra = {}
+    ncomm = None
     if world == 1:
-        t_step, wall = timed_launches(reducer, args.steps, args.warmup)
-        t_kernel = t_step
+        per = []
         if not args.kernel_only:
-            with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
-                want = json.load(f)[f"fedavg/{LAYOUT}/n{N_CLIENTS}"]
-            got = digest_of(layout, out32, out64)
-            extra["parity"] = {"vs": "reference server_aggregate SHA-256 (tests/golden)",
-                               "bit_exact": got == want}
-            # streaming-copy ceiling of this box (same 16-B nt load/store path)
+            # streaming work BEFORE the headline's own W warmups, so the
+            # timed steps do not see the clocks ramp: the copy ceiling of this
+            # box, the weighted and broadcast variants of the same reduction
             big = torch.empty(256 * 1024 * 1024, dtype=torch.float32, device=dev)  # 1 GiB
             big2 = torch.empty_like(big)
 
@@ -778,20 +995,33 @@ def main():
             tc, _ = timed_launches(copy_big, 20, 3)
             extra["copy_ceiling_GBps"] = round(2 * big.numel() * 4 / tc / 1e9, 1)
             del big, big2
-            extra["host_inclusive"] = host_inclusive(layout, clients, reducer, out32, out64)
             # weighted variant (client-size weights, BASELINE config 4's extension)
             from feddct_amd.aggregate import client_weights as weights_from_sizes
             w = weights_from_sizes(np.arange(1, N_CLIENTS + 1))
-            wred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
-                           weights=w, plan=reducer.plan)
-            tw, _ = timed_launches(wred, max(10, args.steps // 2), 3)
+            wo32, wo64 = torch.zeros_like(out32), torch.zeros_like(out64)
+            wred = Reducer(layout, clients, wo32, wo64, weights=w, plan=reducer.plan)
+            wper = []
+            tw, _ = timed_launches(wred, max(10, args.steps // 2), 3, per_launch=wper)
             extra["weighted_GBps"] = round(nbytes_rank / tw / 1e9, 1)
+            extra["weighted_launch"] = launch_stats(wper)
+            extra["weighted_parity"] = weighted_digest_check("wrn16_8_c10/n20/sizes_1_20",
+                                                             layout, wo32, wo64)
             # the round with its broadcast (FA_F_BCAST: reduce launch + broadcast
             # launch over the same tiles), N*B read + (N+1)*B written
             bred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
                            flags=_lib.FA_F_BCAST, plan=reducer.plan)
             tb, _ = timed_launches(bred, max(10, args.steps // 2), 3)
             extra["round_with_broadcast_us"] = round(tb * 1e6, 1)
+        t_step, wall = timed_launches(reducer, args.steps, args.warmup, per_launch=per)
+        t_kernel = t_step
+        extra["headline_launch"] = launch_stats(per)
+        if not args.kernel_only:
+            with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+                want = json.load(f)[f"fedavg/{LAYOUT}/n{N_CLIENTS}"]
+            got = digest_of(layout, out32, out64)
+            extra["parity"] = {"vs": "reference server_aggregate SHA-256 (tests/golden)",
+                               "bit_exact": got == want}
+            extra["host_inclusive"] = host_inclusive(layout, clients, reducer, out32, out64)
             extra["dropin"] = dropin_timing(layout, clients, dev)
             try:
                 extra["dropin_feddct_cfg3"] = dropin_feddct_timing(dev)
@@ -807,126 +1037,8 @@ def main():
             except Exception as e:  # noqa: BLE001
                 extra["cfg1_host_resident_n2"] = {"error": repr(e)}
     else:
-        from feddct_amd.dist import ShardedAggregator
-        log(f"[rank {rank}] e1 torch.distributed")
-        agg = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
-                                N_CLIENTS * world, out32, out64, nchunks=args.chunks,
-                                final="reduce")
-        t_step, wall = timed_launches(agg.step, args.steps, args.warmup, sync_group=group)
-        # the same round with the global state delivered to every GPU
-        # (extras are guarded: an error every rank hits alike is reported in
-        # the line instead of losing the headline)
-        a32, a64 = torch.zeros_like(out32), torch.zeros_like(out64)
-        try:
-            agg_all = ShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients],
-                                        N_CLIENTS * world, a32, a64, nchunks=args.chunks,
-                                        final="allreduce")
-            t_all, _ = timed_launches(agg_all.step, max(10, args.steps // 2), 5,
-                                      sync_group=group)
-            ta = torch.tensor([t_all], dtype=torch.float64, device=dev)
-            dist.all_reduce(ta, op=dist.ReduceOp.MAX)
-            extra["allreduce_mode"] = {
-                "mode": "client shards + RCCL all-reduce (global state on every GPU)",
-                "ms_per_step": round(float(ta.item()) * 1e3, 4),
-                "GBps": round(nbytes_rank * world / float(ta.item()) / 1e9, 2)}
-        except Exception as e:  # noqa: BLE001
-            extra["allreduce_mode"] = {"error": repr(e)}
-        # the same round through the native C ABI (libfedagg_comm.so: its own
-        # RCCL communicator, chunked ncclReduce on an internal stream), at
-        # several chunk counts; every variant is a complete round with the
-        # global state on rank 0, timed like the headline (K steps, max over
-        # ranks), and the headline takes the fastest implementation
-        log(f"[rank {rank}] e1 native")
-        n32 = n64 = None
-        ncomm = None
-        e1 = {f"torch.distributed/{args.chunks}chunks": None}
-        try:
-            if args.same_device:
-                # RCCL cannot place two ranks on one GPU; the rehearsal skips
-                # the native communicator (a real N>1 run never sets this)
-                raise RuntimeError("native comm skipped: --same-device rehearsal")
-            from feddct_amd.comm import Comm, NativeShardedAggregator
-            ncomm = Comm.from_process_group(group)
-            n32, n64 = torch.zeros_like(out32), torch.zeros_like(out64)
-            nat = {}
-            for nch in (4, 8, 16):
-                nagg = NativeShardedAggregator(layout, [c[0] for c in clients],
-                                               [c[1] for c in clients], N_CLIENTS * world, n32,
-                                               n64, ncomm, nchunks=nch, final="reduce")
-                t_nat, _ = timed_launches(nagg.step, args.steps, args.warmup, sync_group=group)
-                tn = torch.tensor([t_nat], dtype=torch.float64, device=dev)
-                dist.all_reduce(tn, op=dist.ReduceOp.MAX)
-                nat[nch] = float(tn.item())
-                del nagg
-            best = min(nat, key=nat.get)
-            extra["native_mode"] = {
-                "mode": "C ABI fa_reduce_sharded: client shards + chunked ncclReduce to rank 0",
-                "ms_per_step_by_chunks": {str(k): round(v * 1e3, 4) for k, v in nat.items()},
-                "ms_per_step": round(nat[best] * 1e3, 4), "chunks": best,
-                "GBps": round(nbytes_rank * world / nat[best] / 1e9, 2)}
-            for k, v in nat.items():
-                e1[f"native/{k}chunks"] = v
-        except Exception as e:  # noqa: BLE001
-            extra["native_mode"] = {"error": repr(e)}
-            n32 = None
-        # kernel-only launch time for the roofline: the same reduce over this
-        # rank's clients into scratch outputs (out32/out64 hold the round's result)
-        kred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
-                       flags=_lib.FA_F_SUM_ONLY, plan=reducer.plan)
-        t_kernel, _ = timed_launches(kred, max(10, args.steps // 2), 3)
-        tt = torch.tensor([t_step], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_step = float(tt.item())
-        e1[f"torch.distributed/{args.chunks}chunks"] = t_step
-        e1_best = min(e1, key=e1.get)
-        t_step = e1[e1_best]
-        extra["e1_implementations_ms"] = {k: round(v * 1e3, 4) for k, v in e1.items()}
-        extra["e1_selected"] = e1_best
-        if not args.kernel_only:
-            log(f"[rank {rank}] config 5 sharded")
-            try:
-                extra["cfg5_feddct_c100_n24_sharded"] = cfg5_sharded(dev, world, rank, group,
-                                                                      max(10, args.steps // 2),
-                                                                      ncomm)
-            except Exception as e:  # noqa: BLE001
-                extra["cfg5_feddct_c100_n24_sharded"] = {"error": repr(e)}
-        # the exact (column-striped) mode on the same client placement
-        striped = striped_host = None
-        if not args.kernel_only and not args.no_exact:
-            log(f"[rank {rank}] exact modes")
-            try:
-                striped, striped_host, (s32, s64, h32, h64, x32, x64) = exact_modes(
-                    layout, manifest, clients, out32, out64, world, group, dev, nbytes_rank,
-                    max(3, min(5, args.steps // 10)), ncomm)
-            except Exception as e:  # noqa: BLE001
-                extra["exact_mode"] = {"error": repr(e)}
-        if rank == 0 and not args.kernel_only:
-            # accuracy of the re-associated cross-GPU sum vs the exact order
-            allc = make_clients(layout, manifest, range(N_CLIENTS * world), dev)
-            ex32 = torch.zeros_like(out32)
-            ex64 = torch.zeros_like(out64)
-            Reducer(layout, allc, ex32, ex64)()
-            torch.cuda.synchronize()
-            extra["parity"] = {"vs": f"exact single-GPU torch order over {N_CLIENTS * world} clients",
-                               "max_ulp_fp32": ulp_dist(out32, ex32),
-                               "ulp_histogram_fp32": ulp_hist(out32, ex32),
-                               "max_abs_err_fp32": float((out32 - ex32).abs().max()),
-                               "int64_bit_exact": bool(torch.equal(out64, ex64)),
-                               "allreduce_mode_same_as_reduce_mode": bool(torch.equal(a32, out32))}
-            if n32 is not None and "error" not in extra.get("native_mode", {}):
-                extra["native_mode"]["max_ulp_fp32_vs_exact"] = ulp_dist(n32, ex32)
-                extra["native_mode"]["ulp_histogram_fp32"] = ulp_hist(n32, ex32)
-                extra["native_mode"]["int64_bit_exact"] = bool(torch.equal(n64, ex64))
-            if striped is not None:
-                striped["bit_exact"] = bool(torch.equal(s32, ex32) and torch.equal(s64, ex64))
-                if x32 is not None:
-                    striped["native"]["bit_exact"] = bool(torch.equal(x32, ex32)
-                                                          and torch.equal(x64, ex64))
-                extra["exact_mode"] = striped
-            if striped_host is not None:
-                striped_host["bit_exact"] = bool(torch.equal(h32, ex32) and torch.equal(h64, ex64))
-                extra["exact_mode_host_ingress"] = striped_host
-            del allc
+        t_step, t_kernel, ncomm = multi_gpu(args, world, rank, dev, group, layout, manifest,
+                                            clients, out32, out64, reducer, nbytes_rank, extra)
 
     achieved = nbytes_rank / t_kernel / 1e9
     traffic = pmc_traffic(world)
@@ -947,8 +1059,8 @@ def main():
                                "(82 fp32 + 16 int64 keys), unweighted mean (reference semantics)",
                    "clients_per_gpu": N_CLIENTS, "bytes_per_client": layout.state_bytes(),
                    "algorithmic_bytes_per_step": nbytes_rank * world,
-                   "parallelism": (f"client-shard x{world}, chunked RCCL reduce to rank 0 "
-                                   f"({extra.get('e1_selected')})"
+                   "parallelism": (f"client shards x{world}: {extra.get('selected_mode')} "
+                                   "(fastest bit-exact round form; all forms in 'modes')"
                                    if world > 1 else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

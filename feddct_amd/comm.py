@@ -29,11 +29,29 @@ FA_E_COMM = -6
 FA_COMM_UID_BYTES = 128
 
 COMM_EXPORTS = ["fa_comm_unique_id", "fa_comm_init_rank", "fa_comm_init", "fa_comm_destroy",
-                "fa_comm_info", "fa_shard_plan_create", "fa_shard_plan_destroy",
-                "fa_reduce_sharded", "fa_mean_f32_multi", "fa_stripe_plan_create",
-                "fa_stripe_plan_destroy", "fa_reduce_striped"]
+                "fa_comm_info", "fa_shard_plan_create", "fa_shard_plan_create_ex",
+                "fa_shard_plan_destroy", "fa_reduce_sharded", "fa_mean_f32_multi",
+                "fa_stripe_plan_create", "fa_stripe_plan_destroy", "fa_reduce_striped",
+                "fa_chain_plan_create", "fa_chain_plan_destroy", "fa_reduce_chained",
+                "fa_describe_round"]
+
+FA_XCHG_REDUCE, FA_XCHG_RS_GATHER = 0, 1
+FA_MODE_SHARDED, FA_MODE_STRIPED, FA_MODE_CHAINED = 0, 1, 2
+X = dict(SEND=1, RECV=2, REDUCE=3, ALLREDUCE=4, REDUCE_SCATTER=5, GATHER=6, ALLGATHER=7, BCAST=8,
+         K_SUM=16, K_ZERO=17, K_DIV=18, K_COPY=19, K_STRIPE=20, K_CHAIN=21, K_STACK=22,
+         K_TAILS=23)
+B = dict(NONE=0, CLIENT=1, OUT=2, PARTIAL=4, RECV=5, STRIPE=6, STATE=7, FIN=8, STACK=9, GATHER=10)
+XNAME = {v: k for k, v in X.items()}
+BNAME = {v: k for k, v in B.items()}
 
 _P, _I, _I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+
+
+class FaXfer(ctypes.Structure):
+    _fields_ = [("step", ctypes.c_int32), ("op", ctypes.c_int32), ("peer", ctypes.c_int32),
+                ("chunk", ctypes.c_int32), ("src", ctypes.c_int32), ("src_index", ctypes.c_int32),
+                ("dst", ctypes.c_int32), ("dst_index", ctypes.c_int32), ("offset", ctypes.c_int64),
+                ("count", ctypes.c_int64), ("row0", ctypes.c_int32), ("nrows", ctypes.c_int32)]
 
 
 class FaShardIO(ctypes.Structure):
@@ -61,6 +79,15 @@ def _load():
                                   ctypes.c_uint, ctypes.POINTER(_P)],
         "fa_stripe_plan_destroy": [_P],
         "fa_reduce_striped": [ctypes.POINTER(_P), _I, ctypes.POINTER(FaShardIO), _I],
+        "fa_shard_plan_create_ex": [_P, _P, _I, _I64, _P, _I, _I64, ctypes.POINTER(_I), _I, _I,
+                                    ctypes.c_uint, ctypes.POINTER(_P)],
+        "fa_chain_plan_create": [_P, _P, _I, _I64, _P, _I, _I64, ctypes.POINTER(_I), _I,
+                                 ctypes.c_uint, ctypes.POINTER(_P)],
+        "fa_chain_plan_destroy": [_P],
+        "fa_reduce_chained": [ctypes.POINTER(_P), _I, ctypes.POINTER(FaShardIO), _I],
+        "fa_describe_round": [_I, _I, _I, ctypes.POINTER(_I), _P, _I, _I64, _P, _I, _I64, _I, _I,
+                              ctypes.c_uint, _I, _I, ctypes.POINTER(FaXfer), _I,
+                              ctypes.POINTER(_I)],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -83,6 +110,38 @@ def unique_id() -> bytes:
     buf = ctypes.create_string_buffer(FA_COMM_UID_BYTES)
     _lib.check(lib().fa_comm_unique_id(buf, FA_COMM_UID_BYTES), "fa_comm_unique_id")
     return buf.raw
+
+
+def _segs(layout: BucketLayout):
+    a32, n32 = _lib.seg_array(layout.segs32 if len(layout.segs32) else np.zeros((0, 2), np.int64))
+    a64, n64 = _lib.seg_array(layout.segs64 if len(layout.segs64) else np.zeros((0, 2), np.int64))
+    return a32, n32, a64, n64
+
+
+def describe(mode: int, layout: BucketLayout, counts: Sequence[int], rank: int,
+             nchunks: int = 8, exchange: int = FA_XCHG_REDUCE, root: int = 0,
+             weighted: bool = False) -> List[dict]:
+    """Rank ``rank``'s schedule of one round (fa_describe_round): the exact
+    list of exchanges and kernels the native executor issues, computed on the
+    host (no GPU, no communicator)."""
+    a32, n32, a64, n64 = _segs(layout)
+    c = (_I * len(counts))(*map(int, counts))
+    n = _I()
+    args = (mode, len(counts), rank, c, a32, n32, int(layout.f32_numel), a64, n64,
+            int(layout.i64_numel), int(nchunks), int(exchange), _lib.FA_PLAN_GAPS_ARE_PADDING,
+            int(root), int(bool(weighted)))
+    _lib.check(lib().fa_describe_round(*args, None, 0, ctypes.byref(n)), "fa_describe_round")
+    arr = (FaXfer * max(1, n.value))()
+    _lib.check(lib().fa_describe_round(*args, arr, n.value, ctypes.byref(n)), "fa_describe_round")
+    out = []
+    for i in range(n.value):
+        x = arr[i]
+        d = {f: getattr(x, f) for f, _ in FaXfer._fields_}
+        d["op"] = XNAME.get(d["op"], d["op"])
+        d["src"] = BNAME.get(d["src"], d["src"])
+        d["dst"] = BNAME.get(d["dst"], d["dst"])
+        out.append(d)
+    return out
 
 
 class Comm:
@@ -140,17 +199,14 @@ class ShardPlan:
     """This rank's shard plan for a layout (chunk subplans + scratch)."""
 
     def __init__(self, comm: Comm, layout: BucketLayout, counts: Sequence[int],
-                 nchunks: int = 8):
-        a32, n32 = _lib.seg_array(layout.segs32 if len(layout.segs32)
-                                  else np.zeros((0, 2), np.int64))
-        a64, n64 = _lib.seg_array(layout.segs64 if len(layout.segs64)
-                                  else np.zeros((0, 2), np.int64))
+                 nchunks: int = 8, exchange: int = FA_XCHG_REDUCE):
+        a32, n32, a64, n64 = _segs(layout)
         c = (_I * len(counts))(*map(int, counts))
         h = _P()
-        _lib.check(lib().fa_shard_plan_create(comm.handle, a32, n32, int(layout.f32_numel), a64,
-                                              n64, int(layout.i64_numel), c, int(nchunks),
-                                              _lib.FA_PLAN_GAPS_ARE_PADDING, ctypes.byref(h)),
-                   "fa_shard_plan_create")
+        _lib.check(lib().fa_shard_plan_create_ex(comm.handle, a32, n32, int(layout.f32_numel),
+                                                 a64, n64, int(layout.i64_numel), c, int(nchunks),
+                                                 int(exchange), _lib.FA_PLAN_GAPS_ARE_PADDING,
+                                                 ctypes.byref(h)), "fa_shard_plan_create")
         self.handle = h
         self.comm = comm  # the plan must not outlive its communicator
 
@@ -175,14 +231,15 @@ class NativeShardedAggregator:
     def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
                  local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
                  out64: torch.Tensor, comm: Comm, nchunks: int = 8, final: str = "reduce",
-                 root: int = 0, weights: Optional[Sequence[float]] = None):
+                 root: int = 0, weights: Optional[Sequence[float]] = None,
+                 exchange: int = FA_XCHG_REDUCE):
         if final not in ("reduce", "allreduce"):
             raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
         world, rank, _ = comm.info()
         counts = [b - a for a, b in (shard_range(n_total, world, r) for r in range(world))]
         if len(local32) != counts[rank]:
             raise ValueError(f"rank {rank} holds {len(local32)} clients, shard is {counts[rank]}")
-        self.plan = ShardPlan(comm, layout, counts, nchunks)
+        self.plan = ShardPlan(comm, layout, counts, nchunks, exchange)
         self.root = root if final == "reduce" else -1
         self._a32 = _lib.ptr_array([t.data_ptr() for t in local32])
         self._a64 = _lib.ptr_array([t.data_ptr() for t in local64])
@@ -209,10 +266,7 @@ class StripePlan:
     receive rows, int64 gather buffers)."""
 
     def __init__(self, comm: Comm, layout: BucketLayout, counts: Sequence[int]):
-        a32, n32 = _lib.seg_array(layout.segs32 if len(layout.segs32)
-                                  else np.zeros((0, 2), np.int64))
-        a64, n64 = _lib.seg_array(layout.segs64 if len(layout.segs64)
-                                  else np.zeros((0, 2), np.int64))
+        a32, n32, a64, n64 = _segs(layout)
         c = (_I * len(counts))(*map(int, counts))
         h = _P()
         _lib.check(lib().fa_stripe_plan_create(comm.handle, a32, n32, int(layout.f32_numel), a64,
@@ -265,3 +319,70 @@ class NativeStripedAggregator(NativeShardedAggregator):
         self.io.stream = s
         _lib.check(lib().fa_reduce_striped(self._plans, 1, ctypes.byref(self.io), self.root),
                    "fa_reduce_striped")
+
+
+class ChainPlan:
+    """This rank's chained-mode plan (vector-tile chunk plans, the state
+    planes, the raw scalar-column gather buffers)."""
+
+    def __init__(self, comm: Comm, layout: BucketLayout, counts: Sequence[int],
+                 nchunks: int = 16):
+        a32, n32, a64, n64 = _segs(layout)
+        c = (_I * len(counts))(*map(int, counts))
+        h = _P()
+        _lib.check(lib().fa_chain_plan_create(comm.handle, a32, n32, int(layout.f32_numel), a64,
+                                              n64, int(layout.i64_numel), c, int(nchunks),
+                                              _lib.FA_PLAN_GAPS_ARE_PADDING, ctypes.byref(h)),
+                   "fa_chain_plan_create")
+        self.handle = h
+        self.comm = comm
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                lib().fa_chain_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+class NativeChainedAggregator(NativeShardedAggregator):
+    """The exact client-sharded round (fa_reduce_chained): the shards stay
+    where they are and the cascade state travels rank to rank in slot order
+    (train_feddct.py:42-50's order over all slots).  ``final="reduce"``: the
+    result lands on ``root`` (cheapest when root is the last rank holding
+    clients); ``"allreduce"``: on every rank."""
+
+    def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
+                 local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
+                 out64: torch.Tensor, comm: Comm, nchunks: int = 16, final: str = "reduce",
+                 root: int = 0, weights: Optional[Sequence[float]] = None,
+                 counts: Optional[Sequence[int]] = None):
+        if final not in ("reduce", "allreduce"):
+            raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
+        world, rank, _ = comm.info()
+        if counts is None:
+            counts = [b - a for a, b in (shard_range(n_total, world, r) for r in range(world))]
+        if len(local32) != counts[rank] or sum(counts) != n_total:
+            raise ValueError(f"rank {rank} holds {len(local32)} clients, shard is {counts[rank]}")
+        self.plan = ChainPlan(comm, layout, counts, nchunks)
+        self.root = root if final == "reduce" else -1
+        self._a32 = _lib.ptr_array([t.data_ptr() for t in local32])
+        self._a64 = _lib.ptr_array([t.data_ptr() for t in local64])
+        self._w = (None if weights is None
+                   else (ctypes.c_float * max(1, len(weights)))(*map(float, weights)))
+        self._plans = (_P * 1)(self.plan.handle.value)
+        self.io = FaShardIO()
+        self.io.c32 = ctypes.cast(self._a32, _P)
+        self.io.c64 = ctypes.cast(self._a64, _P) if layout.i64_numel else None
+        self.io.weights = ctypes.cast(self._w, _P) if self._w is not None else None
+        self.io.out32 = out32.data_ptr()
+        self.io.out64 = out64.data_ptr() if layout.i64_numel else None
+        self._keep = (local32, local64, out32, out64)
+
+    def step(self, stream=None) -> None:
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self.io.stream = s
+        _lib.check(lib().fa_reduce_chained(self._plans, 1, ctypes.byref(self.io), self.root),
+                   "fa_reduce_chained")

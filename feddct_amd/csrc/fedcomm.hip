@@ -3,16 +3,31 @@
 //
 // Layering: this library uses only libfedagg.so's public ABI for the
 // arithmetic (fa_plan_build_host to enumerate the layout's tiles,
-// fa_plan_create_from_tiles for tile subsets, fa_reduce for the reductions,
-// fa_div_f32 for the /N finish) and adds the exchanges:
-//   e1 (fa_reduce_sharded): one ncclReduce / ncclAllReduce per column chunk
-//      on an internal communication stream, issued as soon as the kernel
-//      over that chunk is done, so the exchange of chunk c overlaps the
-//      reduction of chunk c+1;
-//   e2 (fa_reduce_striped): grouped ncclSend/ncclRecv move every client's
-//      values for rank r's column stripe to rank r, which reduces its stripe
-//      over all clients in the exact order; the stripes then travel to the
-//      root (or to every rank).  Bit-identical to one GPU.
+// fa_plan_create_from_tiles for tile subsets, fa_reduce / fa_reduce_chain for
+// the reductions, fa_div_f32 for the /N finish) and adds the exchanges.
+//
+// Every round is a SCHEDULE: a host-built list of operations per rank
+// (fa_xfer: sends, receives, collectives, kernels), built by pure host code
+// from the layout, the shard counts and the rank — the same list
+// fa_describe_round returns without a GPU, so the multi-rank schedules are
+// testable on a CPU (tests/test_schedule.py replays all ranks' lists with the
+// oracle as the arithmetic).  The executor walks the list: the comm ops of
+// one step form one RCCL group, on the plan's communication stream; kernels
+// that read exchanged data run there too, the others on the caller's stream
+// (event-joined), so a rank's arithmetic overlaps its exchanges.
+//   e1 sharded (fa_reduce_sharded): per column chunk, the partial sum of the
+//      rank's clients, then ncclReduce / ncclAllReduce — or ncclReduceScatter
+//      (in place) + ncclGather / ncclAllGather, spreading the exchange over
+//      every link — and the /N; re-associates the cross-rank sum;
+//   e2 striped (fa_reduce_striped): pairwise rounds of grouped sends and
+//      receives move every client's values for rank r's column stripe to
+//      rank r, which reduces it over all clients; the stripes then travel to
+//      the result ranks.  Bit-identical to one GPU;
+//   chained (fa_reduce_chained): the client shards stay put; the cascade's
+//      accumulator state (fa_reduce_chain) travels rank to rank in slot order,
+//      chunk by chunk, so chunk c's hop overlaps chunk c+1's reduction; the
+//      scalar columns (ILP-4 tails, M==1, int64) are all-gathered raw.
+//      Bit-identical to one GPU.
 // RCCL resolves to the librccl.so.1 torch has already loaded (same soname),
 // so a process holds one RCCL.
 
@@ -32,6 +47,7 @@
 #include "common.h"
 
 static_assert(sizeof(ncclUniqueId) == FA_COMM_UID_BYTES, "unique id size");
+static_assert(sizeof(fa_xfer) == 56, "fa_xfer is 56 B");
 
 using fa::set_err;
 
@@ -50,78 +66,113 @@ struct fa_comm {
 
 namespace {
 
-// ------------------------------------------------------------ int64 keys --
-// The int64 keys (num_batches_tracked) are a few bytes per client: every
-// rank's buckets are stacked into rows, all-gathered raw, and the result
-// ranks reduce all n_total rows exactly (slot order = rank order).
+// ------------------------------------------------------------ small kernels --
+// Stacks of the scalar columns: local client j's values at idx[0..width) as
+// row j (fp32: times the client's weight when weighted, the product rounded
+// exactly as the weighted kernel rounds it, so the root can reduce the rows
+// unweighted with FA_F_SUM_ONLY and get the weighted order's bits).
 constexpr int kStackPtrs = 64;
 struct StackArgs {
-  const int64_t* src[kStackPtrs];
-  int64_t* dst;
+  const void* src[kStackPtrs];
+  float w[kStackPtrs];
+  void* dst;
+  const int64_t* idx;  // fp32 tails: bucket index of each column (NULL: 0..width)
   int64_t width;
+  int64_t stride;      // row stride of dst (elements)
   int rows;
+  int weighted;
 };
 __global__ void stack_i64_kernel(StackArgs a) {
   const int r = blockIdx.y;
   if (r >= a.rows) return;
+  const int64_t* s = (const int64_t*)a.src[r];
+  int64_t* d = (int64_t*)a.dst + r * a.stride;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < a.width;
        e += (int64_t)gridDim.x * blockDim.x)
-    a.dst[r * a.width + e] = a.src[r][e];
+    d[e] = s[e];
+}
+__global__ void stack_f32_kernel(StackArgs a) {
+  const int r = blockIdx.y;
+  if (r >= a.rows) return;
+  const float* s = (const float*)a.src[r];
+  float* d = (float*)a.dst + r * a.stride;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < a.width;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const float x = s[a.idx[e]];
+    d[e] = a.weighted ? __fmul_rn(x, a.w[r]) : x;
+  }
+}
+__global__ void scatter_f32_kernel(const float* __restrict__ src, const int64_t* __restrict__ idx,
+                                   float* __restrict__ dst, int64_t width) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < width;
+       e += (int64_t)gridDim.x * blockDim.x)
+    dst[idx[e]] = src[e];
 }
 
-struct I64Part {
-  fa_plan* plan = nullptr;  // the int64 tiles (nullptr: no int64 keys)
-  int64_t* stack = nullptr;   // nmax rows of width
-  int64_t* gather = nullptr;  // nranks * nmax rows
-  std::vector<const int64_t*> rows;  // the n_total real rows, slot order
-  int nmax = 0;
-  int64_t width = 0;
-
-  int init(const fa_comm* c, const std::vector<fa_tile_desc>& t64, const int* counts,
-           int64_t f32_numel, int64_t i64_numel, unsigned flags) {
-    if (t64.empty()) return FA_OK;
-    int rc = fa_plan_create_from_tiles(t64.data(), (int)t64.size(), f32_numel, i64_numel, 0,
-                                       flags, &plan);
-    if (rc) return rc;
-    width = i64_numel;
-    for (int r = 0; r < c->nranks; ++r) nmax = std::max(nmax, counts[r]);
-    const size_t row = (size_t)width * 8;
-    FA_HIP_TRY(hipMalloc(&stack, std::max<size_t>(1, (size_t)nmax * row)));
-    FA_HIP_TRY(hipMalloc(&gather, std::max<size_t>(1, (size_t)nmax * c->nranks * row)));
-    for (int r = 0; r < c->nranks; ++r)
-      for (int j = 0; j < counts[r]; ++j)
-        rows.push_back(gather + ((size_t)r * nmax + j) * width);
-    return FA_OK;
-  }
-  void release() {
-    fa_plan_destroy(plan);
-    if (stack) (void)hipFree(stack);
-    if (gather) (void)hipFree(gather);
-    plan = nullptr;
-    stack = gather = nullptr;
-  }
-  // stack this rank's n_local buckets on stream s
-  int stack_local(const int64_t* const* c64, int n_local, hipStream_t s) {
-    for (int j0 = 0; j0 < n_local; j0 += kStackPtrs) {
-      StackArgs a;
-      memset(&a, 0, sizeof a);
-      a.rows = std::min(kStackPtrs, n_local - j0);
-      for (int j = 0; j < a.rows; ++j) a.src[j] = c64[j0 + j];
-      a.dst = stack + (size_t)j0 * width;
-      a.width = width;
-      const int gx = (int)std::min<int64_t>(64, (width + 255) / 256);
-      hipLaunchKernelGGL(stack_i64_kernel, dim3(gx, a.rows), dim3(256), 0, s, a);
-      FA_HIP_TRY(hipGetLastError());
+int launch_stack(bool f32, const void* const* src, const float* w, int n_local, void* dst,
+                 const int64_t* idx, int64_t width, int64_t stride, hipStream_t s) {
+  for (int j0 = 0; j0 < n_local; j0 += kStackPtrs) {
+    StackArgs a;
+    memset(&a, 0, sizeof a);
+    a.rows = std::min(kStackPtrs, n_local - j0);
+    for (int j = 0; j < a.rows; ++j) {
+      a.src[j] = src[j0 + j];
+      a.w[j] = w ? w[j0 + j] : 1.f;
     }
-    return FA_OK;
+    a.weighted = w != nullptr;
+    a.dst = (char*)dst + (size_t)j0 * stride * (f32 ? 4 : 8);
+    a.idx = idx;
+    a.width = width;
+    a.stride = stride;
+    const int gx = (int)std::min<int64_t>(64, (width + 255) / 256);
+    if (f32) hipLaunchKernelGGL(stack_f32_kernel, dim3(gx, a.rows), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(stack_i64_kernel, dim3(gx, a.rows), dim3(256), 0, s, a);
+    FA_HIP_TRY(hipGetLastError());
   }
+  return FA_OK;
+}
+
+// ------------------------------------------------------------- geometry ----
+// Everything a schedule depends on, host-only (no device, no communicator).
+struct Geo {
+  int nranks = 1, rank = 0;
+  std::vector<int> counts, first;  // per rank: slots held, first slot
+  int n_total = 0, n_local = 0, lo_slot = 0, nmax = 0;
+  int64_t f32_numel = 0, i64_numel = 0;
+  unsigned flags = 0;
+  std::vector<fa_tile_desc> t32, t64;  // fp32 tiles sorted by start; int64 tiles
 };
 
-// ------------------------------------------------------------ tile cuts --
-// The layout's fp32 tiles sorted by start, and its int64 tiles.
-int layout_tiles(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_seg* seg64,
-                 int nseg64, int64_t i64_numel, unsigned flags, std::vector<fa_tile_desc>* t32,
-                 std::vector<fa_tile_desc>* t64) {
+int make_geo(int nranks, int rank, const int* counts, const fa_seg* seg32, int nseg32,
+             int64_t f32_numel, const fa_seg* seg64, int nseg64, int64_t i64_numel,
+             unsigned flags, const char* who, Geo* g) {
+  if (!counts) return set_err(FA_E_INVAL, "%s: counts is NULL", who);
+  if (nranks < 1 || rank < 0 || rank >= nranks)
+    return set_err(FA_E_INVAL, "%s: rank %d of %d", who, rank, nranks);
+  if (!(flags & FA_PLAN_GAPS_ARE_PADDING))
+    return set_err(FA_E_INVAL,
+                   "%s: the layout must allow writes to its padding "
+                   "(FA_PLAN_GAPS_ARE_PADDING): exchanges span it",
+                   who);
+  g->nranks = nranks;
+  g->rank = rank;
+  g->counts.assign(counts, counts + nranks);
+  g->first.clear();
+  g->n_total = 0;
+  g->nmax = 0;
+  for (int r = 0; r < nranks; ++r) {
+    if (counts[r] < 0) return set_err(FA_E_INVAL, "%s: counts[%d]=%d", who, r, counts[r]);
+    g->first.push_back(g->n_total);
+    g->n_total += counts[r];
+    g->nmax = std::max(g->nmax, counts[r]);
+  }
+  if (g->n_total < 1 || g->n_total > FA_MAX_CLIENTS)
+    return set_err(FA_E_RANGE, "%s: %d clients in total", who, g->n_total);
+  g->n_local = counts[rank];
+  g->lo_slot = g->first[rank];
+  g->f32_numel = f32_numel;
+  g->i64_numel = i64_numel;
+  g->flags = flags;
   fa_plan_info info{};
   int rc = fa_plan_build_host(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, 0, flags,
                               nullptr, 0, &info);
@@ -131,35 +182,316 @@ int layout_tiles(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_se
                           tiles.data(), info.ntiles, &info);
   if (rc) return rc;
   tiles.resize(info.ntiles);
-  for (const fa_tile_desc& t : tiles) (t.kind >= 4 ? t64 : t32)->push_back(t);
-  std::sort(t32->begin(), t32->end(),
+  g->t32.clear();
+  g->t64.clear();
+  for (const fa_tile_desc& t : tiles) (t.kind >= 4 ? g->t64 : g->t32).push_back(t);
+  std::sort(g->t32.begin(), g->t32.end(),
             [](const fa_tile_desc& a, const fa_tile_desc& b) { return a.start < b.start; });
   return FA_OK;
 }
 
-// k contiguous groups of the sorted fp32 tiles with equal shares of the
-// elements, cut only before a vector tile on a 256-B boundary (so every
-// group's byte range starts aligned); exactly k groups, trailing ones may be
-// empty.  Group g = tiles [cut[g], cut[g+1]), byte range [lo[g], lo[g+1])
-// with lo[0] = 0 and lo[k] = f32_numel (the padding between tensors is
-// covered, FA_PLAN_GAPS_ARE_PADDING).
-void cut_tiles(const std::vector<fa_tile_desc>& t32, int k, int64_t f32_numel,
-               std::vector<size_t>* cut, std::vector<int64_t>* lo) {
+// k contiguous groups of sorted tiles with equal shares of the elements, cut
+// only before a vector tile on a 256-B boundary; exactly k groups, trailing
+// ones may be empty.  Group g = tiles [cut[g], cut[g+1]).
+void cut_tiles(const std::vector<fa_tile_desc>& t, int k, std::vector<size_t>* cut) {
   int64_t total = 0;
-  for (const fa_tile_desc& t : t32) total += t.count;
+  for (const fa_tile_desc& x : t) total += x.count;
   cut->assign(1, 0);
   int64_t acc = 0;
-  for (size_t i = 0; i < t32.size(); ++i) {
+  for (size_t i = 0; i < t.size(); ++i) {
     const int c = (int)cut->size();
-    if (c < k && i > 0 && acc >= total * c / k && t32[i].kind == 0 && t32[i].start % 64 == 0)
+    if (c < k && i > 0 && acc >= total * c / k && t[i].kind == 0 && t[i].start % 64 == 0)
       cut->push_back(i);
-    acc += t32[i].count;
+    acc += t[i].count;
   }
-  while ((int)cut->size() < k + 1) cut->push_back(t32.size());
-  lo->assign(k + 1, f32_numel);
-  (*lo)[0] = 0;
-  for (int g = 1; g < k; ++g)
-    (*lo)[g] = (*cut)[g] < t32.size() ? t32[(*cut)[g]].start : f32_numel;
+  while ((int)cut->size() < k + 1) cut->push_back(t.size());
+}
+
+// Group g's bucket range: [lo[g], lo[g+1]) with lo[0] = 0 and lo[k] =
+// f32_numel — the groups tile the whole bucket (padding included).
+std::vector<int64_t> cut_bounds(const std::vector<fa_tile_desc>& t,
+                                const std::vector<size_t>& cut, int64_t f32_numel) {
+  const int k = (int)cut.size() - 1;
+  std::vector<int64_t> lo(k + 1, f32_numel);
+  lo[0] = 0;
+  for (int g = 1; g < k; ++g) lo[g] = cut[g] < t.size() ? t[cut[g]].start : f32_numel;
+  return lo;
+}
+
+// ------------------------------------------------------------- schedules ---
+inline bool is_comm(int op) { return op >= FA_X_SEND && op <= FA_X_BCAST; }
+
+struct Sched {
+  std::vector<fa_xfer> ops;
+  int step = 0;
+  void add(int op, int peer, int src, int si, int dst, int di, int64_t off, int64_t cnt,
+           int chunk = -1, int row0 = 0, int nrows = 0) {
+    fa_xfer x;
+    memset(&x, 0, sizeof x);
+    x.step = step;
+    x.op = op;
+    x.peer = peer;
+    x.chunk = chunk;
+    x.src = src;
+    x.src_index = si;
+    x.dst = dst;
+    x.dst_index = di;
+    x.offset = off;
+    x.count = cnt;
+    x.row0 = row0;
+    x.nrows = nrows;
+    ops.push_back(x);
+  }
+  void next() { ++step; }
+};
+
+// Round-robin pairing of the ranks (circle method): round t's partner of
+// rank r, or -1 (the odd rank out).  Every pair meets in exactly one round,
+// and within a pair the lower rank sends first, so a transport that
+// serialises a rank's sends and receives (gloo) cannot deadlock.
+int partner(int nranks, int r, int t) {
+  const int m = nranks % 2 ? nranks + 1 : nranks;  // even, with a dummy rank m-1
+  if (m < 2) return -1;
+  const int k = m - 1;                             // rounds t = 0..k-1
+  int q = -1;
+  if (r == k) {
+    for (int i = 0; i < k; ++i)
+      if ((2 * i) % k == t % k) q = i;             // the i with 2i == t (mod k)
+  } else if ((2 * r) % k == t % k) {
+    q = k;
+  } else {
+    q = ((t - r) % k + k) % k;                     // pairs i + j == t (mod k)
+  }
+  return q >= nranks ? -1 : q;
+}
+
+// The int64 keys (num_batches_tracked) of every client, gathered raw and
+// reduced exactly by the result ranks; with `tails`, the fp32 scalar columns
+// (ILP-4 tails, M==1) too.  stack -> all-gather -> (result ranks) reduce.
+void sched_raw_gather(Sched* S, const Geo& g, int64_t t32_width, bool tails, bool result) {
+  const bool i64 = !g.t64.empty();
+  if (!i64 && !(tails && t32_width)) return;
+  if (g.n_local > 0) S->add(FA_X_K_STACK, -1, FA_B_CLIENT, -1, FA_B_STACK, -1, 0, 0, -1,
+                            g.lo_slot, g.n_local);
+  S->next();
+  if (tails && t32_width)
+    S->add(FA_X_ALLGATHER, -1, FA_B_STACK, 0, FA_B_GATHER, 0, 0, (int64_t)g.nmax * t32_width);
+  if (i64)
+    S->add(FA_X_ALLGATHER, -1, FA_B_STACK, 1, FA_B_GATHER, 1, 0,
+           (int64_t)g.nmax * g.i64_numel);
+  S->next();
+  if (result) S->add(FA_X_K_TAILS, -1, FA_B_GATHER, -1, FA_B_OUT, -1, 0, 0, -1, 0, g.n_total);
+  S->next();
+}
+
+// e1: chunked partial sums + RCCL reduce (or reduce-scatter + gather).
+void sched_sharded(const Geo& g, const std::vector<std::pair<int64_t, int64_t>>& range, int xchg,
+                   int root, bool weighted, Sched* S) {
+  const int me = g.rank, W = g.nranks;
+  const bool result = root < 0 || root == me;
+  for (size_t c = 0; c < range.size(); ++c) {
+    const int64_t lo = range[c].first, L = range[c].second - lo;
+    if (g.n_local > 0)
+      S->add(FA_X_K_SUM, -1, FA_B_CLIENT, -1, FA_B_PARTIAL, -1, lo, L, (int)c, g.lo_slot,
+             g.n_local);
+    else
+      S->add(FA_X_K_ZERO, -1, FA_B_NONE, -1, FA_B_PARTIAL, -1, lo, L, (int)c);
+    S->next();
+    const int64_t q = xchg == FA_XCHG_RS_GATHER ? L / W : 0;
+    if (q > 0) {
+      // in place: rank r's share of the sum lands at partial[lo + r*q, +q)
+      S->add(FA_X_REDUCE_SCATTER, -1, FA_B_PARTIAL, -1, FA_B_PARTIAL, -1, lo, q * W);
+      S->next();
+      if (root < 0)
+        S->add(FA_X_ALLGATHER, -1, FA_B_PARTIAL, -1, FA_B_OUT, -1, lo, q * W);
+      else
+        S->add(FA_X_GATHER, root, FA_B_PARTIAL, -1, result ? FA_B_OUT : FA_B_NONE, -1, lo,
+               q * W);
+    }
+    const int64_t rlo = lo + q * W, rl = L - q * W;  // (all of it for a plain reduce)
+    if (rl > 0) {
+      if (root < 0)
+        S->add(FA_X_ALLREDUCE, -1, FA_B_PARTIAL, -1, FA_B_OUT, -1, rlo, rl);
+      else
+        S->add(FA_X_REDUCE, root, FA_B_PARTIAL, -1, result ? FA_B_OUT : FA_B_PARTIAL, -1, rlo,
+               rl);
+    }
+    S->next();
+    if (result && !weighted) S->add(FA_X_K_DIV, -1, FA_B_OUT, -1, FA_B_OUT, -1, lo, L, (int)c);
+    S->next();
+  }
+  sched_raw_gather(S, g, 0, false, result);
+}
+
+// e2: column stripes.
+void sched_striped(const Geo& g, const std::vector<int64_t>& lo, int root, Sched* S) {
+  const int me = g.rank, W = g.nranks;
+  const bool result = root < 0 || root == me;
+  const int64_t Lme = lo[me + 1] - lo[me];
+  // 1. every client's values for stripe r go to rank r, one partner per round
+  const int rounds = W % 2 ? W : W - 1;
+  for (int t = 0; t < rounds; ++t) {
+    const int r = partner(W, me, t);
+    if (r < 0 || r == me) continue;
+    const int64_t Lr = lo[r + 1] - lo[r];
+    auto sends = [&]() {
+      if (Lr > 0)
+        for (int j = 0; j < g.n_local; ++j)
+          S->add(FA_X_SEND, r, FA_B_CLIENT, j, FA_B_NONE, -1, lo[r], Lr);
+    };
+    auto recvs = [&]() {
+      if (Lme > 0)
+        for (int k = 0; k < g.counts[r]; ++k)
+          S->add(FA_X_RECV, r, FA_B_NONE, -1, FA_B_RECV, g.first[r] + k, lo[me], Lme);
+    };
+    if (me < r) { sends(); recvs(); } else { recvs(); sends(); }
+    S->next();
+  }
+  S->next();
+  // 2. the stripe over all n_total clients, exact order
+  if (Lme > 0)
+    S->add(FA_X_K_STRIPE, -1, FA_B_RECV, -1, FA_B_STRIPE, -1, lo[me], Lme, me, 0, g.n_total);
+  S->next();
+  // 3. the finished stripes to the result ranks, pairwise again
+  for (int t = 0; t < rounds; ++t) {
+    const int r = partner(W, me, t);
+    if (r < 0 || r == me) continue;
+    const int64_t Lr = lo[r + 1] - lo[r];
+    const bool r_result = root < 0 || root == r;
+    auto sends = [&]() {
+      if (Lme > 0 && r_result) S->add(FA_X_SEND, r, FA_B_STRIPE, -1, FA_B_NONE, -1, lo[me], Lme);
+    };
+    auto recvs = [&]() {
+      if (Lr > 0 && result) S->add(FA_X_RECV, r, FA_B_NONE, -1, FA_B_OUT, -1, lo[r], Lr);
+    };
+    if (me < r) { sends(); recvs(); } else { recvs(); sends(); }
+    S->next();
+  }
+  S->next();
+  if (result && Lme > 0) S->add(FA_X_K_COPY, -1, FA_B_STRIPE, -1, FA_B_OUT, -1, lo[me], Lme);
+  S->next();
+  sched_raw_gather(S, g, 0, false, result);
+}
+
+// Chained: state hops rank to rank, chunk by chunk.
+struct ChainGeo {
+  std::vector<std::pair<int64_t, int64_t>> range;  // vector-tile chunks [lo, hi)
+  int finisher = 0;                                // last rank holding clients
+  unsigned lev_in = 0, lev_out = 0;
+  int64_t t32_width = 0;                           // scalar fp32 columns
+  int64_t t32_row = 0;                             // their stack row stride (64-aligned)
+};
+
+void sched_chained(const Geo& g, const ChainGeo& cg, int root, Sched* S) {
+  const int me = g.rank, F = cg.finisher;
+  const bool result = root < 0 || root == me;
+  // the raw scalar columns first: their gather overlaps the chain
+  const int64_t C = (int64_t)cg.range.size();
+  const bool i64 = !g.t64.empty();
+  if (i64 || cg.t32_width) {
+    if (g.n_local > 0)
+      S->add(FA_X_K_STACK, -1, FA_B_CLIENT, -1, FA_B_STACK, -1, 0, 0, -1, g.lo_slot, g.n_local);
+    S->next();
+    if (cg.t32_width)
+      S->add(FA_X_ALLGATHER, -1, FA_B_STACK, 0, FA_B_GATHER, 0, 0, (int64_t)g.nmax * cg.t32_row);
+    if (i64)
+      S->add(FA_X_ALLGATHER, -1, FA_B_STACK, 1, FA_B_GATHER, 1, 0,
+             (int64_t)g.nmax * g.i64_numel);
+    S->next();
+  }
+  if (me <= F) {
+    const bool pred = me > 0 && cg.lev_in, succ = me < F && cg.lev_out;
+    auto planes = [&](int op, int peer, unsigned lev, int64_t c) {
+      for (int l = 0; l < 4; ++l)
+        if (lev & (1u << l)) {
+          const int64_t lo = cg.range[c].first, L = cg.range[c].second - lo;
+          if (op == FA_X_SEND) S->add(op, peer, FA_B_STATE, l, FA_B_NONE, -1, lo, L, (int)c);
+          else S->add(op, peer, FA_B_NONE, -1, FA_B_STATE, l, lo, L, (int)c);
+        }
+    };
+    const int fin = me < F ? FA_B_STATE : (result ? FA_B_OUT : FA_B_FIN);
+    for (int64_t c = 0; c <= C; ++c) {
+      if (succ && c > 0) planes(FA_X_SEND, me + 1, cg.lev_out, c - 1);
+      if (pred && c < C) planes(FA_X_RECV, me - 1, cg.lev_in, c);
+      S->next();
+      if (c < C && g.n_local > 0) {
+        const int64_t lo = cg.range[c].first, L = cg.range[c].second - lo;
+        S->add(FA_X_K_CHAIN, -1, pred ? FA_B_STATE : FA_B_NONE, -1, fin, -1, lo, L, (int)c,
+               g.lo_slot, g.n_local);
+      }
+      S->next();
+    }
+  } else {
+    S->step += 2 * (int)(C + 1);
+  }
+  // the finished vector columns to the result ranks
+  if (C > 0) {
+    const int64_t lo = cg.range[0].first, L = cg.range[C - 1].second - lo;
+    if (root < 0) {
+      S->add(FA_X_BCAST, F, me == F ? FA_B_OUT : FA_B_NONE, -1, FA_B_OUT, -1, lo, L);
+    } else if (root != F) {
+      if (me == F) S->add(FA_X_SEND, root, FA_B_FIN, -1, FA_B_NONE, -1, lo, L);
+      if (me == root) S->add(FA_X_RECV, F, FA_B_NONE, -1, FA_B_OUT, -1, lo, L);
+    }
+  }
+  S->next();
+  if (result && (i64 || cg.t32_width))
+    S->add(FA_X_K_TAILS, -1, FA_B_GATHER, -1, FA_B_OUT, -1, 0, 0, -1, 0, g.n_total);
+  S->next();
+}
+
+// The chained mode's cut of the layout: vector tiles chunked, scalar fp32
+// columns compacted (their bucket index per compact column).
+void chain_geo(const Geo& g, int nchunks, ChainGeo* cg, std::vector<fa_tile_desc>* vec,
+               std::vector<size_t>* cut, std::vector<fa_tile_desc>* tails,
+               std::vector<int64_t>* tidx) {
+  vec->clear();
+  tails->clear();
+  tidx->clear();
+  for (const fa_tile_desc& t : g.t32) {
+    if (t.kind == 0) {
+      vec->push_back(t);
+    } else {
+      fa_tile_desc c = t;
+      c.start = (int64_t)tidx->size();  // compact coordinates
+      tails->push_back(c);
+      for (int32_t e = 0; e < t.count; ++e) tidx->push_back(t.start + e);
+    }
+  }
+  cg->t32_width = (int64_t)tidx->size();
+  cg->t32_row = (cg->t32_width + 63) / 64 * 64;
+  cg->range.clear();
+  cut_tiles(*vec, nchunks, cut);
+  std::vector<size_t> keep(1, 0);
+  for (int c = 0; c < nchunks; ++c) {
+    if ((*cut)[c] == (*cut)[c + 1]) continue;
+    const fa_tile_desc& a = (*vec)[(*cut)[c]];
+    const fa_tile_desc& b = (*vec)[(*cut)[c + 1] - 1];
+    cg->range.emplace_back(a.start, b.start + b.count);
+    keep.push_back((*cut)[c + 1]);
+  }
+  *cut = keep;
+  cg->finisher = 0;
+  for (int r = 0; r < g.nranks; ++r)
+    if (g.counts[r] > 0) cg->finisher = r;
+  cg->lev_in = fa_chain_levels(g.lo_slot, g.n_total);
+  cg->lev_out = fa_chain_levels(g.lo_slot + g.n_local, g.n_total);
+}
+
+// e1 chunk ranges over the whole bucket.
+void shard_ranges(const Geo& g, int nchunks, std::vector<size_t>* cut_out,
+                  std::vector<std::pair<int64_t, int64_t>>* range) {
+  std::vector<size_t> cut;
+  cut_tiles(g.t32, nchunks, &cut);
+  const std::vector<int64_t> lo = cut_bounds(g.t32, cut, g.f32_numel);
+  range->clear();
+  cut_out->assign(1, 0);
+  for (int c = 0; c < nchunks; ++c) {
+    if (cut[c] == cut[c + 1]) continue;
+    range->emplace_back(lo[c], lo[c + 1]);
+    cut_out->push_back(cut[c + 1]);
+  }
+  if (!range->empty()) range->back().second = g.f32_numel;
 }
 
 struct DeviceGuard {
@@ -190,104 +522,514 @@ int make_comm(ncclComm_t nc, int device, fa_comm** out) {
   return FA_OK;
 }
 
-int slot_layout(const fa_comm* comm, const int* counts, int* n_total, int* lo_slot,
-                const char* who) {
-  *n_total = 0;
-  *lo_slot = 0;
-  for (int r = 0; r < comm->nranks; ++r) {
-    if (counts[r] < 0) return set_err(FA_E_INVAL, "%s: counts[%d]=%d", who, r, counts[r]);
-    if (r < comm->rank) *lo_slot += counts[r];
-    *n_total += counts[r];
-  }
-  if (*n_total < 1 || *n_total > FA_MAX_CLIENTS)
-    return set_err(FA_E_RANGE, "%s: %d clients in total", who, *n_total);
-  return FA_OK;
-}
-
-int make_events(std::vector<hipEvent_t>* ev, size_t n) {
-  for (size_t i = 0; i < n; ++i) {
-    hipEvent_t e;
-    FA_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    ev->push_back(e);
-  }
-  return FA_OK;
-}
-
 }  // namespace
 
-struct fa_shard_plan {
+// =========================================================== round plans ==
+// One plan type for the three modes: the schedule geometry plus the device
+// resources its ops address.
+struct fa_round_plan {
+  int mode = 0;  // FA_MODE_*
+  int xchg = 0;
   fa_comm* comm = nullptr;
-  int64_t f32_numel = 0, i64_numel = 0;
-  int n_local = 0, n_total = 0, lo_slot = 0;
-  std::vector<fa_plan*> chunk;                     // tile subset per column chunk
-  std::vector<std::pair<int64_t, int64_t>> range;  // [lo, hi) of each chunk
-  float* partial = nullptr;                        // f32_numel (library scratch)
-  I64Part i64;
-  std::vector<hipEvent_t> ev;  // per chunk (+ int64, + done)
-};
-
-struct fa_stripe_plan {
-  fa_comm* comm = nullptr;
-  int64_t f32_numel = 0, i64_numel = 0;
-  int n_local = 0, n_total = 0, lo_slot = 0;
-  std::vector<int> counts, first_slot;  // per rank
-  std::vector<int64_t> lo;              // nranks + 1 stripe bounds
-  fa_plan* stripe = nullptr;            // this rank's stripe tiles (nullptr: empty)
-  int64_t row = 0;                      // recv row stride (floats, 64-aligned)
-  float* recv = nullptr;                // n_total rows of the stripe
-  float* sbuf = nullptr;                // the reduced stripe
-  std::vector<const float*> ptrs;       // the n_total source pointers (see create)
-  I64Part i64;
-  std::vector<hipEvent_t> ev;  // start, int64, done
+  Geo g;
+  // e1: chunk plans + their ranges; chained: vector-tile chunk plans + ranges
+  std::vector<fa_plan*> chunk;
+  std::vector<std::pair<int64_t, int64_t>> range;
+  float* partial = nullptr;  // e1 partial sums (f32_numel)
+  // e2
+  std::vector<int64_t> lo;   // nranks + 1 stripe bounds
+  fa_plan* stripe = nullptr;
+  int64_t row = 0;           // receive row stride (floats)
+  float* recv = nullptr;     // n_total rows
+  float* sbuf = nullptr;     // the reduced stripe
+  // chained
+  ChainGeo cg;
+  float* state = nullptr;    // nplanes * plane floats
+  int64_t plane = 0;
+  float* fin = nullptr;      // the finisher's result when it is not a result rank
+  // raw scalar columns (int64 keys; chained: also the fp32 tails)
+  fa_plan* plan64 = nullptr;
+  fa_plan* plan_t32 = nullptr;  // compact tail tiles
+  int64_t* tidx = nullptr;      // device: bucket index per compact tail column
+  float* t32_stack = nullptr;
+  float* t32_gather = nullptr;
+  float* t32_out = nullptr;
+  int64_t* i64_stack = nullptr;
+  int64_t* i64_gather = nullptr;
+  std::vector<const float*> t32_rows;
+  std::vector<const int64_t*> i64_rows;
+  std::vector<hipEvent_t> ev;  // start, compute-joins (ring), done
+  std::map<std::pair<int, int>, std::vector<fa_xfer>> sched;  // (root, weighted) -> ops
 };
 
 namespace {
-void free_shard(fa_shard_plan* p) {
+
+void free_round(fa_round_plan* p) {
   if (!p) return;
-  DeviceGuard g;
+  DeviceGuard dg;
   if (p->comm) (void)hipSetDevice(p->comm->device);
   for (fa_plan* c : p->chunk) fa_plan_destroy(c);
-  if (p->partial) (void)hipFree(p->partial);
-  p->i64.release();
-  for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
-  delete p;
-}
-void free_stripe(fa_stripe_plan* p) {
-  if (!p) return;
-  DeviceGuard g;
-  if (p->comm) (void)hipSetDevice(p->comm->device);
   fa_plan_destroy(p->stripe);
-  if (p->recv) (void)hipFree(p->recv);
-  if (p->sbuf) (void)hipFree(p->sbuf);
-  p->i64.release();
+  fa_plan_destroy(p->plan64);
+  fa_plan_destroy(p->plan_t32);
+  void* bufs[] = {p->partial, p->recv,      p->sbuf,    p->state,     p->fin,       p->tidx,
+                  p->t32_stack, p->t32_gather, p->t32_out, p->i64_stack, p->i64_gather};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
   for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
   delete p;
 }
 
-// int64 keys after the local buckets are stacked on stream s: all-gather
-// (grouped over the local GPUs by the caller) happens in run_i64_exchange.
-int i64_exchange(I64Part* const* parts, const fa_comm* const* comms, int nlocal) {
-  NCCL_TRY(ncclGroupStart());
-  for (int d = 0; d < nlocal; ++d) {
-    (void)hipSetDevice(comms[d]->device);
-    ncclResult_t r = ncclAllGather(parts[d]->stack, parts[d]->gather,
-                                   (size_t)parts[d]->nmax * parts[d]->width, ncclInt64,
-                                   comms[d]->nc, comms[d]->cs);
-    if (r != ncclSuccess) {
-      ncclGroupEnd();
-      return set_err(FA_E_COMM, "int64 all-gather: %s", ncclGetErrorString(r));
-    }
+// Host-only part of a plan: geometry and the cut.  With `dev`, also the
+// device resources (tile plans, scratch, events) on the comm's device.
+int build_round(fa_round_plan* p, int nchunks, std::vector<fa_tile_desc>* vec_out,
+                std::vector<size_t>* cut_out, std::vector<fa_tile_desc>* tails_out,
+                std::vector<int64_t>* tidx_out) {
+  const Geo& g = p->g;
+  if (p->mode == FA_MODE_SHARDED) {
+    shard_ranges(g, nchunks, cut_out, &p->range);
+  } else if (p->mode == FA_MODE_STRIPED) {
+    std::vector<size_t> cut;
+    cut_tiles(g.t32, g.nranks, &cut);
+    p->lo = cut_bounds(g.t32, cut, g.f32_numel);
+    *cut_out = cut;
+  } else {
+    chain_geo(g, nchunks, &p->cg, vec_out, cut_out, tails_out, tidx_out);
+    p->range = p->cg.range;
   }
-  NCCL_TRY(ncclGroupEnd());
   return FA_OK;
 }
-}  // namespace
+
+int alloc(void** p, size_t bytes, bool zero) {
+  FA_HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 16)));
+  if (zero) FA_HIP_TRY(hipMemset(*p, 0, std::max<size_t>(bytes, 16)));
+  return FA_OK;
+}
+
+int make_round(fa_comm* comm, int mode, const fa_seg* seg32, int nseg32, int64_t f32_numel,
+               const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
+               int nchunks, int xchg, unsigned flags, const char* who, fa_round_plan** out) {
+  if (!out) return set_err(FA_E_INVAL, "%s: out is NULL", who);
+  *out = nullptr;
+  if (!comm || !counts) return set_err(FA_E_INVAL, "%s: NULL comm/counts", who);
+  if (nchunks == 0) nchunks = 8;
+  if (nchunks < 1 || nchunks > FA_COMM_MAX_CHUNKS)
+    return set_err(FA_E_INVAL, "%s: nchunks=%d", who, nchunks);
+  if (xchg != FA_XCHG_REDUCE && xchg != FA_XCHG_RS_GATHER)
+    return set_err(FA_E_INVAL, "%s: exchange %d", who, xchg);
+  fa_round_plan* p = new fa_round_plan();
+  p->mode = mode;
+  p->xchg = xchg;
+  p->comm = comm;
+  int rc = make_geo(comm->nranks, comm->rank, counts, seg32, nseg32, f32_numel, seg64, nseg64,
+                    i64_numel, flags, who, &p->g);
+  if (rc) {
+    delete p;
+    return rc;
+  }
+  DeviceGuard dg;
+  hipError_t he = hipSetDevice(comm->device);
+  if (he != hipSuccess) {
+    delete p;
+    return set_err(FA_E_HIP, "%s: %s", who, hipGetErrorString(he));
+  }
+  const Geo& g = p->g;
+  std::vector<fa_tile_desc> vec, tails;
+  std::vector<size_t> cut;
+  std::vector<int64_t> tidx;
+  build_round(p, nchunks, &vec, &cut, &tails, &tidx);
+  auto fail = [&](int code) {
+    free_round(p);
+    return code;
+  };
+  // tile plans
+  if (mode == FA_MODE_SHARDED) {
+    for (size_t c = 0; c + 1 < cut.size(); ++c) {
+      fa_plan* sub = nullptr;
+      rc = fa_plan_create_from_tiles(g.t32.data() + cut[c], (int)(cut[c + 1] - cut[c]),
+                                     f32_numel, i64_numel, 0, flags, &sub);
+      if (rc) return fail(rc);
+      p->chunk.push_back(sub);
+    }
+    if (!p->chunk.empty() && (rc = alloc((void**)&p->partial, (size_t)f32_numel * 4, true)))
+      return fail(rc);
+  } else if (mode == FA_MODE_STRIPED) {
+    const int me = g.rank;
+    const int64_t L = p->lo[me + 1] - p->lo[me];
+    if (cut[me] < cut[me + 1]) {
+      rc = fa_plan_create_from_tiles(g.t32.data() + cut[me], (int)(cut[me + 1] - cut[me]),
+                                     f32_numel, i64_numel, 0, flags, &p->stripe);
+      if (rc) return fail(rc);
+      // one row per client slot, 256-B aligned; the stripe starts on a
+      // 64-float boundary, so (row - lo) keeps the 16-B alignment
+      p->row = (L + 63) / 64 * 64;
+      if ((rc = alloc((void**)&p->recv, (size_t)g.n_total * p->row * 4, false))) return fail(rc);
+      if ((rc = alloc((void**)&p->sbuf, (size_t)p->row * 4, true))) return fail(rc);
+    }
+  } else {
+    for (size_t c = 0; c + 1 < cut.size(); ++c) {
+      fa_plan* sub = nullptr;
+      rc = fa_plan_create_from_tiles(vec.data() + cut[c], (int)(cut[c + 1] - cut[c]), f32_numel,
+                                     0, 0, flags, &sub);
+      if (rc) return fail(rc);
+      p->chunk.push_back(sub);
+    }
+    const int nplanes = g.n_total >= 256 ? 4 : 2;
+    p->plane = (f32_numel + 63) / 64 * 64;
+    if (!p->chunk.empty()) {
+      if ((rc = alloc((void**)&p->state, (size_t)nplanes * p->plane * 4, true))) return fail(rc);
+      if (g.rank == p->cg.finisher &&
+          (rc = alloc((void**)&p->fin, (size_t)f32_numel * 4, true)))
+        return fail(rc);
+    }
+    if (!tails.empty()) {
+      const int64_t T = p->cg.t32_width;
+      rc = fa_plan_create_from_tiles(tails.data(), (int)tails.size(), T, 0, 0, 0, &p->plan_t32);
+      if (rc) return fail(rc);
+      if ((rc = alloc((void**)&p->tidx, (size_t)T * 8, false))) return fail(rc);
+      he = hipMemcpy(p->tidx, tidx.data(), (size_t)T * 8, hipMemcpyHostToDevice);
+      if (he != hipSuccess) return fail(set_err(FA_E_HIP, "%s: %s", who, hipGetErrorString(he)));
+      const int64_t R = p->cg.t32_row;
+      if ((rc = alloc((void**)&p->t32_stack, (size_t)g.nmax * R * 4, true))) return fail(rc);
+      if ((rc = alloc((void**)&p->t32_gather, (size_t)g.nranks * g.nmax * R * 4, true)))
+        return fail(rc);
+      if ((rc = alloc((void**)&p->t32_out, (size_t)((T + 63) / 64 * 64) * 4, true)))
+        return fail(rc);
+      for (int r = 0; r < g.nranks; ++r)
+        for (int j = 0; j < g.counts[r]; ++j)
+          p->t32_rows.push_back(p->t32_gather + ((size_t)r * g.nmax + j) * R);
+    }
+  }
+  if (!g.t64.empty()) {
+    rc = fa_plan_create_from_tiles(g.t64.data(), (int)g.t64.size(), f32_numel, i64_numel, 0,
+                                   flags, &p->plan64);
+    if (rc) return fail(rc);
+    const size_t rowb = (size_t)i64_numel * 8;
+    if ((rc = alloc((void**)&p->i64_stack, (size_t)g.nmax * rowb, true))) return fail(rc);
+    if ((rc = alloc((void**)&p->i64_gather, (size_t)g.nranks * g.nmax * rowb, true)))
+      return fail(rc);
+    for (int r = 0; r < g.nranks; ++r)
+      for (int j = 0; j < g.counts[r]; ++j)
+        p->i64_rows.push_back(p->i64_gather + ((size_t)r * g.nmax + j) * i64_numel);
+  }
+  for (int i = 0; i < 3; ++i) {
+    hipEvent_t e;
+    he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (he != hipSuccess) return fail(set_err(FA_E_HIP, "%s: %s", who, hipGetErrorString(he)));
+    p->ev.push_back(e);
+  }
+  *out = p;
+  return FA_OK;
+}
+
+const std::vector<fa_xfer>& schedule(fa_round_plan* p, int root, bool weighted) {
+  auto key = std::make_pair(root, weighted ? 1 : 0);
+  auto it = p->sched.find(key);
+  if (it != p->sched.end()) return it->second;
+  Sched S;
+  if (p->mode == FA_MODE_SHARDED) sched_sharded(p->g, p->range, p->xchg, root, weighted, &S);
+  else if (p->mode == FA_MODE_STRIPED) sched_striped(p->g, p->lo, root, &S);
+  else sched_chained(p->g, p->cg, root, &S);
+  return p->sched[key] = S.ops;
+}
+
+// ------------------------------------------------------------ executor ----
+struct Local {
+  fa_round_plan* p;
+  const fa_shard_io* io;
+  hipStream_t user;  // the caller's stream (compute)
+  bool comp_dirty;   // compute-stream work the comm stream has not joined yet
+  std::vector<const float*> src;  // e2 stripe sources
+};
+
+ncclDataType_t dtype_of(int buf, int index) {
+  return ((buf == FA_B_STACK || buf == FA_B_GATHER) && index == 1) ? ncclInt64 : ncclFloat32;
+}
+
+// Device address of (buffer, index, bucket offset).
+void* addr(Local& L, int buf, int index, int64_t off) {
+  fa_round_plan* p = L.p;
+  const fa_shard_io* io = L.io;
+  switch (buf) {
+    case FA_B_CLIENT: return (void*)(io->c32[index] + off);
+    case FA_B_OUT: return io->out32 ? (void*)(io->out32 + off) : nullptr;
+    case FA_B_PARTIAL: return p->partial + off;
+    case FA_B_RECV: return p->recv + (size_t)index * p->row + (off - p->lo[p->g.rank]);
+    case FA_B_STRIPE: return p->sbuf + (off - p->lo[p->g.rank]);
+    case FA_B_STATE: return p->state + (size_t)index * p->plane + off;
+    case FA_B_FIN: return p->fin + off;
+    case FA_B_STACK: return index == 1 ? (void*)(p->i64_stack + off) : (void*)(p->t32_stack + off);
+    case FA_B_GATHER:
+      return index == 1 ? (void*)(p->i64_gather + off) : (void*)(p->t32_gather + off);
+    default: return nullptr;
+  }
+}
+
+bool on_comm_stream(const fa_xfer& x) {
+  if (is_comm(x.op)) return true;
+  switch (x.op) {
+    case FA_X_K_SUM:
+    case FA_X_K_ZERO:
+    case FA_X_K_STACK: return false;                 // read local inputs only
+    case FA_X_K_CHAIN: return x.src == FA_B_STATE;   // after the state's hop
+    default: return true;                            // read exchanged data
+  }
+}
+
+int issue_comm(Local& L, const fa_xfer& x) {
+  fa_comm* c = L.p->comm;
+  const int64_t n = x.count;
+  ncclResult_t r = ncclSuccess;
+  switch (x.op) {
+    case FA_X_SEND:
+      r = ncclSend(addr(L, x.src, x.src_index, x.offset), (size_t)n, ncclFloat32, x.peer, c->nc,
+                   c->cs);
+      break;
+    case FA_X_RECV:
+      r = ncclRecv(addr(L, x.dst, x.dst_index, x.offset), (size_t)n, ncclFloat32, x.peer, c->nc,
+                   c->cs);
+      break;
+    case FA_X_REDUCE:
+      r = ncclReduce(addr(L, x.src, -1, x.offset),
+                     x.dst == FA_B_NONE ? addr(L, x.src, -1, x.offset)
+                                        : addr(L, x.dst, -1, x.offset),
+                     (size_t)n, ncclFloat32, ncclSum, x.peer, c->nc, c->cs);
+      break;
+    case FA_X_ALLREDUCE:
+      r = ncclAllReduce(addr(L, x.src, -1, x.offset), addr(L, x.dst, -1, x.offset), (size_t)n,
+                        ncclFloat32, ncclSum, c->nc, c->cs);
+      break;
+    case FA_X_REDUCE_SCATTER: {
+      const int64_t q = n / c->nranks;
+      r = ncclReduceScatter(addr(L, x.src, -1, x.offset),
+                            addr(L, x.dst, -1, x.offset + (int64_t)c->rank * q), (size_t)q,
+                            ncclFloat32, ncclSum, c->nc, c->cs);
+      break;
+    }
+    case FA_X_GATHER: {
+      const int64_t q = n / c->nranks;
+      // non-root ranks receive nothing; RCCL still gets a valid pointer
+      void* dst = x.dst == FA_B_NONE ? addr(L, x.src, -1, x.offset) : addr(L, x.dst, -1, x.offset);
+      r = ncclGather(addr(L, x.src, -1, x.offset + (int64_t)c->rank * q), dst, (size_t)q,
+                     ncclFloat32, x.peer, c->nc, c->cs);
+      break;
+    }
+    case FA_X_ALLGATHER: {
+      if (x.src == FA_B_PARTIAL) {  // e1: every rank's share of the chunk
+        const int64_t q = n / c->nranks;
+        r = ncclAllGather(addr(L, x.src, -1, x.offset + (int64_t)c->rank * q),
+                          addr(L, x.dst, -1, x.offset), (size_t)q, ncclFloat32, c->nc, c->cs);
+      } else {                      // raw scalar columns: n = one rank's rows
+        r = ncclAllGather(addr(L, x.src, x.src_index, x.offset),
+                          addr(L, x.dst, x.dst_index, x.offset), (size_t)n,
+                          dtype_of(x.src, x.src_index), c->nc, c->cs);
+      }
+      break;
+    }
+    case FA_X_BCAST: {
+      void* b = addr(L, x.dst, -1, x.offset);
+      r = ncclBroadcast(b, b, (size_t)n, ncclFloat32, x.peer, c->nc, c->cs);
+      break;
+    }
+    default: return set_err(FA_E_INVAL, "schedule: op %d is not an exchange", x.op);
+  }
+  if (r != ncclSuccess) return set_err(FA_E_COMM, "op %d (peer %d, %lld floats): %s", x.op,
+                                       x.peer, (long long)n, ncclGetErrorString(r));
+  return FA_OK;
+}
+
+int issue_local(Local& L, const fa_xfer& x, hipStream_t s) {
+  fa_round_plan* p = L.p;
+  const fa_shard_io* io = L.io;
+  const Geo& g = p->g;
+  switch (x.op) {
+    case FA_X_K_SUM:
+      return fa_reduce(p->chunk[x.chunk], io->c32, nullptr, x.nrows, io->weights, p->partial,
+                       nullptr, FA_F_SUM_ONLY, s);
+    case FA_X_K_ZERO:
+      FA_HIP_TRY(hipMemsetAsync(p->partial + x.offset, 0, (size_t)x.count * 4, s));
+      return FA_OK;
+    case FA_X_K_DIV:
+      return fa_div_f32(io->out32 + x.offset, (float)g.n_total, io->out32 + x.offset, x.count,
+                        s);
+    case FA_X_K_COPY:
+      FA_HIP_TRY(hipMemcpyAsync(addr(L, x.dst, x.dst_index, x.offset),
+                                addr(L, x.src, x.src_index, x.offset), (size_t)x.count * 4,
+                                hipMemcpyDeviceToDevice, s));
+      return FA_OK;
+    case FA_X_K_STRIPE: {
+      L.src.assign(p->g.n_total, nullptr);
+      for (int k = 0; k < g.n_total; ++k)
+        L.src[k] = p->recv + (size_t)k * p->row - p->lo[g.rank];  // element e at [e - lo]
+      for (int j = 0; j < g.n_local; ++j) L.src[g.lo_slot + j] = io->c32[j];
+      return fa_reduce(p->stripe, L.src.data(), nullptr, g.n_total, nullptr,
+                       p->sbuf - p->lo[g.rank], nullptr, 0, s);
+    }
+    case FA_X_K_CHAIN: {
+      fa_chain ch;
+      ch.row0 = x.row0;
+      ch.n_total = g.n_total;
+      ch.state_in = x.src == FA_B_STATE ? p->state : nullptr;
+      ch.state_out = x.dst == FA_B_STATE ? p->state : nullptr;
+      ch.plane = p->plane;
+      float* out = x.dst == FA_B_OUT ? io->out32 : (x.dst == FA_B_FIN ? p->fin : nullptr);
+      return fa_reduce_chain(p->chunk[x.chunk], io->c32, x.nrows, io->weights, &ch, out, 0, s);
+    }
+    case FA_X_K_STACK: {
+      if (p->plan64) {
+        const int rc = launch_stack(false, (const void* const*)io->c64, nullptr, g.n_local,
+                                    p->i64_stack, nullptr, g.i64_numel, g.i64_numel, s);
+        if (rc) return rc;
+      }
+      if (p->plan_t32)
+        return launch_stack(true, (const void* const*)io->c32, io->weights, g.n_local,
+                            p->t32_stack, p->tidx, p->cg.t32_width, p->cg.t32_row, s);
+      return FA_OK;
+    }
+    case FA_X_K_TAILS: {
+      if (p->plan64) {
+        const int rc = fa_reduce(p->plan64, nullptr, p->i64_rows.data(), g.n_total, nullptr,
+                                 nullptr, io->out64, 0, s);
+        if (rc) return rc;
+      }
+      if (p->plan_t32) {
+        // pre-multiplied rows when weighted: their plain sum is the weighted order
+        const int rc = fa_reduce(p->plan_t32, p->t32_rows.data(), nullptr, g.n_total, nullptr,
+                                 p->t32_out, nullptr, io->weights ? FA_F_SUM_ONLY : 0, s);
+        if (rc) return rc;
+        const int64_t T = p->cg.t32_width;
+        hipLaunchKernelGGL(scatter_f32_kernel, dim3((unsigned)std::min<int64_t>(64, (T + 255) / 256)),
+                           dim3(256), 0, s, p->t32_out, p->tidx, io->out32, T);
+        FA_HIP_TRY(hipGetLastError());
+      }
+      return FA_OK;
+    }
+    default: return set_err(FA_E_INVAL, "schedule: op %d is not local", x.op);
+  }
+}
+
+// Walk the local GPUs' schedules step by step: one RCCL group per step over
+// every local GPU's exchanges, then the step's kernels.
+int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_xfer>*>& scheds) {
+  const size_t nl = locals.size();
+  std::vector<size_t> pos(nl, 0);
+  for (size_t d = 0; d < nl; ++d) {
+    fa_round_plan* p = locals[d].p;
+    FA_HIP_TRY(hipSetDevice(p->comm->device));
+    // the inputs are ready on the caller's stream
+    FA_HIP_TRY(hipEventRecord(p->ev[0], locals[d].user));
+    FA_HIP_TRY(hipStreamWaitEvent(p->comm->cs, p->ev[0], 0));
+    locals[d].comp_dirty = false;
+  }
+  int step = 0;
+  for (;;) {
+    bool any = false, comm = false;
+    for (size_t d = 0; d < nl; ++d) {
+      const std::vector<fa_xfer>& o = *scheds[d];
+      for (size_t i = pos[d]; i < o.size() && o[i].step == step; ++i) {
+        any = true;
+        comm |= is_comm(o[i].op);
+      }
+      if (pos[d] < o.size()) any = true;
+    }
+    if (!any) break;
+    // comm stream joins the compute stream before this step's exchanges
+    if (comm) {
+      for (size_t d = 0; d < nl; ++d) {
+        Local& L = locals[d];
+        if (!L.comp_dirty) continue;
+        FA_HIP_TRY(hipSetDevice(L.p->comm->device));
+        FA_HIP_TRY(hipEventRecord(L.p->ev[1], L.user));
+        FA_HIP_TRY(hipStreamWaitEvent(L.p->comm->cs, L.p->ev[1], 0));
+        L.comp_dirty = false;
+      }
+      NCCL_TRY(ncclGroupStart());
+      for (size_t d = 0; d < nl; ++d) {
+        const std::vector<fa_xfer>& o = *scheds[d];
+        (void)hipSetDevice(locals[d].p->comm->device);
+        for (size_t i = pos[d]; i < o.size() && o[i].step == step; ++i) {
+          if (!is_comm(o[i].op)) continue;
+          const int rc = issue_comm(locals[d], o[i]);
+          if (rc) {
+            ncclGroupEnd();
+            return rc;
+          }
+        }
+      }
+      NCCL_TRY(ncclGroupEnd());
+    }
+    for (size_t d = 0; d < nl; ++d) {
+      Local& L = locals[d];
+      const std::vector<fa_xfer>& o = *scheds[d];
+      FA_HIP_TRY(hipSetDevice(L.p->comm->device));
+      for (; pos[d] < o.size() && o[pos[d]].step == step; ++pos[d]) {
+        const fa_xfer& x = o[pos[d]];
+        if (is_comm(x.op)) continue;
+        const bool cs = on_comm_stream(x);
+        if (cs && L.comp_dirty) {
+          FA_HIP_TRY(hipEventRecord(L.p->ev[1], L.user));
+          FA_HIP_TRY(hipStreamWaitEvent(L.p->comm->cs, L.p->ev[1], 0));
+          L.comp_dirty = false;
+        }
+        const int rc = issue_local(L, x, cs ? L.p->comm->cs : L.user);
+        if (rc) return rc;
+        if (!cs) L.comp_dirty = true;
+      }
+    }
+    ++step;
+  }
+  // the caller's stream joins the communication stream
+  for (size_t d = 0; d < nl; ++d) {
+    Local& L = locals[d];
+    FA_HIP_TRY(hipSetDevice(L.p->comm->device));
+    FA_HIP_TRY(hipEventRecord(L.p->ev[2], L.p->comm->cs));
+    FA_HIP_TRY(hipStreamWaitEvent(L.user, L.p->ev[2], 0));
+  }
+  return FA_OK;
+}
+
+int run_round(fa_round_plan* const* plans, int nlocal, const fa_shard_io* io, int root, int mode,
+              const char* who) {
+  if (nlocal < 1 || !plans || !io) return set_err(FA_E_INVAL, "%s: bad arguments", who);
+  const bool weighted = io[0].weights != nullptr;
+  std::vector<Local> locals;
+  std::vector<const std::vector<fa_xfer>*> scheds;
+  for (int d = 0; d < nlocal; ++d) {
+    fa_round_plan* p = plans[d];
+    if (!p) return set_err(FA_E_INVAL, "%s: plan %d is NULL", who, d);
+    if (p->mode != mode) return set_err(FA_E_INVAL, "%s: plan %d is of another mode", who, d);
+    if (root >= p->comm->nranks) return set_err(FA_E_INVAL, "%s: root=%d", who, root);
+    if ((io[d].weights != nullptr) != weighted)
+      return set_err(FA_E_INVAL, "%s: weights on some GPUs only", who);
+    if (weighted && mode == FA_MODE_STRIPED)
+      return set_err(FA_E_INVAL, "%s: the striped mode takes no weights", who);
+    const Geo& g = p->g;
+    const bool result = root < 0 || root == g.rank;
+    if (g.n_local > 0 && !io[d].c32)
+      return set_err(FA_E_INVAL, "%s: fp32 buckets required (GPU %d)", who, d);
+    if (g.n_local > 0 && !g.t64.empty() && !io[d].c64)
+      return set_err(FA_E_INVAL, "%s: int64 buckets required (GPU %d)", who, d);
+    if (result && (!io[d].out32 || (!g.t64.empty() && !io[d].out64)))
+      return set_err(FA_E_INVAL, "%s: result buckets required on rank %d", who, g.rank);
+    if (p->g.n_total != plans[0]->g.n_total || p->range.size() != plans[0]->range.size())
+      return set_err(FA_E_INVAL, "%s: plans of different layouts", who);
+    Local L;
+    L.p = p;
+    L.io = &io[d];
+    L.user = (hipStream_t)io[d].stream;
+    L.comp_dirty = false;
+    locals.push_back(L);
+    scheds.push_back(&schedule(p, root, weighted));
+  }
+  DeviceGuard dg;
+  return execute(locals, scheds);
+}
 
 // fa_mean_f32_multi's shard plans, by (communicator, layout, counts); a
 // communicator's entries go with it (fa_comm_destroy).
-namespace {
 std::mutex g_multi_mu;
-std::map<std::string, fa_shard_plan*> g_multi;
+std::map<std::string, fa_round_plan*> g_multi;
+
 }  // namespace
 
 extern "C" {
@@ -343,7 +1085,7 @@ int fa_comm_destroy(fa_comm* c) {
     std::lock_guard<std::mutex> lk(g_multi_mu);
     for (auto it = g_multi.begin(); it != g_multi.end();) {
       if (it->second->comm == c) {
-        free_shard(it->second);
+        free_round(it->second);
         it = g_multi.erase(it);
       } else {
         ++it;
@@ -371,172 +1113,26 @@ int fa_comm_info(const fa_comm* c, int* nranks, int* rank, int* device) {
 int fa_shard_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
                          const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
                          int nchunks, unsigned flags, fa_shard_plan** out) {
-  if (!out) return set_err(FA_E_INVAL, "fa_shard_plan_create: out is NULL");
-  *out = nullptr;
-  if (!comm || !counts) return set_err(FA_E_INVAL, "fa_shard_plan_create: NULL comm/counts");
-  if (!(flags & FA_PLAN_GAPS_ARE_PADDING))
-    return set_err(FA_E_INVAL,
-                   "fa_shard_plan_create: the layout must allow writes to its padding "
-                   "(FA_PLAN_GAPS_ARE_PADDING): chunk exchanges span it");
-  if (nchunks == 0) nchunks = 8;
-  if (nchunks < 1 || nchunks > FA_COMM_MAX_CHUNKS)
-    return set_err(FA_E_INVAL, "fa_shard_plan_create: nchunks=%d", nchunks);
-  int n_total = 0, lo_slot = 0;
-  int rc = slot_layout(comm, counts, &n_total, &lo_slot, "fa_shard_plan_create");
-  if (rc) return rc;
-  DeviceGuard g;
-  FA_HIP_TRY(hipSetDevice(comm->device));
-  std::vector<fa_tile_desc> t32, t64;
-  rc = layout_tiles(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, flags, &t32, &t64);
-  if (rc) return rc;
+  return fa_shard_plan_create_ex(comm, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, counts,
+                                 nchunks, FA_XCHG_REDUCE, flags, out);
+}
 
-  fa_shard_plan* p = new fa_shard_plan();
-  p->comm = comm;
-  p->f32_numel = f32_numel;
-  p->i64_numel = i64_numel;
-  p->n_local = counts[comm->rank];
-  p->n_total = n_total;
-  p->lo_slot = lo_slot;
-  if (!t32.empty()) {
-    std::vector<size_t> cut;
-    std::vector<int64_t> lo;
-    cut_tiles(t32, nchunks, f32_numel, &cut, &lo);
-    for (int c = 0; c < nchunks; ++c) {
-      if (cut[c] == cut[c + 1]) continue;  // empty trailing group
-      fa_plan* sub = nullptr;
-      rc = fa_plan_create_from_tiles(t32.data() + cut[c], (int)(cut[c + 1] - cut[c]),
-                                     f32_numel, i64_numel, 0, flags, &sub);
-      if (rc) {
-        free_shard(p);
-        return rc;
-      }
-      p->chunk.push_back(sub);
-      // the last non-empty chunk's exchange runs to the end of the bucket
-      p->range.emplace_back(lo[c], lo[c + 1]);
-    }
-    p->range.back().second = f32_numel;
-    hipError_t e = hipMalloc(&p->partial, (size_t)f32_numel * 4);
-    if (e == hipSuccess) e = hipMemset(p->partial, 0, (size_t)f32_numel * 4);
-    if (e != hipSuccess) {
-      free_shard(p);
-      return set_err(FA_E_HIP, "fa_shard_plan_create: %s", hipGetErrorString(e));
-    }
-  }
-  rc = p->i64.init(comm, t64, counts, f32_numel, i64_numel, flags);
-  if (!rc) rc = make_events(&p->ev, p->chunk.size() + 2);
-  if (rc) {
-    free_shard(p);
-    return rc;
-  }
-  *out = p;
-  return FA_OK;
+int fa_shard_plan_create_ex(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
+                            const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
+                            int nchunks, int exchange, unsigned flags, fa_shard_plan** out) {
+  return make_round(comm, FA_MODE_SHARDED, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel,
+                    counts, nchunks, exchange, flags, "fa_shard_plan_create",
+                    (fa_round_plan**)out);
 }
 
 int fa_shard_plan_destroy(fa_shard_plan* p) {
-  free_shard(p);
+  free_round((fa_round_plan*)p);
   return FA_OK;
 }
 
 int fa_reduce_sharded(fa_shard_plan* const* plans, int nlocal, const fa_shard_io* io, int root) {
-  if (nlocal < 1 || !plans || !io) return set_err(FA_E_INVAL, "fa_reduce_sharded: bad arguments");
-  const bool weighted = io[0].weights != nullptr;
-  for (int d = 0; d < nlocal; ++d) {
-    const fa_shard_plan* p = plans[d];
-    if (!p) return set_err(FA_E_INVAL, "fa_reduce_sharded: plan %d is NULL", d);
-    if (root >= p->comm->nranks) return set_err(FA_E_INVAL, "fa_reduce_sharded: root=%d", root);
-    if ((io[d].weights != nullptr) != weighted)
-      return set_err(FA_E_INVAL, "fa_reduce_sharded: weights on some GPUs only");
-    const bool result = root < 0 || root == p->comm->rank;
-    if (p->n_local > 0 && !p->chunk.empty() && !io[d].c32)
-      return set_err(FA_E_INVAL, "fa_reduce_sharded: fp32 buckets required (GPU %d)", d);
-    if (p->n_local > 0 && p->i64.plan && !io[d].c64)
-      return set_err(FA_E_INVAL, "fa_reduce_sharded: int64 buckets required (GPU %d)", d);
-    if (result && ((!p->chunk.empty() && !io[d].out32) || (p->i64.plan && !io[d].out64)))
-      return set_err(FA_E_INVAL, "fa_reduce_sharded: result buckets required on rank %d",
-                     p->comm->rank);
-    if (p->chunk.size() != plans[0]->chunk.size())
-      return set_err(FA_E_INVAL, "fa_reduce_sharded: plans of different layouts");
-  }
-  DeviceGuard g;
-  const size_t nch = plans[0]->chunk.size();
-  for (size_t c = 0; c < nch; ++c) {
-    // partial sums of chunk c on every local GPU, then its exchange
-    for (int d = 0; d < nlocal; ++d) {
-      fa_shard_plan* p = plans[d];
-      hipStream_t s = (hipStream_t)io[d].stream;
-      FA_HIP_TRY(hipSetDevice(p->comm->device));
-      if (p->n_local > 0) {
-        const int rc = fa_reduce(p->chunk[c], io[d].c32, nullptr, p->n_local, io[d].weights,
-                                 p->partial, nullptr, FA_F_SUM_ONLY, s);
-        if (rc) return rc;
-      }
-      FA_HIP_TRY(hipEventRecord(p->ev[c], s));
-      FA_HIP_TRY(hipStreamWaitEvent(p->comm->cs, p->ev[c], 0));
-    }
-    NCCL_TRY(ncclGroupStart());
-    for (int d = 0; d < nlocal; ++d) {
-      fa_shard_plan* p = plans[d];
-      (void)hipSetDevice(p->comm->device);
-      const int64_t lo = p->range[c].first, cnt = p->range[c].second - lo;
-      const bool result = root < 0 || root == p->comm->rank;
-      float* dst = result ? io[d].out32 + lo : p->partial + lo;
-      ncclResult_t r = root < 0
-          ? ncclAllReduce(p->partial + lo, dst, (size_t)cnt, ncclFloat32, ncclSum, p->comm->nc,
-                          p->comm->cs)
-          : ncclReduce(p->partial + lo, dst, (size_t)cnt, ncclFloat32, ncclSum, root,
-                       p->comm->nc, p->comm->cs);
-      if (r != ncclSuccess) {
-        ncclGroupEnd();
-        return set_err(FA_E_COMM, "chunk %zu exchange: %s", c, ncclGetErrorString(r));
-      }
-    }
-    NCCL_TRY(ncclGroupEnd());
-    if (!weighted) {
-      for (int d = 0; d < nlocal; ++d) {
-        fa_shard_plan* p = plans[d];
-        if (!(root < 0 || root == p->comm->rank)) continue;
-        FA_HIP_TRY(hipSetDevice(p->comm->device));
-        const int64_t lo = p->range[c].first, cnt = p->range[c].second - lo;
-        const int rc = fa_div_f32(io[d].out32 + lo, (float)p->n_total, io[d].out32 + lo, cnt,
-                                  p->comm->cs);
-        if (rc) return rc;
-      }
-    }
-  }
-  if (plans[0]->i64.plan) {
-    std::vector<I64Part*> parts;
-    std::vector<const fa_comm*> comms;
-    for (int d = 0; d < nlocal; ++d) {
-      fa_shard_plan* p = plans[d];
-      hipStream_t s = (hipStream_t)io[d].stream;
-      FA_HIP_TRY(hipSetDevice(p->comm->device));
-      int rc = p->i64.stack_local(io[d].c64, p->n_local, s);
-      if (rc) return rc;
-      FA_HIP_TRY(hipEventRecord(p->ev[nch], s));
-      FA_HIP_TRY(hipStreamWaitEvent(p->comm->cs, p->ev[nch], 0));
-      parts.push_back(&p->i64);
-      comms.push_back(p->comm);
-    }
-    int rc = i64_exchange(parts.data(), comms.data(), nlocal);
-    if (rc) return rc;
-    for (int d = 0; d < nlocal; ++d) {
-      fa_shard_plan* p = plans[d];
-      if (!(root < 0 || root == p->comm->rank)) continue;
-      FA_HIP_TRY(hipSetDevice(p->comm->device));
-      rc = fa_reduce(p->i64.plan, nullptr, p->i64.rows.data(), p->n_total, nullptr, nullptr,
-                     io[d].out64, 0, p->comm->cs);
-      if (rc) return rc;
-    }
-  }
-  // the caller's stream joins the communication stream
-  for (int d = 0; d < nlocal; ++d) {
-    fa_shard_plan* p = plans[d];
-    FA_HIP_TRY(hipSetDevice(p->comm->device));
-    hipEvent_t done = p->ev[nch + 1];
-    FA_HIP_TRY(hipEventRecord(done, p->comm->cs));
-    FA_HIP_TRY(hipStreamWaitEvent((hipStream_t)io[d].stream, done, 0));
-  }
-  return FA_OK;
+  return run_round((fa_round_plan* const*)plans, nlocal, io, root, FA_MODE_SHARDED,
+                   "fa_reduce_sharded");
 }
 
 // Stateless form (SURVEY.md §8 b's fa_mean_f32_multi): fp32 segments only,
@@ -555,12 +1151,12 @@ int fa_mean_f32_multi(fa_comm* comm, const float* const* clients, const int* cou
     std::lock_guard<std::mutex> lk(g_multi_mu);
     auto it = g_multi.find(key);
     if (it != g_multi.end()) {
-      plan = it->second;
+      plan = (fa_shard_plan*)it->second;
     } else {
       const int rc = fa_shard_plan_create(comm, segs, nseg, numel, nullptr, 0, 0, counts, 8,
                                           FA_PLAN_GAPS_ARE_PADDING, &plan);
       if (rc) return rc;
-      g_multi[key] = plan;
+      g_multi[key] = (fa_round_plan*)plan;
     }
   }
   fa_shard_io io{};
@@ -574,197 +1170,72 @@ int fa_mean_f32_multi(fa_comm* comm, const float* const* clients, const int* cou
 int fa_stripe_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
                           const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
                           unsigned flags, fa_stripe_plan** out) {
-  if (!out) return set_err(FA_E_INVAL, "fa_stripe_plan_create: out is NULL");
-  *out = nullptr;
-  if (!comm || !counts) return set_err(FA_E_INVAL, "fa_stripe_plan_create: NULL comm/counts");
-  if (!(flags & FA_PLAN_GAPS_ARE_PADDING))
-    return set_err(FA_E_INVAL,
-                   "fa_stripe_plan_create: the layout must allow writes to its padding "
-                   "(FA_PLAN_GAPS_ARE_PADDING): stripe exchanges span it");
-  int n_total = 0, lo_slot = 0;
-  int rc = slot_layout(comm, counts, &n_total, &lo_slot, "fa_stripe_plan_create");
-  if (rc) return rc;
-  DeviceGuard g;
-  FA_HIP_TRY(hipSetDevice(comm->device));
-  std::vector<fa_tile_desc> t32, t64;
-  rc = layout_tiles(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, flags, &t32, &t64);
-  if (rc) return rc;
-
-  fa_stripe_plan* p = new fa_stripe_plan();
-  p->comm = comm;
-  p->f32_numel = f32_numel;
-  p->i64_numel = i64_numel;
-  p->n_local = counts[comm->rank];
-  p->n_total = n_total;
-  p->lo_slot = lo_slot;
-  p->counts.assign(counts, counts + comm->nranks);
-  int s0 = 0;
-  for (int r = 0; r < comm->nranks; ++r) {
-    p->first_slot.push_back(s0);
-    s0 += counts[r];
-  }
-  std::vector<size_t> cut;
-  cut_tiles(t32, comm->nranks, f32_numel, &cut, &p->lo);
-  const int me = comm->rank;
-  const int64_t L = p->lo[me + 1] - p->lo[me];
-  hipError_t e = hipSuccess;
-  if (cut[me] < cut[me + 1]) {
-    rc = fa_plan_create_from_tiles(t32.data() + cut[me], (int)(cut[me + 1] - cut[me]),
-                                   f32_numel, i64_numel, 0, flags, &p->stripe);
-    if (rc) {
-      free_stripe(p);
-      return rc;
-    }
-    // one row per client slot (local rows unused), 256-B aligned rows; the
-    // stripe starts on a 64-float boundary, so (row - lo) stays aligned
-    p->row = (L + 63) / 64 * 64;
-    e = hipMalloc(&p->recv, (size_t)n_total * p->row * 4);
-    if (e == hipSuccess) e = hipMalloc(&p->sbuf, (size_t)p->row * 4);
-    if (e == hipSuccess) e = hipMemset(p->sbuf, 0, (size_t)p->row * 4);
-    for (int k = 0; e == hipSuccess && k < n_total; ++k)
-      p->ptrs.push_back(p->recv + (size_t)k * p->row - p->lo[me]);  // element e at [e - lo]
-  }
-  if (e != hipSuccess) {
-    free_stripe(p);
-    return set_err(FA_E_HIP, "fa_stripe_plan_create: %s", hipGetErrorString(e));
-  }
-  rc = p->i64.init(comm, t64, counts, f32_numel, i64_numel, flags);
-  if (!rc) rc = make_events(&p->ev, 3);
-  if (rc) {
-    free_stripe(p);
-    return rc;
-  }
-  *out = p;
-  return FA_OK;
+  return make_round(comm, FA_MODE_STRIPED, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel,
+                    counts, 1, FA_XCHG_REDUCE, flags, "fa_stripe_plan_create",
+                    (fa_round_plan**)out);
 }
 
 int fa_stripe_plan_destroy(fa_stripe_plan* p) {
-  free_stripe(p);
+  free_round((fa_round_plan*)p);
   return FA_OK;
 }
 
 int fa_reduce_striped(fa_stripe_plan* const* plans, int nlocal, const fa_shard_io* io,
                       int root) {
-  if (nlocal < 1 || !plans || !io) return set_err(FA_E_INVAL, "fa_reduce_striped: bad arguments");
-  for (int d = 0; d < nlocal; ++d) {
-    const fa_stripe_plan* p = plans[d];
-    if (!p) return set_err(FA_E_INVAL, "fa_reduce_striped: plan %d is NULL", d);
-    if (root >= p->comm->nranks) return set_err(FA_E_INVAL, "fa_reduce_striped: root=%d", root);
-    if (io[d].weights)
-      return set_err(FA_E_INVAL, "fa_reduce_striped: the exact mode takes no weights");
-    const bool result = root < 0 || root == p->comm->rank;
-    if (p->n_local > 0 && !io[d].c32)
-      return set_err(FA_E_INVAL, "fa_reduce_striped: fp32 buckets required (GPU %d)", d);
-    if (p->n_local > 0 && p->i64.plan && !io[d].c64)
-      return set_err(FA_E_INVAL, "fa_reduce_striped: int64 buckets required (GPU %d)", d);
-    if (result && (!io[d].out32 || (p->i64.plan && !io[d].out64)))
-      return set_err(FA_E_INVAL, "fa_reduce_striped: result buckets required on rank %d",
-                     p->comm->rank);
-  }
-  DeviceGuard g;
-  // the inputs are ready on the caller's streams
-  for (int d = 0; d < nlocal; ++d) {
-    fa_stripe_plan* p = plans[d];
-    FA_HIP_TRY(hipSetDevice(p->comm->device));
-    FA_HIP_TRY(hipEventRecord(p->ev[0], (hipStream_t)io[d].stream));
-    FA_HIP_TRY(hipStreamWaitEvent(p->comm->cs, p->ev[0], 0));
-  }
-  // 1. every client's values for stripe r go to rank r
-  NCCL_TRY(ncclGroupStart());
-  for (int d = 0; d < nlocal; ++d) {
-    fa_stripe_plan* p = plans[d];
-    (void)hipSetDevice(p->comm->device);
-    const int me = p->comm->rank;
-    const int64_t Lme = p->lo[me + 1] - p->lo[me];
-    for (int r = 0; r < p->comm->nranks; ++r) {
-      if (r == me) continue;
-      const int64_t Lr = p->lo[r + 1] - p->lo[r];
-      ncclResult_t x = ncclSuccess;
-      for (int j = 0; x == ncclSuccess && Lr > 0 && j < p->n_local; ++j)
-        x = ncclSend(io[d].c32[j] + p->lo[r], (size_t)Lr, ncclFloat32, r, p->comm->nc,
-                     p->comm->cs);
-      for (int k = 0; x == ncclSuccess && Lme > 0 && k < p->counts[r]; ++k)
-        x = ncclRecv(p->recv + (size_t)(p->first_slot[r] + k) * p->row, (size_t)Lme,
-                     ncclFloat32, r, p->comm->nc, p->comm->cs);
-      if (x != ncclSuccess) {
-        ncclGroupEnd();
-        return set_err(FA_E_COMM, "stripe exchange: %s", ncclGetErrorString(x));
-      }
-    }
-  }
-  NCCL_TRY(ncclGroupEnd());
-  // 2. each rank reduces its stripe over all n_total clients, exact order
-  for (int d = 0; d < nlocal; ++d) {
-    fa_stripe_plan* p = plans[d];
-    if (!p->stripe) continue;
-    FA_HIP_TRY(hipSetDevice(p->comm->device));
-    std::vector<const float*> src(p->ptrs);
-    for (int j = 0; j < p->n_local; ++j) src[p->lo_slot + j] = io[d].c32[j];
-    const int rc = fa_reduce(p->stripe, src.data(), nullptr, p->n_total, nullptr,
-                             p->sbuf - p->lo[p->comm->rank], nullptr, 0, p->comm->cs);
-    if (rc) return rc;
-  }
-  // 3. the stripes to the result ranks
-  NCCL_TRY(ncclGroupStart());
-  for (int d = 0; d < nlocal; ++d) {
-    fa_stripe_plan* p = plans[d];
-    (void)hipSetDevice(p->comm->device);
-    const int me = p->comm->rank;
-    const bool result = root < 0 || root == me;
-    const int64_t Lme = p->lo[me + 1] - p->lo[me];
-    ncclResult_t x = ncclSuccess;
-    for (int r = 0; x == ncclSuccess && r < p->comm->nranks; ++r) {
-      if (r == me) continue;
-      const int64_t Lr = p->lo[r + 1] - p->lo[r];
-      if (Lme > 0 && (root < 0 || r == root))
-        x = ncclSend(p->sbuf, (size_t)Lme, ncclFloat32, r, p->comm->nc, p->comm->cs);
-      if (x == ncclSuccess && Lr > 0 && result)
-        x = ncclRecv(io[d].out32 + p->lo[r], (size_t)Lr, ncclFloat32, r, p->comm->nc,
-                     p->comm->cs);
-    }
-    if (x != ncclSuccess) {
-      ncclGroupEnd();
-      return set_err(FA_E_COMM, "stripe gather: %s", ncclGetErrorString(x));
-    }
-  }
-  NCCL_TRY(ncclGroupEnd());
-  for (int d = 0; d < nlocal; ++d) {
-    fa_stripe_plan* p = plans[d];
-    const int me = p->comm->rank;
-    const int64_t Lme = p->lo[me + 1] - p->lo[me];
-    if (!(root < 0 || root == me) || Lme == 0) continue;
-    FA_HIP_TRY(hipSetDevice(p->comm->device));
-    FA_HIP_TRY(hipMemcpyAsync(io[d].out32 + p->lo[me], p->sbuf, (size_t)Lme * 4,
-                              hipMemcpyDeviceToDevice, p->comm->cs));
-  }
-  // 4. int64 keys as in e1
-  if (plans[0]->i64.plan) {
-    std::vector<I64Part*> parts;
-    std::vector<const fa_comm*> comms;
-    for (int d = 0; d < nlocal; ++d) {
-      fa_stripe_plan* p = plans[d];
-      FA_HIP_TRY(hipSetDevice(p->comm->device));
-      int rc = p->i64.stack_local(io[d].c64, p->n_local, p->comm->cs);
-      if (rc) return rc;
-      parts.push_back(&p->i64);
-      comms.push_back(p->comm);
-    }
-    int rc = i64_exchange(parts.data(), comms.data(), nlocal);
-    if (rc) return rc;
-    for (int d = 0; d < nlocal; ++d) {
-      fa_stripe_plan* p = plans[d];
-      if (!(root < 0 || root == p->comm->rank)) continue;
-      FA_HIP_TRY(hipSetDevice(p->comm->device));
-      rc = fa_reduce(p->i64.plan, nullptr, p->i64.rows.data(), p->n_total, nullptr, nullptr,
-                     io[d].out64, 0, p->comm->cs);
-      if (rc) return rc;
-    }
-  }
-  for (int d = 0; d < nlocal; ++d) {
-    fa_stripe_plan* p = plans[d];
-    FA_HIP_TRY(hipSetDevice(p->comm->device));
-    FA_HIP_TRY(hipEventRecord(p->ev[2], p->comm->cs));
-    FA_HIP_TRY(hipStreamWaitEvent((hipStream_t)io[d].stream, p->ev[2], 0));
+  return run_round((fa_round_plan* const*)plans, nlocal, io, root, FA_MODE_STRIPED,
+                   "fa_reduce_striped");
+}
+
+// =========================================================== chained ======
+int fa_chain_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
+                         const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
+                         int nchunks, unsigned flags, fa_chain_plan** out) {
+  return make_round(comm, FA_MODE_CHAINED, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel,
+                    counts, nchunks, FA_XCHG_REDUCE, flags, "fa_chain_plan_create",
+                    (fa_round_plan**)out);
+}
+
+int fa_chain_plan_destroy(fa_chain_plan* p) {
+  free_round((fa_round_plan*)p);
+  return FA_OK;
+}
+
+int fa_reduce_chained(fa_chain_plan* const* plans, int nlocal, const fa_shard_io* io, int root) {
+  return run_round((fa_round_plan* const*)plans, nlocal, io, root, FA_MODE_CHAINED,
+                   "fa_reduce_chained");
+}
+
+// ====================================================== host-only view =====
+int fa_describe_round(int mode, int nranks, int rank, const int* counts, const fa_seg* seg32,
+                      int nseg32, int64_t f32_numel, const fa_seg* seg64, int nseg64,
+                      int64_t i64_numel, int nchunks, int exchange, unsigned flags, int root,
+                      int weighted, fa_xfer* ops, int cap, int* nops) {
+  if (!nops) return set_err(FA_E_INVAL, "fa_describe_round: nops is NULL");
+  *nops = 0;
+  if (mode != FA_MODE_SHARDED && mode != FA_MODE_STRIPED && mode != FA_MODE_CHAINED)
+    return set_err(FA_E_INVAL, "fa_describe_round: mode %d", mode);
+  if (nchunks == 0) nchunks = 8;
+  if (nchunks < 1 || nchunks > FA_COMM_MAX_CHUNKS)
+    return set_err(FA_E_INVAL, "fa_describe_round: nchunks=%d", nchunks);
+  if (exchange != FA_XCHG_REDUCE && exchange != FA_XCHG_RS_GATHER)
+    return set_err(FA_E_INVAL, "fa_describe_round: exchange %d", exchange);
+  if (root >= nranks) return set_err(FA_E_INVAL, "fa_describe_round: root=%d", root);
+  fa_round_plan p;
+  p.mode = mode;
+  p.xchg = exchange;
+  int rc = make_geo(nranks, rank, counts, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel,
+                    flags, "fa_describe_round", &p.g);
+  if (rc) return rc;
+  std::vector<fa_tile_desc> vec, tails;
+  std::vector<size_t> cut;
+  std::vector<int64_t> tidx;
+  build_round(&p, nchunks, &vec, &cut, &tails, &tidx);
+  const std::vector<fa_xfer>& s = schedule(&p, root, weighted != 0);
+  *nops = (int)s.size();
+  if (ops) {
+    if (cap < (int)s.size())
+      return set_err(FA_E_RANGE, "fa_describe_round: %d ops, capacity %d", (int)s.size(), cap);
+    std::copy(s.begin(), s.end(), ops);
   }
   return FA_OK;
 }

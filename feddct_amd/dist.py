@@ -1,29 +1,36 @@
-"""Client-sharded aggregation across the GPUs of one node.
+"""Aggregation across the GPUs of one node (SURVEY.md §8 e) over
+torch.distributed (backend "nccl" = RCCL over xGMI), one process per GPU.
+Rank r holds a contiguous shard of the client slots, in slot order
+(``shard_range``).  Three round forms:
 
-One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).
-Rank r holds a contiguous shard of the client slots.  A round is:
+* ``ShardedAggregator`` (e1, the north_star's partitioning): the HIP kernel
+  sums the rank's clients in the torch order without the /N
+  (FA_F_SUM_ONLY), chunk by column chunk; each chunk's partial bucket is
+  summed across ranks by an RCCL reduce to the server rank (``final=
+  "reduce"``) or an all-reduce (``"allreduce"``) while the kernel sums the
+  next chunk; then ``/ N_total``.  The cross-rank sum re-associates fp32:
+  NOT bit-identical to the single-process reference (bench.py reports the
+  ULP distance);
+* ``ChainAggregator`` (exact client shards): the shards stay put and the
+  cascade's accumulator state travels rank to rank in slot order, chunk by
+  chunk (fa_reduce_chain); the scalar columns are all-gathered raw.
+  Bit-identical;
+* ``StripedAggregator`` (e2, exact column stripes): every client's values
+  for rank r's column stripe go to rank r, which reduces the stripe over all
+  clients.  Bit-identical.
 
-1. local partial: the HIP kernel sums the rank's clients for every fp32 key
-   in the torch order, without the /N (FA_F_SUM_ONLY);
-2. exchange: ``all_reduce(SUM)`` of the partial bucket over RCCL — every rank
-   needs the global model afterwards to reload its own client slots, so the
-   "final reduce" of the north_star is an all-reduce; the bucket is cut into
-   chunks at key boundaries and chunk c's all-reduce (RCCL's own stream) runs
-   while the kernel sums chunk c+1;
-3. finish: ``/ N_total`` (IEEE division, fa_div_f32).
+int64 keys (a few bytes) always travel raw — an all-gather of every rank's
+int64 buckets — and are reduced exactly over all N_total clients.
 
-int64 keys (a few bytes) are exchanged raw — an all-gather of every rank's
-int64 buckets — and reduced exactly over all N_total clients by the same
-kernel, so they match the single-process reference bit-for-bit.
-
-The fp32 result is the exact torch-order sum within each shard, but the
-cross-rank all-reduce re-associates it: it is NOT bit-identical to the
-single-process reference (bench.py reports the max ULP distance).  The exact
-element-sharded mode (§8 e2) is listed under "next" in DESIGN.md.
+Point-to-point exchanges run in pairwise rounds (``pair_rounds``): in every
+round each rank meets one partner, and the lower rank of a pair sends
+first, so a transport that serialises a rank's sends and receives (gloo)
+cannot stall.  The native library (libfedagg_comm.so) runs the same rounds
+(tests/test_schedule.py checks they agree).
 
 The arithmetic backends are pluggable so the orchestration is testable on
 CPU with gloo (tests/test_dist_gloo.py injects oracle backends); the product
-backend is ``HipBackend``.
+backends are the Hip* classes.
 """
 from __future__ import annotations
 
@@ -42,6 +49,44 @@ def shard_range(n_total: int, world: int, rank: int):
     base, rem = divmod(n_total, world)
     lo = rank * base + min(rank, rem)
     return lo, lo + base + (1 if rank < rem else 0)
+
+
+def partner(world: int, rank: int, t: int) -> int:
+    """Rank ``rank``'s partner in round ``t`` of the circle-method pairing
+    (or -1: sits out), as fedcomm.hip's ``partner``."""
+    m = world + 1 if world % 2 else world
+    if m < 2:
+        return -1
+    k = m - 1
+    if rank == k:
+        q = next(i for i in range(k) if (2 * i) % k == t % k)
+    elif (2 * rank) % k == t % k:
+        q = k
+    else:
+        q = (t - rank) % k
+    return -1 if q >= world else q
+
+
+def pair_rounds(world: int, rank: int):
+    """The partners of ``rank``, one per round, every other rank once."""
+    rounds = world if world % 2 else world - 1
+    return [p for p in (partner(world, rank, t) for t in range(rounds)) if p >= 0 and p != rank]
+
+
+def stripe_p2p_schedule(ranges, shards, me):
+    """The striped round's client exchange for rank ``me``: ("send", peer,
+    slot, offset, count) / ("recv", peer, slot, offset, count) in issue order
+    (pairwise rounds; the lower rank of a pair sends first).  ``ranges[r]`` =
+    rank r's column stripe, ``shards[r]`` = its slot range."""
+    out = []
+    lo_me, hi_me = ranges[me]
+    for r in pair_rounds(len(ranges), me):
+        lo, hi = ranges[r]
+        sends = [("send", r, k, lo, hi - lo) for k in range(*shards[me])] if hi > lo else []
+        recvs = ([("recv", r, k, lo_me, hi_me - lo_me) for k in range(*shards[r])]
+                 if hi_me > lo_me else [])
+        out += sends + recvs if me < r else recvs + sends
+    return out
 
 
 def chunk_segments(layout: BucketLayout, nchunks: int):
@@ -264,19 +309,20 @@ class StripedAggregator:
     def _peer(self, r):
         return r if self.group is None else dist.get_global_rank(self.group, r)
 
-    def _gather_stripes(self, ops):
+    def _gather_stripes(self):
         """Finished stripes of out32 to every other rank ("allreduce") or to
-        the root only ("reduce"), P2P straight into out32 views."""
+        the root only ("reduce"), P2P straight into out32 views, one partner
+        per round (the lower rank sends first)."""
         me = self.rank
-        for r in range(self.world):
-            if r == me:
-                continue
+        for r in pair_rounds(self.world, me):
             lo, hi = self.ranges[r]
+            sends, recvs = [], []
             if self.hi > self.lo and (self.final == "allreduce" or r == self.root):
-                ops.append(dist.P2POp(dist.isend, self.out32[self.lo:self.hi], self._peer(r),
-                                      self.group))
+                sends.append(dist.P2POp(dist.isend, self.out32[self.lo:self.hi], self._peer(r),
+                                        self.group))
             if hi > lo and (self.final == "allreduce" or me == self.root):
-                ops.append(dist.P2POp(dist.irecv, self.out32[lo:hi], self._peer(r), self.group))
+                recvs.append(dist.P2POp(dist.irecv, self.out32[lo:hi], self._peer(r), self.group))
+            self._run(sends + recvs if me < r else recvs + sends)
 
     def _run(self, ops):
         if ops:
@@ -291,24 +337,29 @@ class StripedAggregator:
         dist.all_gather_into_tensor(self.gather64, self.stack64, group=self.group)
         self.backend.reduce_i64([self.gather64[r] for r in self.rows64], self.out64)
 
+    def p2p_schedule(self):
+        """This rank's client exchange, in issue order (stripe_p2p_schedule)."""
+        return stripe_p2p_schedule(self.ranges, self.shards, self.rank)
+
     def step_device(self, local32: List[torch.Tensor], local64: List[torch.Tensor]) -> None:
         me = self.rank
         a, b = self.shards[me]
         assert len(local32) == b - a
-        ops = []
-        for r in range(self.world):
-            if r == me:
-                continue
-            lo, hi = self.ranges[r]
-            if hi > lo:
-                for t in local32:
-                    ops.append(dist.P2POp(dist.isend, t[lo:hi], self._peer(r), self.group))
-            qa, qb = self.shards[r]
-            if self.hi > self.lo:
-                for k in range(qa, qb):
-                    ops.append(dist.P2POp(dist.irecv, self.recv[k, :self.hi - self.lo],
-                                          self._peer(r), self.group))
-        self._run(ops)
+        sched = self.p2p_schedule()
+        i = 0
+        while i < len(sched):   # one partner (round) at a time
+            peer = sched[i][1]
+            ops = []
+            while i < len(sched) and sched[i][1] == peer:
+                kind, _, slot, off, cnt = sched[i]
+                if kind == "send":
+                    ops.append(dist.P2POp(dist.isend, local32[slot - a][off:off + cnt],
+                                          self._peer(peer), self.group))
+                else:
+                    ops.append(dist.P2POp(dist.irecv, self.recv[slot, :cnt], self._peer(peer),
+                                          self.group))
+                i += 1
+            self._run(ops)
         sources = []
         for k in range(self.n_total):
             if a <= k < b:
@@ -317,9 +368,7 @@ class StripedAggregator:
                 sources.append((self.recv[k], self.lo))
         self.backend.reduce_stripe(sources, self.out32)
         self._i64(local64)
-        ops = []
-        self._gather_stripes(ops)
-        self._run(ops)
+        self._gather_stripes()
 
     def step_host(self, stripes32: Sequence[torch.Tensor], clients64: Sequence[torch.Tensor],
                   local64: Optional[List[torch.Tensor]] = None) -> None:
@@ -333,6 +382,198 @@ class StripedAggregator:
         if self.layout.i64_numel:
             g = torch.stack([t.to(self.out64.device, non_blocking=True) for t in clients64])
             self.backend.reduce_i64(list(g.unbind(0)), self.out64)
-        ops = []
-        self._gather_stripes(ops)
-        self._run(ops)
+        self._gather_stripes()
+
+
+# --------------------------------------------------------------------------
+# Exact client shards: the cascade state travels (fa_reduce_chain).
+# --------------------------------------------------------------------------
+def chain_levels(rows: int, n_total: int) -> int:
+    """Bit l: state plane l may be nonzero after ``rows`` of ``n_total`` rows
+    (fa_chain_levels; the cascade's level step is 16 below 2**16 clients)."""
+    if rows <= 0:
+        return 0
+    lp = max(4, (int(n_total - 1).bit_length() if n_total > 1 else 0) // 4)
+    step = 1 << lp
+    m = 0
+    if rows % step:
+        m |= 1
+    if (rows >> lp) % step:
+        m |= 2
+    if n_total >= 256:
+        if (rows >> (2 * lp)) % step:
+            m |= 4
+        if rows >> (3 * lp):
+            m |= 8
+    return m
+
+
+class HipChainBackend:
+    """fa_reduce_chain over the vector-tile chunks; the raw scalar columns
+    (compact tail plan + int64 plan) reduced with fa_reduce."""
+
+    def __init__(self, layout: BucketLayout, chunks, compact, tidx, t64):
+        from . import _lib
+        self._lib = _lib
+        self.layout = layout
+        self.plans = [_lib.Plan(None, layout.f32_numel, None, 0, 0, tiles=t) for _, _, t in chunks]
+        T = len(tidx)
+        self.plan_t32 = _lib.Plan(None, T, None, 0, 0, tiles=compact) if T else None
+        self.plan64 = (_lib.Plan(None, layout.f32_numel, None, layout.i64_numel, 0, tiles=t64)
+                       if len(t64) else None)
+        self.tout = None
+
+    def _s(self):
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def chain(self, c, clients32, row0, n_total, state, state_in, out, plane, weights=None):
+        L = self._lib
+        ch = L.FaChain(row0, n_total, state.data_ptr() if state_in else None,
+                       None if out is not None else state.data_ptr(), plane)
+        w = None if weights is None else (ctypes.c_float * len(weights))(*map(float, weights))
+        L.check(L.lib.fa_reduce_chain(self.plans[c].handle,
+                                      L.ptr_array([t.data_ptr() for t in clients32]),
+                                      len(clients32), w, ctypes.byref(ch),
+                                      out.data_ptr() if out is not None else None, 0, self._s()),
+                "fa_reduce_chain")
+
+    def tails(self, rows32, tidx, out32, weighted):
+        L = self._lib
+        if self.tout is None:
+            self.tout = torch.zeros(max(64, -(-len(tidx) // 64) * 64), device=out32.device)
+        L.check(L.lib.fa_reduce(self.plan_t32.handle, L.ptr_array([r.data_ptr() for r in rows32]),
+                                None, len(rows32), None, self.tout.data_ptr(), None,
+                                L.FA_F_SUM_ONLY if weighted else 0, self._s()), "fa_reduce(tails)")
+        out32[tidx] = self.tout[:len(tidx)]
+
+    def reduce_i64(self, clients64, out64):
+        if self.plan64 is None:
+            return
+        L = self._lib
+        L.check(L.lib.fa_reduce(self.plan64.handle, None,
+                                L.ptr_array([t.data_ptr() for t in clients64]), len(clients64),
+                                None, None, out64.data_ptr(), 0, self._s()), "fa_reduce(i64)")
+
+
+class ChainAggregator:
+    """Exact client-sharded round over torch.distributed (the Python form of
+    the native fa_reduce_chained; same cut, same hops, same tails).
+
+    Rank r holds slots ``shards[r]`` (contiguous, slot order).  Per vector
+    column chunk, rank r receives the cascade state after slots
+    0..first[r]-1 from rank r-1, continues it over its own clients
+    (fa_reduce_chain) and sends it on to rank r+1; the last rank holding
+    clients finishes the mean.  Only the state planes chain_levels() names
+    travel — one float per element below 16 slots, two below 256.  The
+    scalar columns (ILP-4 tails, M==1) and int64 keys are all-gathered raw and
+    reduced by the result ranks.  ``final="reduce"``: the result on ``root``;
+    ``"allreduce"``: on every rank (a broadcast from the finisher)."""
+
+    def __init__(self, layout: BucketLayout, n_total: int, out32: torch.Tensor,
+                 out64: torch.Tensor, group=None, backend=None, final: str = "reduce",
+                 root: int = 0, nchunks: int = 16, counts: Optional[Sequence[int]] = None):
+        from .partition import chain_cut
+        if final not in ("reduce", "allreduce"):
+            raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
+        self.layout, self.n_total = layout, n_total
+        self.out32, self.out64 = out32, out64
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.root = root if final == "reduce" else -1
+        if counts is None:
+            counts = [b - a for a, b in (shard_range(n_total, self.world, r)
+                                         for r in range(self.world))]
+        self.counts = list(counts)
+        self.first = [sum(self.counts[:r]) for r in range(self.world)]
+        self.finisher = max(r for r in range(self.world) if self.counts[r] > 0)
+        self.chunks, compact, tidx, t64 = chain_cut(layout, nchunks)
+        dev = out32.device
+        self.tidx = torch.from_numpy(tidx).to(dev)
+        self.T = len(tidx)
+        self.trow = -(-self.T // 64) * 64
+        self.backend = backend or HipChainBackend(layout, self.chunks, compact, tidx, t64)
+        self.plane = -(-layout.f32_numel // 64) * 64
+        nplanes = 4 if n_total >= 256 else 2
+        self.state = torch.zeros(nplanes * self.plane, dtype=torch.float32, device=dev)
+        me = self.rank
+        self.lev_in = chain_levels(self.first[me], n_total)
+        self.lev_out = chain_levels(self.first[me] + self.counts[me], n_total)
+        self.fin = (torch.zeros_like(out32) if me == self.finisher and self.root >= 0
+                    and self.root != me else None)
+        nmax = max(self.counts)
+        self.nmax = nmax
+        self.stack32 = torch.zeros((nmax, max(self.trow, 1)), dtype=torch.float32, device=dev)
+        self.gather32 = torch.zeros((self.world * nmax, max(self.trow, 1)), dtype=torch.float32,
+                                    device=dev)
+        w64 = max(1, layout.i64_numel)
+        self.stack64 = torch.zeros((nmax, w64), dtype=torch.int64, device=dev)
+        self.gather64 = torch.zeros((self.world * nmax, w64), dtype=torch.int64, device=dev)
+        self.rows = [r * nmax + j for r in range(self.world) for j in range(self.counts[r])]
+
+    def _peer(self, r):
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def _planes(self, lev, lo, hi):
+        return [self.state[l * self.plane + lo:l * self.plane + hi] for l in range(4)
+                if lev & (1 << l)]
+
+    def step(self, local32: List[torch.Tensor], local64: List[torch.Tensor],
+             weights: Optional[Sequence[float]] = None) -> None:
+        me, F = self.rank, self.finisher
+        n_loc = self.counts[me]
+        assert len(local32) == n_loc
+        result = self.root < 0 or self.root == me
+        # the raw scalar columns: stacked, gathered while the chain runs
+        if self.T:
+            for j, t in enumerate(local32):
+                v = t[self.tidx]
+                if weights is not None:
+                    v = v * torch.tensor(float(np.float32(weights[j])), device=v.device)
+                self.stack32[j, :self.T] = v
+        for j, t in enumerate(local64):
+            self.stack64[j].copy_(t)
+        gw = []
+        if self.T:
+            gw.append(dist.all_gather_into_tensor(self.gather32, self.stack32, group=self.group,
+                                                  async_op=True))
+        if self.layout.i64_numel:
+            gw.append(dist.all_gather_into_tensor(self.gather64, self.stack64, group=self.group,
+                                                  async_op=True))
+        for w in gw:   # (gloo runs collectives and P2P on one thread: finish first)
+            w.wait()
+        # the chain
+        sends = []
+        if me <= F:
+            pred = me > 0 and self.lev_in
+            succ = me < F and self.lev_out
+            dst = None if me < F else (self.out32 if result else self.fin)
+            for c, (lo, hi, _) in enumerate(self.chunks):
+                if pred:
+                    for req in dist.batch_isend_irecv(
+                            [dist.P2POp(dist.irecv, p, self._peer(me - 1), self.group)
+                             for p in self._planes(self.lev_in, lo, hi)]):
+                        req.wait()
+                if n_loc:
+                    self.backend.chain(c, local32, self.first[me], self.n_total, self.state,
+                                       bool(pred), dst, self.plane, weights)
+                if succ:
+                    sends += dist.batch_isend_irecv(
+                        [dist.P2POp(dist.isend, p, self._peer(me + 1), self.group)
+                         for p in self._planes(self.lev_out, lo, hi)])
+        for req in sends:
+            req.wait()
+        if self.chunks:
+            lo, hi = self.chunks[0][0], self.chunks[-1][1]
+            if self.root < 0:
+                dist.broadcast(self.out32[lo:hi], src=self._peer(F), group=self.group)
+            elif self.root != F:
+                if me == F:
+                    dist.send(self.fin[lo:hi], self._peer(self.root), group=self.group)
+                elif me == self.root:
+                    dist.recv(self.out32[lo:hi], self._peer(F), group=self.group)
+        if result:
+            if self.T:
+                self.backend.tails([self.gather32[r] for r in self.rows], self.tidx, self.out32,
+                                   weights is not None)
+            self.backend.reduce_i64([self.gather64[r] for r in self.rows], self.out64)

@@ -33,6 +33,24 @@ def layout_tiles(layout: BucketLayout, tile_elems: int = 0):
                          layout.segs64.tobytes(), layout.i64_numel, tile_elems)
 
 
+def cut_index(t: np.ndarray, parts: int) -> List[int]:
+    """Group boundaries (tile indices, len parts+1) of the sorted tiles ``t``
+    into ``parts`` runs of about equal element count, cut only before a
+    vector tile on a 256-B boundary — fedcomm.hip's cut_tiles, the same rule
+    the native schedules use."""
+    total = int(t[:, 1].sum()) if len(t) else 0
+    cut = [0]
+    acc = 0
+    for i, (s, c, kind) in enumerate(t):
+        k = len(cut)
+        if k < parts and i > 0 and acc >= total * k // parts and kind == 0 and s % 64 == 0:
+            cut.append(i)
+        acc += int(c)
+    while len(cut) < parts + 1:
+        cut.append(len(t))
+    return cut
+
+
 def split_tiles(tiles: np.ndarray, parts: int, f32_numel: int
                 ) -> List[Tuple[int, int, np.ndarray]]:
     """Cut the fp32 tiles into ``parts`` contiguous ranges of about equal
@@ -40,17 +58,9 @@ def split_tiles(tiles: np.ndarray, parts: int, f32_numel: int
     [0, f32_numel) exactly (some ranges may be empty)."""
     t32 = tiles[tiles[:, 2] < K_I64_MIN]
     t32 = t32[np.argsort(t32[:, 0], kind="stable")]
-    total = int(t32[:, 1].sum()) if len(t32) else 0
-    cuts = [0]
-    acc = 0
-    k = 1
-    for s, c, kind in t32:
-        if k < parts and kind == 0 and acc >= total * k / parts and s > cuts[-1]:
-            cuts.append(int(s))
-            k += 1
-        acc += int(c)
-    while len(cuts) < parts:
-        cuts.append(f32_numel)
+    ci = cut_index(t32, parts)
+    cuts = [0] + [int(t32[ci[g], 0]) if ci[g] < len(t32) else f32_numel
+                  for g in range(1, parts)]
     cuts.append(f32_numel)
     out = []
     for i in range(parts):
@@ -79,3 +89,27 @@ def range_plans(layout: BucketLayout, parts: int, tile_elems: int = 0, flags=Non
     p64 = (_lib.Plan(None, layout.f32_numel, None, layout.i64_numel, te, flags, tiles=t64)
            if len(t64) else None)
     return out, p64
+
+
+def chain_cut(layout: BucketLayout, nchunks: int):
+    """The chained round's cut (fedcomm.hip chain_geo): the vector (cascade)
+    tiles in ``nchunks`` column chunks [(lo, hi, tiles)], empty ones dropped;
+    the scalar fp32 tiles re-based to compact columns (tiles, and the bucket
+    index of each compact column); the int64 tiles."""
+    _, tiles = layout_tiles(layout)
+    t32 = tiles[tiles[:, 2] < K_I64_MIN]
+    t32 = t32[np.argsort(t32[:, 0], kind="stable")]
+    vec = t32[t32[:, 2] == 0]
+    sc = t32[t32[:, 2] != 0]
+    ci = cut_index(vec, nchunks)
+    chunks = []
+    for g in range(nchunks):
+        if ci[g] == ci[g + 1]:
+            continue
+        sel = vec[ci[g]:ci[g + 1]]
+        chunks.append((int(sel[0, 0]), int(sel[-1, 0] + sel[-1, 1]), sel))
+    tidx = (np.concatenate([np.arange(s, s + c) for s, c, _ in sc]) if len(sc)
+            else np.zeros(0, np.int64))
+    starts = np.concatenate([[0], np.cumsum(sc[:, 1])[:-1]]) if len(sc) else np.zeros(0, np.int64)
+    compact = np.stack([starts, sc[:, 1], sc[:, 2]], 1) if len(sc) else np.zeros((0, 3), np.int64)
+    return chunks, compact, tidx, i64_tiles(tiles)

@@ -128,6 +128,108 @@ int fa_stripe_plan_destroy(fa_stripe_plan *plan);
 int fa_reduce_striped(fa_stripe_plan *const *plans, int nlocal,
                       const fa_shard_io *io, int root);
 
+/* ---- e1 exchange options ---------------------------------------------------
+ * FA_XCHG_REDUCE     : per chunk, one ncclReduce (root) / ncclAllReduce.
+ * FA_XCHG_RS_GATHER  : per chunk, an in-place ncclReduceScatter (each rank
+ *                      sums 1/W of the chunk) then ncclGather to the root /
+ *                      ncclAllGather — every rank's links carry the exchange,
+ *                      not one ring's; the chunk's last len % W floats take
+ *                      the plain reduce.  Same arithmetic class as REDUCE
+ *                      (re-associated across ranks). */
+#define FA_XCHG_REDUCE 0
+#define FA_XCHG_RS_GATHER 1
+int fa_shard_plan_create_ex(fa_comm *comm, const fa_seg *seg32, int nseg32,
+                            int64_t f32_numel, const fa_seg *seg64, int nseg64,
+                            int64_t i64_numel, const int *counts, int nchunks,
+                            int exchange, unsigned flags, fa_shard_plan **out);
+
+/* ---- chained mode: client shards, exact order (fedagg.h fa_reduce_chain) ---
+ * The client slots stay sharded as in e1 (rank r holds counts[r] slots, in
+ * slot order), but instead of partial sums the cascade's accumulator STATE
+ * travels: rank r continues rank r-1's state over its own clients, column
+ * chunk by column chunk, and hands it to rank r+1 (ncclSend/ncclRecv of the
+ * fa_chain_levels planes: one or two floats per element for N < 256), so
+ * chunk c's hop overlaps chunk c+1's reduction.  The last rank holding
+ * clients (the finisher) finishes the sum; the result then goes to `root`
+ * (one send; none when root is the finisher) or to every rank (root < 0:
+ * ncclBroadcast).  The scalar columns (ILP-4 tails, M==1 keys: a few hundred
+ * floats) and the int64 keys are all-gathered raw and reduced in their own
+ * orders by the result ranks (weighted: the fp32 rows are pre-multiplied).
+ * The result is bit-identical to one GPU's fa_reduce over all clients, for
+ * any counts.  Per hop: (1-2) * 4 B per vector element (4 planes for
+ * N >= 256); no all-to-all of client state. */
+typedef struct fa_chain_plan fa_chain_plan;
+int fa_chain_plan_create(fa_comm *comm, const fa_seg *seg32, int nseg32,
+                         int64_t f32_numel, const fa_seg *seg64, int nseg64,
+                         int64_t i64_numel, const int *counts, int nchunks,
+                         unsigned flags, fa_chain_plan **out);
+int fa_chain_plan_destroy(fa_chain_plan *plan);
+int fa_reduce_chained(fa_chain_plan *const *plans, int nlocal,
+                      const fa_shard_io *io, int root);
+
+/* ---- schedules, host-only -------------------------------------------------
+ * Every round above runs a schedule: a list of operations per rank, built on
+ * the host from the layout, the counts and the rank.  fa_describe_round
+ * returns rank `rank`'s list exactly as the executor issues it — no GPU, no
+ * communicator — so the multi-rank schedules can be checked (and replayed)
+ * on a CPU.  Ops with the same `step` are issued together: the exchanges of
+ * a step form one RCCL group; a step's kernels follow its exchanges.
+ * Offsets are bucket element offsets for CLIENT / OUT / PARTIAL / RECV /
+ * STRIPE / STATE / FIN buffers, and element offsets into the stack for
+ * STACK / GATHER (index 0: fp32 scalar columns, 1: int64 keys). */
+#define FA_MODE_SHARDED 0
+#define FA_MODE_STRIPED 1
+#define FA_MODE_CHAINED 2
+
+#define FA_X_SEND 1           /* ncclSend of src[offset, +count) to peer         */
+#define FA_X_RECV 2           /* ncclRecv into dst[offset, +count) from peer     */
+#define FA_X_REDUCE 3         /* ncclReduce to root `peer`                       */
+#define FA_X_ALLREDUCE 4
+#define FA_X_REDUCE_SCATTER 5 /* in place: rank r's sum at offset + r*count/W    */
+#define FA_X_GATHER 6         /* every rank's count/W share to root `peer`       */
+#define FA_X_ALLGATHER 7
+#define FA_X_BCAST 8          /* from root `peer`                                */
+#define FA_X_K_SUM 16         /* partial sum of the local clients, chunk `chunk`  */
+#define FA_X_K_ZERO 17        /* zero dst[offset, +count) (a rank with no client) */
+#define FA_X_K_DIV 18         /* dst[offset, +count) /= n_total                  */
+#define FA_X_K_COPY 19
+#define FA_X_K_STRIPE 20      /* this rank's stripe over all n_total clients     */
+#define FA_X_K_CHAIN 21       /* fa_reduce_chain: rows row0..row0+nrows-1        */
+#define FA_X_K_STACK 22       /* local clients' scalar columns / int64 keys      */
+#define FA_X_K_TAILS 23       /* reduce the gathered rows into the result        */
+
+#define FA_B_NONE 0
+#define FA_B_CLIENT 1         /* local client src_index's fp32 bucket            */
+#define FA_B_OUT 2            /* the result buckets                              */
+#define FA_B_PARTIAL 4        /* e1 partial sums                                 */
+#define FA_B_RECV 5           /* e2 receive row of client slot `index`           */
+#define FA_B_STRIPE 6         /* e2 this rank's reduced stripe                   */
+#define FA_B_STATE 7          /* chained: cascade state plane `index`            */
+#define FA_B_FIN 8            /* chained: the finisher's result (not a result rank) */
+#define FA_B_STACK 9          /* raw scalar columns, this rank's rows            */
+#define FA_B_GATHER 10        /* ... every rank's rows                           */
+
+typedef struct fa_xfer {
+  int32_t step;
+  int32_t op;        /* FA_X_*                                                 */
+  int32_t peer;      /* p2p: the other rank; rooted collectives: the root      */
+  int32_t chunk;     /* kernels: chunk (chained/e1) or stripe (e2); else -1    */
+  int32_t src, src_index; /* FA_B_* read, and its client / slot / plane index  */
+  int32_t dst, dst_index; /* FA_B_* written                                    */
+  int64_t offset;
+  int64_t count;
+  int32_t row0;      /* kernels: first client slot reduced                     */
+  int32_t nrows;     /* kernels: clients reduced                               */
+} fa_xfer;
+
+/* mode FA_MODE_*; exchange FA_XCHG_* (e1 only); root as in the run call;
+ * weighted != 0: the schedule of a weighted round.  ops == NULL: only *nops. */
+int fa_describe_round(int mode, int nranks, int rank, const int *counts,
+                      const fa_seg *seg32, int nseg32, int64_t f32_numel,
+                      const fa_seg *seg64, int nseg64, int64_t i64_numel,
+                      int nchunks, int exchange, unsigned flags, int root,
+                      int weighted, fa_xfer *ops, int cap, int *nops);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,7 +46,7 @@ class StateModule(torch.nn.Module):
                     mod.add_module(p, torch.nn.Module())
                 mod = mod._modules[p]
             t = torch.zeros(e["shape"], dtype=getattr(torch, e["dtype"]))
-            if e["dtype"] in ("int64", "int32", "bool", "uint8"):
+            if not (t.is_floating_point() or t.is_complex()):
                 mod.register_buffer(parts[-1], t)
             else:
                 mod.register_parameter(parts[-1], torch.nn.Parameter(t))

@@ -218,3 +218,115 @@ def test_striped_round_is_exact_gloo(world, n_total, host, final):
             got = src[s.offset:s.offset + s.numel].reshape(s.shape)
             want = exact[s.key]
             assert got.tobytes() == np.asarray(want).tobytes(), s.key
+
+
+# ------------------------------------------- exact client shards (chained) --
+class OracleChainBackend:
+    """The chained kernels restated with the oracle (cascade_state)."""
+
+    def __init__(self, layout, chunks, compact):
+        self.layout, self.chunks, self.compact = layout, chunks, compact
+
+    def chain(self, c, clients32, row0, n_total, state, state_in, out, plane, weights=None):
+        lev_in = O.chain_levels(row0, n_total)
+        lev_out = O.chain_levels(row0 + len(clients32), n_total)
+        for st, cnt, _ in self.chunks[c][2]:
+            rows = []
+            for j, t in enumerate(clients32):
+                v = t[st:st + cnt].numpy()
+                if weights is not None:
+                    v = (v * np.float32(weights[j])).astype(np.float32)
+                rows.append(v)
+            acc = None
+            if state_in:
+                acc = [state[l * plane + st:l * plane + st + cnt].numpy().copy()
+                       if lev_in & (1 << l) else np.zeros(cnt, np.float32) for l in range(4)]
+            acc = O.cascade_state(rows, row0, n_total, acc)
+            if out is None:
+                for l in range(4):
+                    if lev_out & (1 << l):
+                        state[l * plane + st:l * plane + st + cnt] = torch.from_numpy(acc[l])
+            else:
+                s = O.cascade_finish(acc)
+                if weights is None:
+                    s = (s / np.float32(n_total)).astype(np.float32)
+                out[st:st + cnt] = torch.from_numpy(s)
+
+    def tails(self, rows32, tidx, out32, weighted):
+        from schedsim import _column_sum
+        n = len(rows32)
+        for cs, cnt, kind in self.compact:
+            res = _column_sum(kind, [r[cs:cs + cnt].numpy() for r in rows32])
+            res = (np.float32(0) + res).astype(np.float32)
+            if not weighted:
+                res = (res / np.float32(n)).astype(np.float32)
+            out32[tidx[cs:cs + cnt]] = torch.from_numpy(res)
+
+    def reduce_i64(self, clients64, out):
+        for o, m in self.layout.segs64:
+            x = np.stack([t[o:o + m].numpy() for t in clients64])
+            out[o:o + m] = torch.from_numpy(O.mean_i64_trunc(x))
+
+
+def _chain_worker(rank, world, port, counts, final, weighted, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from feddct_amd.dist import ChainAggregator
+    from feddct_amd.partition import chain_cut
+    layout = BucketLayout.from_manifest(MAN)
+    n_total = sum(counts)
+    a = sum(counts[:rank])
+    bk = [_bucket(layout, synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL))
+          for c in range(a, a + counts[rank])]
+    out32 = torch.full((layout.f32_numel,), float("nan"))
+    out64 = torch.full((max(1, layout.i64_numel),), -7, dtype=torch.int64)
+    chunks, compact, tidx, _ = chain_cut(layout, 3)
+    w = O.weights_from_sizes(np.arange(1, n_total + 1) * 3 + 2) if weighted else None
+    agg = ChainAggregator(layout, n_total, out32, out64, backend=OracleChainBackend(
+        layout, chunks, compact), final=final, nchunks=3, counts=counts)
+    agg.step([x[0] for x in bk], [x[1] for x in bk],
+             None if w is None else w[a:a + counts[rank]])
+    q.put((rank, out32.numpy().copy(), out64.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("counts,final,weighted", [([10, 10], "reduce", False),
+                                                   ([3, 4, 2], "allreduce", False),
+                                                   ([0, 6, 3], "reduce", False),
+                                                   ([5, 17], "allreduce", True),
+                                                   ([9, 0, 8], "reduce", True)])
+def test_chained_round_is_exact_gloo(counts, final, weighted):
+    """The Python ChainAggregator over real torch.distributed (gloo): client
+    shards stay put, the cascade state hops rank to rank; every result rank
+    ends with the single-process reference's bits."""
+    world = len(counts)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chain_worker, args=(r, world, port, counts, final, weighted, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    layout = BucketLayout.from_manifest(MAN)
+    n = sum(counts)
+    states = [synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL) for c in range(n)]
+    if weighted:
+        w = O.weights_from_sizes(np.arange(1, n + 1) * 3 + 2)
+        exact = {}
+        for j, (k, v0) in enumerate(states[0]):
+            x = np.stack([np.asarray(s[j][1]) for s in states])
+            exact[k] = O.mean_i64_trunc(x) if x.dtype == np.int64 else O.weighted_sum0(x, w)
+    else:
+        exact = dict(O.aggregate_state(states))
+    for rk, o32, o64 in res:
+        if final == "reduce" and rk != 0:
+            continue
+        for s in layout.slots:
+            src = o64 if s.kind == "i64" else o32
+            got = src[s.offset:s.offset + s.numel].reshape(s.shape)
+            assert got.tobytes() == np.asarray(exact[s.key]).tobytes(), (rk, s.key)

@@ -205,3 +205,110 @@ def test_stateless_mean_f32_multi():
     mask = _layout_pad_mask(layout)
     assert torch.equal(got[mask], want[mask])
     c.close()
+
+
+@pytest.mark.parametrize("lay", ["wrn16_8_c10", "wrnsl16_8_sf4_c10_proxy", "wrnsl16_8_sf4_c10_main"])
+@pytest.mark.parametrize("final", ["reduce", "allreduce"])
+@pytest.mark.parametrize("nchunks", [1, 16])
+def test_native_chained_one_rank_is_bit_exact(comm, lay, final, nchunks):
+    """fa_reduce_chained with one rank: the rank is its own finisher, so the
+    vector chunks finish from the first segment and the scalar columns go
+    through the raw stack/gather/compact-reduce/scatter path — all of which
+    must reproduce the single-GPU reduction bit for bit (the multi-rank
+    hops are replayed on CPU: tests/test_schedule.py)."""
+    from feddct_amd.comm import NativeChainedAggregator
+    man = load_manifest(lay)
+    layout = BucketLayout.from_manifest(man)
+    n = 20
+    clients = make_clients(layout, man, range(n), DEV, mode=synth.MODE_ADVERSARIAL)
+    want32, want64 = _single_gpu(layout, clients)
+    out32 = torch.full_like(clients[0][0], float("nan"))
+    out64 = torch.full_like(clients[0][1], -7)
+    agg = NativeChainedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], n,
+                                  out32, out64, comm, nchunks=nchunks, final=final)
+    for _ in range(2):
+        agg.step()
+    torch.cuda.synchronize()
+    mask = _layout_pad_mask(layout)
+    nan = torch.isnan(want32[mask])
+    assert torch.equal(torch.isnan(out32[mask]), nan)
+    assert torch.equal(out32[mask].view(torch.int32)[~nan], want32[mask].view(torch.int32)[~nan])
+    assert torch.equal(out64, want64)
+
+
+def test_native_chained_weighted(comm):
+    from feddct_amd.comm import NativeChainedAggregator
+    man = load_manifest("wrn16_8_c100")
+    layout = BucketLayout.from_manifest(man)
+    n = 7
+    clients = make_clients(layout, man, range(n), DEV, mode=synth.MODE_ADVERSARIAL)
+    w = [float(np.float32(k / 28.0)) for k in range(1, n + 1)]
+    want32, want64 = _single_gpu(layout, clients, weights=w)
+    out32, out64 = torch.zeros_like(want32), torch.zeros_like(want64)
+    NativeChainedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], n, out32,
+                            out64, comm, weights=w).step()
+    torch.cuda.synchronize()
+    mask = _layout_pad_mask(layout)
+    assert torch.equal(out32[mask].view(torch.int32), want32[mask].view(torch.int32))
+    assert torch.equal(out64, want64)
+
+
+@pytest.mark.parametrize("final", ["reduce", "allreduce"])
+def test_native_rs_gather_exchange_one_rank(comm, final):
+    """e1 with the reduce-scatter + gather exchange (FA_XCHG_RS_GATHER): one
+    rank's reduce-scatter / gather are the identity, so the round equals the
+    single-GPU reduction (the remainder path included: chunk lengths are not
+    multiples of anything in particular)."""
+    from feddct_amd.comm import FA_XCHG_RS_GATHER, NativeShardedAggregator
+    man = load_manifest("wrn16_8_c10")
+    layout = BucketLayout.from_manifest(man)
+    n = 20
+    clients = make_clients(layout, man, range(n), DEV, mode=synth.MODE_ADVERSARIAL)
+    want32, want64 = _single_gpu(layout, clients)
+    out32 = torch.full_like(clients[0][0], float("nan"))
+    out64 = torch.full_like(clients[0][1], -7)
+    agg = NativeShardedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], n,
+                                  out32, out64, comm, nchunks=13, final=final,
+                                  exchange=FA_XCHG_RS_GATHER)
+    for _ in range(2):
+        agg.step()
+    torch.cuda.synchronize()
+    mask = _layout_pad_mask(layout)
+    nan = torch.isnan(want32[mask])
+    assert torch.equal(out32[mask].view(torch.int32)[~nan], want32[mask].view(torch.int32)[~nan])
+    assert torch.equal(out64, want64)
+
+
+def test_python_chain_aggregator_one_rank_nccl():
+    """dist.ChainAggregator (torch.distributed orchestration, HIP backend) in
+    a one-rank RCCL group: bit-exact with the single-GPU reduction, also for
+    the full FedDCT config-5 layout (24 slots)."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from feddct_amd.dist import ChainAggregator
+    from feddct_amd.workload import joint_manifest
+    torch.cuda.set_device(DEV)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=DEV)
+    try:
+        mm = load_manifest("wrnsl16_8_sf4_c100_main")
+        pm = load_manifest("wrnsl16_8_sf4_c100_proxy")
+        layout = BucketLayout.from_manifest(joint_manifest([mm, pm]))
+        n = 24
+        clients = make_clients(layout, [(mm, "0."), (pm, "1.")], range(n), DEV)
+        want32, want64 = _single_gpu(layout, clients)
+        out32 = torch.full_like(clients[0][0], float("nan"))
+        out64 = torch.full_like(clients[0][1], -7)
+        agg = ChainAggregator(layout, n, out32, out64, final="reduce", root=0, nchunks=8)
+        agg.step([c[0] for c in clients], [c[1] for c in clients])
+        torch.cuda.synchronize()
+        mask = _layout_pad_mask(layout)
+        assert torch.equal(out32[mask].view(torch.int32), want32[mask].view(torch.int32))
+        assert torch.equal(out64, want64)
+    finally:
+        dist.destroy_process_group()

@@ -716,3 +716,25 @@ def test_unit_key_between_aligned_keys_n9():
         torch.cuda.synchronize()
         for (k, want), (k2, v) in zip(O.aggregate_state(states), g.state_dict().items()):
             assert k == k2 and bits_equal(v.cpu().numpy(), want), (rep, k)
+
+
+@pytest.mark.parametrize("case", ["weighted/wrn16_8_c10/n20/sizes_1_20",
+                                  "weighted/wrn16_8_c100/n20/cfg4_sizes"])
+def test_full_size_weighted_digest(lib, case):
+    """the client-size-weighted reduction at full size
+    (BASELINE config 4: wrn16_8 C100 x 20, quantity-skewed sizes) against the
+    committed digest of the build's weighted definition (C oracle,
+    tests/golden/make_weighted_digests.py) — the reference itself has no
+    weights, so this definition is the pin."""
+    import json
+    import os
+    from conftest import ROOT
+    from feddct_amd.workload import make_clients
+    with open(os.path.join(ROOT, "tests", "golden", "weighted_digests.json")) as f:
+        d = json.load(f)[case]
+    lay = case.split("/")[1]
+    man = load_manifest(lay)
+    layout = BucketLayout.from_manifest(man)
+    cl = make_clients(layout, man, range(20), DEV)
+    out32, out64 = _reduce(lib, layout, cl, weights=np.asarray(d["weights"], np.float32))
+    assert O.state_digest(buckets_to_state(layout, out32, out64)) == d["digest"]

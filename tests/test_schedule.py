@@ -1,0 +1,237 @@
+"""The native multi-GPU schedules (libfedagg_comm.so), all ranks at once, on
+a CPU: fa_describe_round gives each rank's exact
+list of exchanges and kernels; tests/schedsim.py replays the lists of every
+rank together under RCCL's group/matching rules with the oracle as the
+arithmetic.  Covers world sizes 2-8, uneven and empty shards, every root,
+weighted rounds, and both e1 exchanges:
+
+* chained and striped rounds must give the single-process reference's bits;
+* the sharded round's int64 keys are exact and its fp32 keys stay within
+  the re-association bound;
+* no schedule may deadlock;
+* the native cut points and peers agree with partition.split_tiles /
+  dist.shard_range and the Python aggregators' own send/receive lists.
+"""
+import numpy as np
+import pytest
+import torch
+
+from feddct_amd import comm as C
+from feddct_amd import synth
+from feddct_amd.dist import shard_range
+from feddct_amd.layout import BucketLayout
+from feddct_amd.partition import layout_tiles, split_tiles
+from oracle import torch_order as O
+from schedsim import Deadlock, Sim
+
+MAN = {"keys": [{"key": f"k{j}", "shape": [m] if m else [], "dtype": "float32"}
+                for j, m in enumerate([100, 4096, 33, 2048 + 8, 7, 0, 5000, 1, 64, 3000])]
+       + [{"key": "nbt", "shape": [], "dtype": "int64"},
+          {"key": "nbt2", "shape": [], "dtype": "int64"}]}
+
+
+def _buckets(layout, states):
+    c32, c64 = [], []
+    for st in states:
+        f32 = np.full(layout.f32_numel, np.nan, np.float32)   # padding must never leak
+        i64 = np.zeros(max(1, layout.i64_numel), np.int64)
+        for k, v in st:
+            s = layout.by_key[k]
+            tgt = i64 if s.kind == "i64" else f32
+            tgt[s.offset:s.offset + s.numel] = np.asarray(v).reshape(-1)
+        c32.append(f32)
+        c64.append(i64)
+    return c32, c64
+
+
+def _expected(states, weights):
+    if weights is None:
+        return dict(O.aggregate_state(states))
+    out = {}
+    for j, (k, v0) in enumerate(states[0]):
+        x = np.stack([np.asarray(s[j][1]) for s in states])
+        out[k] = O.mean_i64_trunc(x) if x.dtype == np.int64 else O.weighted_sum0(x, weights)
+    return out
+
+
+def _run(mode, counts, root, weighted=False, exchange=C.FA_XCHG_REDUCE, nchunks=5):
+    layout = BucketLayout.from_manifest(MAN)
+    n = sum(counts)
+    states = [synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL) for c in range(n)]
+    c32, c64 = _buckets(layout, states)
+    w = O.weights_from_sizes(np.arange(1, n + 1) * 5 + 1) if weighted else None
+    _, tiles = layout_tiles(layout)
+    scheds = [C.describe(mode, layout, counts, r, nchunks=nchunks, exchange=exchange, root=root,
+                         weighted=weighted) for r in range(len(counts))]
+    bufs = Sim(layout, tiles, counts, c32, c64, w, root).run(scheds)
+    return layout, states, w, bufs, scheds
+
+
+def _result_ranks(W, root):
+    return range(W) if root < 0 else [root]
+
+
+COUNTS = [[10, 10], [7, 0, 13], [3, 3, 3, 3, 3, 3, 3, 3], [0, 5, 1, 14], [4, 9, 0, 2, 5],
+          [1, 1, 1, 17], [16, 16, 1], [2, 30, 2, 0, 0, 1, 3, 2]]
+
+
+@pytest.mark.parametrize("counts", COUNTS)
+@pytest.mark.parametrize("root", [0, -1, "last", 1])
+def test_chained_schedule_is_exact(counts, root):
+    W = len(counts)
+    root = W - 1 if root == "last" else root
+    layout, states, _, bufs, _ = _run(C.FA_MODE_CHAINED, counts, root)
+    want = _expected(states, None)
+    for r in _result_ranks(W, root):
+        for s in layout.slots:
+            src = bufs[r]["OUT64"] if s.kind == "i64" else bufs[r]["OUT"]
+            got = src[s.offset:s.offset + s.numel].reshape(s.shape)
+            assert got.tobytes() == np.asarray(want[s.key]).tobytes(), (r, s.key)
+
+
+@pytest.mark.parametrize("counts", [[10, 10], [4, 9, 0, 2, 5], [2, 30, 2, 0, 0, 1, 3, 2]])
+def test_chained_schedule_weighted_is_exact(counts):
+    layout, states, w, bufs, _ = _run(C.FA_MODE_CHAINED, counts, 0, weighted=True)
+    want = _expected(states, w)
+    for s in layout.slots:
+        src = bufs[0]["OUT64"] if s.kind == "i64" else bufs[0]["OUT"]
+        got = src[s.offset:s.offset + s.numel].reshape(s.shape)
+        assert got.tobytes() == np.asarray(want[s.key]).tobytes(), s.key
+
+
+def test_chained_schedule_deep_levels():
+    """n_total >= 256: four state planes, level-2 promotions across hops."""
+    counts = [100, 156, 44]
+    layout, states, _, bufs, scheds = _run(C.FA_MODE_CHAINED, counts, -1, nchunks=3)
+    want = _expected(states, None)
+    for s in layout.slots:
+        src = bufs[2]["OUT64"] if s.kind == "i64" else bufs[2]["OUT"]
+        assert src[s.offset:s.offset + s.numel].tobytes() == np.asarray(want[s.key]).tobytes()
+    planes = {x["src_index"] for x in scheds[1] if x["op"] == "SEND"}
+    assert planes == set(i for i in range(4) if O.chain_levels(256, 300) & (1 << i))
+
+
+@pytest.mark.parametrize("counts", COUNTS)
+@pytest.mark.parametrize("root", [0, -1, 1])
+def test_striped_schedule_is_exact(counts, root):
+    W = len(counts)
+    layout, states, _, bufs, scheds = _run(C.FA_MODE_STRIPED, counts, root)
+    want = _expected(states, None)
+    for r in _result_ranks(W, root):
+        for s in layout.slots:
+            src = bufs[r]["OUT64"] if s.kind == "i64" else bufs[r]["OUT"]
+            got = src[s.offset:s.offset + s.numel].reshape(s.shape)
+            assert got.tobytes() == np.asarray(want[s.key]).tobytes(), (r, s.key)
+
+
+@pytest.mark.parametrize("counts", COUNTS)
+@pytest.mark.parametrize("exchange", [C.FA_XCHG_REDUCE, C.FA_XCHG_RS_GATHER])
+@pytest.mark.parametrize("root", [0, -1])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_sharded_schedule(counts, exchange, root, weighted):
+    W = len(counts)
+    layout, states, w, bufs, _ = _run(C.FA_MODE_SHARDED, counts, root, weighted, exchange)
+    want = _expected(states, w)
+    n = sum(counts)
+    for r in _result_ranks(W, root):
+        for s in layout.slots:
+            if s.kind == "i64":
+                assert np.array_equal(bufs[r]["OUT64"][s.offset:s.offset + s.numel],
+                                      np.asarray(want[s.key]).reshape(-1)), s.key
+                continue
+            got = bufs[r]["OUT"][s.offset:s.offset + s.numel].astype(np.float64)
+            x = np.stack([dict(st)[s.key].reshape(-1) for st in states]).astype(np.float64)
+            if w is not None:
+                x = x * w[:, None]
+            mag = np.abs(x).mean(0) if w is None else np.abs(x).sum(0)
+            err = np.abs(got - np.asarray(want[s.key], np.float64).reshape(-1))
+            assert (err <= 2 * n * 2.0 ** -24 * mag + 1e-38).all(), (r, s.key)
+
+
+@pytest.mark.parametrize("W", [2, 3, 4, 5, 6, 7, 8])
+def test_striped_cuts_and_peers_match_python(W):
+    """The native stripe bounds are partition.split_tiles', the shards are
+    dist.shard_range's, and the native send/receive lists are exactly the
+    Python StripedAggregator's (same pairwise rounds)."""
+    from feddct_amd.dist import stripe_p2p_schedule
+    layout = BucketLayout.from_manifest(MAN)
+    n = 3 * W + 2
+    counts = [b - a for a, b in (shard_range(n, W, r) for r in range(W))]
+    _, tiles = layout_tiles(layout)
+    parts = split_tiles(tiles, W, layout.f32_numel)
+    for r in range(W):
+        ops = C.describe(C.FA_MODE_STRIPED, layout, counts, r, root=-1)
+        sends = [(x["peer"], sum(counts[:r]) + x["src_index"], x["offset"], x["count"])
+                 for x in ops if x["op"] == "SEND" and x["src"] == "CLIENT"]
+        recvs = [(x["peer"], x["dst_index"], x["offset"], x["count"])
+                 for x in ops if x["op"] == "RECV" and x["dst"] == "RECV"]
+        for peer, slot, off, cnt in sends:
+            assert (off, off + cnt) == parts[peer][:2]
+        for peer, slot, off, cnt in recvs:
+            assert (off, off + cnt) == parts[r][:2]
+            a, b = shard_range(n, W, peer)
+            assert a <= slot < b
+        py = stripe_p2p_schedule([p[:2] for p in parts], [shard_range(n, W, q) for q in range(W)],
+                                 r)
+        native = [("send", x["peer"], sum(counts[:r]) + x["src_index"], x["offset"], x["count"])
+                  if x["op"] == "SEND" else
+                  ("recv", x["peer"], x["dst_index"], x["offset"], x["count"])
+                  for x in ops if x["op"] in ("SEND", "RECV") and
+                  (x["src"] == "CLIENT" or x["dst"] == "RECV")]
+        assert native == py
+
+
+@pytest.mark.parametrize("W", [2, 3, 5, 8])
+def test_chained_hops_follow_slot_order(W):
+    """Each rank receives only from rank-1 and sends only to rank+1 (slot
+    order), one op per nonzero state plane per chunk, and the chunks tile the
+    vector columns."""
+    layout = BucketLayout.from_manifest(MAN)
+    n = 2 * W + 9
+    counts = [b - a for a, b in (shard_range(n, W, r) for r in range(W))]
+    _, tiles = layout_tiles(layout)
+    vec = tiles[tiles[:, 2] == 0]
+    for r in range(W):
+        ops = C.describe(C.FA_MODE_CHAINED, layout, counts, r, nchunks=4, root=W - 1)
+        first = sum(counts[:r])
+        for x in ops:
+            if x["op"] == "SEND" and x["src"] == "STATE":
+                assert x["peer"] == r + 1
+                assert O.chain_levels(first + counts[r], n) & (1 << x["src_index"])
+            if x["op"] == "RECV" and x["dst"] == "STATE":
+                assert x["peer"] == r - 1
+                assert O.chain_levels(first, n) & (1 << x["dst_index"])
+        ks = [x for x in ops if x["op"] == "K_CHAIN"]
+        assert all(k["row0"] == first and k["nrows"] == counts[r] for k in ks)
+        covered = sum(int(((vec[:, 0] >= k["offset"]) & (vec[:, 0] < k["offset"] + k["count"]))
+                          .sum()) for k in ks)
+        assert covered == len(vec)
+
+
+def test_describe_errors():
+    from feddct_amd import _lib
+    layout = BucketLayout.from_manifest(MAN)
+    with pytest.raises(_lib.FedaggError, match="mode"):
+        C.describe(7, layout, [1, 1], 0)
+    with pytest.raises(_lib.FedaggError, match="root"):
+        C.describe(C.FA_MODE_CHAINED, layout, [1, 1], 0, root=2)
+    with pytest.raises(_lib.FedaggError, match="clients in total"):
+        C.describe(C.FA_MODE_CHAINED, layout, [0, 0], 0)
+
+
+def test_deadlock_is_detected():
+    """The replay itself: a schedule whose ranks both receive first is
+    reported, not hung."""
+    layout = BucketLayout.from_manifest(MAN)
+    counts = [2, 2]
+    states = [synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL) for c in range(4)]
+    c32, c64 = _buckets(layout, states)
+    _, tiles = layout_tiles(layout)
+    bad = [[{"step": 0, "op": "RECV", "peer": 1 - r, "chunk": -1, "src": "NONE",
+             "src_index": -1, "dst": "OUT", "dst_index": -1, "offset": 0, "count": 4,
+             "row0": 0, "nrows": 0},
+            {"step": 1, "op": "SEND", "peer": 1 - r, "chunk": -1, "src": "CLIENT",
+             "src_index": 0, "dst": "NONE", "dst_index": -1, "offset": 0, "count": 4,
+             "row0": 0, "nrows": 0}] for r in range(2)]
+    with pytest.raises(Deadlock):
+        Sim(layout, tiles, counts, c32, c64).run(bad)
