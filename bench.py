@@ -152,11 +152,14 @@ def pmc_traffic(n_gpus):
 def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
     from oracle.torch_mirror import arithmetic_core, reference_loop, time_call
 
-    # every host core this process may run on, and the box's CPU share
-    # (OMP_NUM_THREADS, 16 per GPU on the pool); the faster is the baseline
+    # The box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool).  The
+    # affinity mask lists every core of the machine (256), but the process
+    # only gets its share: measured r02, the loop at 256 torch threads took
+    # 64.1 s against 0.40 s at 16 (profiles/r02_bench_n1.json), so the
+    # baseline runs on the share, and on 1 thread.
     all_cores = len(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", all_cores) or all_cores)
-    counts = sorted({max(1, min(share, all_cores)), all_cores})
+    counts = [max(1, min(share, all_cores))]
     threads = counts[0]
     torch.set_num_threads(threads)
 
@@ -213,8 +216,9 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
             "cfg1_n2": {"loop_ms": round(t_cfg1 * 1e3, 2), "runs": reps_cfg1},
             "cfg3_feddct_n5": {"loop_ms": round(t_fd * 1e3, 2), "runs": reps_fd},
             "loop_ms_by_threads": {str(k): round(v[0] * 1e3, 2) for k, v in by_threads.items()},
-            "threads_note": (f"torch intra-op threads: all {all_cores} cores of this process's "
-                             f"affinity and the box's CPU share ({share}); value = the faster"),
+            "threads_note": (f"torch intra-op threads = the box's CPU share ({share}; the "
+                             f"affinity mask shows {all_cores} but 256 threads ran the loop "
+                             "160x slower, r02), and 1 thread"),
             "host_cpus": os.cpu_count(), "affinity_cpus": all_cores, "cpu": _cpu_model()}
 
 
@@ -878,12 +882,11 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
         o32, o64 = m["out"]
         src = 0 if m["root"] < 0 else m["root"]
         if src != 0:
+            from feddct_amd.dist import p2p
             if rank == src:
-                dist.send(o32, 0, group=group)
-                dist.send(o64, 0, group=group)
+                p2p([(dist.isend, o32, 0), (dist.isend, o64, 0)], group)
             elif rank == 0:
-                dist.recv(o32, src, group=group)
-                dist.recv(o64, src, group=group)
+                p2p([(dist.irecv, o32, src), (dist.irecv, o64, src)], group)
         r = {"ms_per_step": round(m["t"] * 1e3, 4),
              "GBps": round(nbytes_rank * world / m["t"] / 1e9, 2),
              "result_on": "every rank" if m["root"] < 0 else f"rank {m['root']}"}
@@ -1006,22 +1009,29 @@ def main():
             extra["weighted_launch"] = launch_stats(wper)
             extra["weighted_parity"] = weighted_digest_check("wrn16_8_c10/n20/sizes_1_20",
                                                              layout, wo32, wo64)
-            # the round with its broadcast (FA_F_BCAST: reduce launch + broadcast
-            # launch over the same tiles), N*B read + (N+1)*B written
-            bred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
-                           flags=_lib.FA_F_BCAST, plan=reducer.plan)
-            tb, _ = timed_launches(bred, max(10, args.steps // 2), 3)
-            extra["round_with_broadcast_us"] = round(tb * 1e6, 1)
-        t_step, wall = timed_launches(reducer, args.steps, args.warmup, per_launch=per)
+            del wred, wo32, wo64
+        t_step, wall = timed_launches(reducer, args.steps, args.warmup)
         t_kernel = t_step
-        extra["headline_launch"] = launch_stats(per)
         if not args.kernel_only:
+            # the same launches once more with an event between consecutive
+            # launches (kept out of the headline's timed region: the extra
+            # event packets add a few µs between kernels) — the spread and
+            # any clock ramp across K launches
+            timed_launches(reducer, args.steps, 0, per_launch=per)
+            extra["headline_launch"] = launch_stats(per)
             with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
                 want = json.load(f)[f"fedavg/{LAYOUT}/n{N_CLIENTS}"]
             got = digest_of(layout, out32, out64)
             extra["parity"] = {"vs": "reference server_aggregate SHA-256 (tests/golden)",
                                "bit_exact": got == want}
             extra["host_inclusive"] = host_inclusive(layout, clients, reducer, out32, out64)
+            # the round with its broadcast (FA_F_BCAST: reduce launch + broadcast
+            # launch over the same tiles), N*B read + (N+1)*B written — after
+            # every measurement that needs the clients' own values
+            bred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
+                           flags=_lib.FA_F_BCAST, plan=reducer.plan)
+            tb, _ = timed_launches(bred, max(10, args.steps // 2), 3)
+            extra["round_with_broadcast_us"] = round(tb * 1e6, 1)
             extra["dropin"] = dropin_timing(layout, clients, dev)
             try:
                 extra["dropin_feddct_cfg3"] = dropin_feddct_timing(dev)

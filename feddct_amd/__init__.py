@@ -15,3 +15,9 @@ __version__ = "0.1.0"
 def server_aggregate(global_model, client_models):
     from .aggregate import server_aggregate as _sa
     return _sa(global_model, client_models)
+
+
+def set_summation_order(order: str) -> None:
+    """"torch_cpu" (default) or "torch_gpu": see aggregate.set_summation_order."""
+    from .aggregate import set_summation_order as _s
+    _s(order)

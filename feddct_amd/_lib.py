@@ -42,6 +42,8 @@ FA_PLAN_TUNE_ST_SC1 = 0x10000
 FA_PLAN_TUNE_BATCH1 = 0x20000
 FA_PLAN_TUNE_BATCH4 = 0x40000
 FA_PLAN_TUNE_FUSED_BCAST = 0x80000
+FA_ORDER_TORCH_CPU = 0
+FA_ORDER_TORCH_GPU = 1
 
 
 def FA_PLAN_TUNE_BLOCKS_PER_CU(c):
@@ -59,7 +61,8 @@ EXPORTS = [
     "fa_mean_i64_trunc", "fa_div_f32", "fa_div_trunc_i64", "fa_broadcast_f32",
     "fa_synth_fill_f32", "fa_synth_fill_i64", "fa_copy_f32",
     "fa_norm_plan_create", "fa_norm_plan_destroy", "fa_prox_norms", "fa_prox_grad",
-    "fa_read_probe_f32", "fa_chain_levels", "fa_reduce_chain",
+    "fa_read_probe_f32", "fa_chain_levels", "fa_reduce_chain", "fa_torch_gpu_config",
+    "fa_plan_create_order",
 ]
 
 
@@ -121,6 +124,9 @@ def _load():
         "fa_copy_f32": (_I, [_P, _P, _I64, _P]),
         "fa_read_probe_f32": (_I, [_P, _I64, _P, _I, _P]),
         "fa_chain_levels": (ctypes.c_uint, [_I, _I]),
+        "fa_torch_gpu_config": (_I, [_I, _I64, ctypes.POINTER(_I)]),
+        "fa_plan_create_order": (_I, [_P, _I, _I64, _P, _I, _I64, _I, _I, ctypes.c_uint,
+                                      ctypes.POINTER(_P)]),
         "fa_reduce_chain": (_I, [_P, _P, _I, _P, ctypes.POINTER(FaChain), _P, ctypes.c_uint, _P]),
         "fa_norm_plan_create": (_I, [_P, _I, _I64, ctypes.POINTER(_P)]),
         "fa_norm_plan_destroy": (_I, [_P]),
@@ -188,9 +194,15 @@ class Plan:
     from a layout's segments, or from an explicit tile subset (``tiles``)."""
 
     def __init__(self, segs32, f32_numel, segs64=(), i64_numel=0, tile_elems=0,
-                 flags=FA_PLAN_GAPS_ARE_PADDING, tiles=None):
+                 flags=FA_PLAN_GAPS_ARE_PADDING, tiles=None, order=FA_ORDER_TORCH_CPU, n=0):
         h = ctypes.c_void_p()
-        if tiles is not None:
+        if order != FA_ORDER_TORCH_CPU:
+            a32, n32 = seg_array(segs32 if len(segs32) else np.zeros((0, 2), np.int64))
+            a64, n64 = seg_array(segs64 if len(segs64) else np.zeros((0, 2), np.int64))
+            check(lib.fa_plan_create_order(a32, n32, int(f32_numel), a64, n64, int(i64_numel),
+                                           int(n), int(order), flags, ctypes.byref(h)),
+                  "fa_plan_create_order")
+        elif tiles is not None:
             tiles = np.asarray(tiles, np.int64).reshape(-1, 3)
             arr = (FaTileDesc * max(1, len(tiles)))()
             for i, (s, c, k) in enumerate(tiles):

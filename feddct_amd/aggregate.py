@@ -38,7 +38,9 @@ from .arena import ModuleArena, get_arena
 from .layout import BucketLayout
 
 __all__ = ["server_aggregate", "server_aggregate_split", "aggregate_weighted", "client_weights",
-           "Engine", "engine"]
+           "Engine", "engine", "set_summation_order", "summation_order"]
+
+ORDERS = {"torch_cpu": 0, "torch_gpu": 1}
 
 
 def _require_gpu():
@@ -51,17 +53,27 @@ class Engine:
     """Plan/staging caches for one process (one GPU per process)."""
 
     def __init__(self):
+        # the summation order device-resident rounds reproduce: torch's CPU
+        # order (default), or torch-ROCm's GPU one (set_summation_order)
+        self.order = "torch_cpu"
         self._plans: Dict[tuple, _lib.Plan] = {}
         self._layouts: Dict[tuple, BucketLayout] = {}
         self._pipes: Dict[tuple, object] = {}
 
     # ------------------------------------------------------------ caches --
-    def plan(self, layout: BucketLayout, device: torch.device) -> _lib.Plan:
-        key = (layout.signature, device.index)
+    def plan(self, layout: BucketLayout, device: torch.device, n: int = 0,
+             order: str = "torch_cpu") -> _lib.Plan:
+        gpu = order == "torch_gpu"
+        key = (layout.signature, device.index) + ((n, order) if gpu else ())
         p = self._plans.get(key)
         if p is None:
             with torch.cuda.device(device):
-                p = _lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel)
+                if gpu:   # cut for this client count (the GPU order depends on N)
+                    p = _lib.Plan(layout.segs32, layout.f32_numel, layout.segs64,
+                                  layout.i64_numel, order=_lib.FA_ORDER_TORCH_GPU, n=n)
+                else:
+                    p = _lib.Plan(layout.segs32, layout.f32_numel, layout.segs64,
+                                  layout.i64_numel)
             self._plans[key] = p
         return p
 
@@ -173,7 +185,10 @@ class Engine:
                        cas: List[ModuleArena], weights, fuse):
         n = len(cas)
         dev = cas[0].device
-        plan = self.plan(layout, dev)
+        order = self.order
+        if order == "torch_gpu" and (weights is not None or n < 2):
+            order = "torch_cpu"   # (the GPU order is torch's unweighted mean, N >= 2)
+        plan = self.plan(layout, dev, n, order)
         flags = _lib.FA_F_BCAST if fuse else 0
         a32, a64 = self._ptr_arrays(cas)
         self._launch(plan, a32, a64, n, self._weights_arg(weights, n), out32.data_ptr(),
@@ -286,3 +301,21 @@ def aggregate_weighted(global_model, client_models, weights=None, sizes=None,
         engine().reduce_modules(global_model, list(client_models), None, broadcast)
     else:
         engine().reduce_modules(global_model, list(client_models), w, broadcast)
+
+
+def set_summation_order(order: str) -> None:
+    """Which torch order device-resident rounds reproduce bit for bit:
+    ``"torch_cpu"`` (default: torch's CPU stack(...).mean(0), the reference's
+    BASELINE config 1 and its device-independent definition) or
+    ``"torch_gpu"`` (torch-ROCm's own GPU reduction — what the reference's
+    training runs computed, their models being on the GPU,
+    train_fedavg.py:244-250; unweighted rounds of N >= 2 clients).
+    Host-resident modules always take the CPU order, which is what the
+    reference computes for them."""
+    if order not in ORDERS:
+        raise ValueError(f"order must be one of {sorted(ORDERS)}, not {order!r}")
+    engine().order = order
+
+
+def summation_order() -> str:
+    return engine().order

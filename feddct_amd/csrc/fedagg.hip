@@ -60,7 +60,19 @@ enum TileKind : int32_t {
   K_I64_CASC = 4,
   K_I64_ILP4 = 5,
   K_I64_INNER = 6,
+  // torch-ROCm's GPU order (fa_plan_create_order, FA_ORDER_TORCH_GPU); the
+  // tile's kind carries log2 of its stride in bits 8-15
+  K_F32_TGPU = 7,     // [N, M>=2]: S-way row split, 4 round-robin accumulators
+  K_I64_TGPU = 8,
+  K_F32_TGPU_IN = 9,  // M == 1: lane split + intra-wave shuffle tree, 1 element/wave
+  K_I64_TGPU_IN = 10,
 };
+
+__host__ __device__ inline bool kind_is64(int kind) {
+  const int b = kind & 0xFF;
+  return b == K_I64_CASC || b == K_I64_ILP4 || b == K_I64_INNER || b == K_I64_TGPU ||
+         b == K_I64_TGPU_IN;
+}
 
 struct Tile {
   int64_t start;  // first element (bucket index)
@@ -98,6 +110,7 @@ struct ReduceArgs {
   const float* st_in;
   float* st_out;
   int64_t plane;
+  const float* tfac;  // torch-GPU order: per-tile mean factor fl(M)/fl(N*M)
   const float* const* tab32;
   const int64_t* const* tab64;
   const float* tabw;
@@ -582,13 +595,126 @@ __global__ __launch_bounds__(kBlock) void bcast_tiles_kernel(ReduceArgs args) {
       }
     } else if ((int)threadIdx.x < t.count) {
       const int64_t e = t.start + threadIdx.x;
-      if (t.kind <= K_F32_INNER) {
+      if (!kind_is64(t.kind)) {
         const float r = a.out32[e];
         for (int i = 0; i < a.n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
       } else {
         const int64_t r = a.out64[e];
         for (int i = 0; i < a.n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
       }
+    }
+  }
+}
+
+// ---------------------------------------------- torch-ROCm's GPU order ----
+// The reduction torch-ROCm itself performs for stack(list, 0).mean(0) on
+// device tensors (ATen/native/hip/Reduce.cuh as built into this torch:
+// setReduceConfig, thread_reduce_impl, block_y_reduce / block_x_reduce;
+// MeanOps: project = acc * factor) — the order of the reference's original
+// GPU runs (train_fedavg.py:244-250 place the models on the GPU before
+// server_aggregate).  Opt-in (fa_plan_create_order); the default order is
+// torch's CPU one.
+//   outer (M >= 2): rows split S ways (S = 1 or the block height bh when
+//     N >= min(16*bh, 256)); part y takes rows y, y+S, ... round-robin into
+//     4 accumulators from +0, combined ((a0+a1)+a2)+a3; the S parts meet in
+//     block_y_reduce's halving tree; times the factor.  One element/thread.
+//   inner (M == 1): lane l < bw = last_pow2(N) takes rows l, l+bw (the same
+//     4-accumulator thread order), then the intra-wave tree with increasing
+//     shuffle offsets (ROCm's), lane 0's value times the factor.  One
+//     element per wave.
+template <class Src, int S>
+__device__ __forceinline__ float tgpu_outer(const Src& src, int64_t e, int n) {
+  float v[S];
+#pragma unroll
+  for (int y = 0; y < S; ++y) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = y;
+    for (; r + 3 * S < n; r += 4 * S) {
+      a0 = __fadd_rn(a0, src(r, e));
+      a1 = __fadd_rn(a1, src(r + S, e));
+      a2 = __fadd_rn(a2, src(r + 2 * S, e));
+      a3 = __fadd_rn(a3, src(r + 3 * S, e));
+    }
+    if (r < n) a0 = __fadd_rn(a0, src(r, e));
+    if (r + S < n) a1 = __fadd_rn(a1, src(r + S, e));
+    if (r + 2 * S < n) a2 = __fadd_rn(a2, src(r + 2 * S, e));
+    v[y] = __fadd_rn(__fadd_rn(__fadd_rn(a0, a1), a2), a3);
+  }
+#pragma unroll
+  for (int off = S / 2; off > 0; off /= 2)
+#pragma unroll
+    for (int y = 0; y < off; ++y) v[y] = __fadd_rn(v[y], v[y + off]);
+  return v[0];
+}
+
+template <class Src>
+__device__ float tgpu_outer_any(const Src& src, int64_t e, int n, int ls) {
+  switch (ls) {
+    case 0: return tgpu_outer<Src, 1>(src, e, n);
+    case 1: return tgpu_outer<Src, 2>(src, e, n);
+    case 2: return tgpu_outer<Src, 4>(src, e, n);
+    case 3: return tgpu_outer<Src, 8>(src, e, n);
+    default: return tgpu_outer<Src, 16>(src, e, n);
+  }
+}
+
+// lane value of the inner order; the wave then runs the shuffle tree
+template <class Src>
+__device__ __forceinline__ float tgpu_inner(const Src& src, int64_t e, int n, int bw, int lane) {
+  float a0 = 0.f, a1 = 0.f;
+  if (lane < n) a0 = __fadd_rn(a0, src(lane, e));
+  if (lane + bw < n) a1 = __fadd_rn(a1, src(lane + bw, e));
+  float v = __fadd_rn(__fadd_rn(__fadd_rn(a0, a1), 0.f), 0.f);
+  for (int off = 1; off < bw; off <<= 1) v = __fadd_rn(v, __shfl_down(v, off, 64));
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
+  (void)args;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const Tile t = a.tiles[blockIdx.x];
+  const float fac = a.tfac[blockIdx.x];
+  const int base = t.kind & 0xFF, ls = (t.kind >> 8) & 0xFF;
+  const bool sum_only = a.flags & FA_F_SUM_ONLY;
+  const int n = a.n;
+  if (base == K_F32_TGPU || base == K_I64_TGPU) {
+    const int j = threadIdx.x;
+    if (j >= t.count) return;
+    const int64_t e = t.start + j;
+    if (base == K_F32_TGPU) {
+      const float s = tgpu_outer_any(SrcF32{a, false}, e, n, ls);
+      const float r = sum_only ? s : __fmul_rn(s, fac);
+      a.out32[e] = r;
+      if (a.flags & FA_F_BCAST)
+        for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
+    } else {
+      const int64_t r = (int64_t)__fmul_rn(tgpu_outer_any(SrcI64{a}, e, n, ls), fac);
+      a.out64[e] = r;
+      if (a.flags & FA_F_BCAST)
+        for (int i = 0; i < n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
+    }
+    return;
+  }
+  // inner: one element per wave
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w >= t.count) return;
+  const int64_t e = t.start + w;
+  const int bw = 1 << ls;
+  if (base == K_F32_TGPU_IN) {
+    const float s = tgpu_inner(SrcF32{a, false}, e, n, bw, lane);
+    if (lane == 0) {
+      const float r = sum_only ? s : __fmul_rn(s, fac);
+      a.out32[e] = r;
+      if (a.flags & FA_F_BCAST)
+        for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
+    }
+  } else {
+    const float s = tgpu_inner(SrcI64{a}, e, n, bw, lane);
+    if (lane == 0) {
+      const int64_t r = (int64_t)__fmul_rn(s, fac);
+      a.out64[e] = r;
+      if (a.flags & FA_F_BCAST)
+        for (int i = 0; i < n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
     }
   }
 }
@@ -714,6 +840,9 @@ struct fa_plan {
   unsigned flags = 0;
   bool has32 = false;  // the tile table touches the fp32 bucket
   bool has64 = false;  // ... the int64 bucket
+  int order = FA_ORDER_TORCH_CPU;
+  int order_n = 0;        // FA_ORDER_TORCH_GPU: the client count it was cut for
+  float* d_fac = nullptr; // ... and its per-tile mean factors
 };
 
 namespace {
@@ -1024,6 +1153,103 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   return FA_OK;
 }
 
+int fa_torch_gpu_config(int n, int64_t m, int* stride) {
+  if (n < 2 || m < 1) return 0;
+  auto last_pow2 = [](int64_t v) {
+    int64_t p = 1;
+    while (p * 2 <= v) p *= 2;
+    return p;
+  };
+  int64_t S;
+  if (m == 1) {
+    if (n >= 128) return 0;  // (torch vectorises the input there)
+    S = last_pow2(n);
+  } else {
+    const int64_t ovs = m % 4 == 0 ? 4 : (m % 2 == 0 ? 2 : 1);
+    const int64_t mnt = 512 / ovs, dim0 = m / ovs;
+    const int64_t d0 = dim0 < mnt ? last_pow2(dim0) : mnt;
+    const int64_t d1 = n < mnt ? last_pow2(n) : mnt;
+    int64_t bw = std::min<int64_t>(d0, 64);
+    const int64_t bh = std::min<int64_t>(d1, mnt / bw);
+    const bool split = n >= std::min<int64_t>(bh * 16, 256);
+    S = split ? bh : 1;
+    if ((n + S - 1) / S >= 256 || S > 16) return 0;  // cross-block split / kernel limit
+  }
+  if (stride) *stride = (int)S;
+  return 1;
+}
+
+int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_seg* seg64,
+                         int nseg64, int64_t i64_numel, int n, int order, unsigned flags,
+                         fa_plan** out) {
+  if (order == FA_ORDER_TORCH_CPU)
+    return fa_plan_create(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, 0, flags, out);
+  if (!out) return set_err(FA_E_INVAL, "fa_plan_create_order: out is NULL");
+  *out = nullptr;
+  if (order != FA_ORDER_TORCH_GPU)
+    return set_err(FA_E_INVAL, "fa_plan_create_order: order %d", order);
+  if (n < 2 || n > FA_MAX_CLIENTS)
+    return set_err(FA_E_RANGE, "fa_plan_create_order: n=%d outside 2..%d", n, FA_MAX_CLIENTS);
+  std::vector<fa_seg> s32, s64;
+  int rc = check_segs(seg32, nseg32, f32_numel, "fp32", &s32);
+  if (rc) return rc;
+  rc = check_segs(seg64, nseg64, i64_numel, "int64", &s64);
+  if (rc) return rc;
+  std::vector<Tile> t;
+  std::vector<float> fac;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (const fa_seg& g : pass ? s64 : s32) {
+      if (g.numel == 0) continue;
+      int S = 1;
+      if (!fa_torch_gpu_config(n, g.numel, &S))
+        return set_err(FA_E_RANGE,
+                       "torch-GPU order: N=%d over a %lld-element tensor is outside the "
+                       "restated configurations (cross-block split)", n, (long long)g.numel);
+      int ls = 0;
+      while ((1 << ls) < S) ++ls;
+      // torch's factor: float(num_outputs) / numel, in float
+      const float f = (float)g.numel / (float)((int64_t)n * g.numel);
+      if (g.numel == 1) {
+        t.push_back(Tile{g.offset, 1, (pass ? K_I64_TGPU_IN : K_F32_TGPU_IN) | (ls << 8)});
+        fac.push_back(f);
+        continue;
+      }
+      for (int64_t c = 0; c < g.numel; c += kBlock) {
+        t.push_back(Tile{g.offset + c, (int32_t)std::min<int64_t>(kBlock, g.numel - c),
+                         (pass ? K_I64_TGPU : K_F32_TGPU) | (ls << 8)});
+        fac.push_back(f);
+      }
+    }
+  }
+  fa_plan* p = new fa_plan();
+  p->info.f32_numel = f32_numel;
+  p->info.i64_numel = i64_numel;
+  p->info.tile_elems = kBlock;
+  p->info.ntiles = (int32_t)t.size();
+  p->info.ntiles_tail = (int32_t)t.size();
+  p->flags = flags;
+  p->order = FA_ORDER_TORCH_GPU;
+  p->order_n = n;
+  for (const Tile& x : t) (kind_is64(x.kind) ? p->has64 : p->has32) = true;
+  hipError_t e = hipGetDevice(&p->device);
+  if (e == hipSuccess && !t.empty()) {
+    e = hipMalloc(&p->d_tiles, t.size() * sizeof(Tile));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_tiles, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_fac, fac.size() * sizeof(float));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_fac, fac.data(), fac.size() * sizeof(float), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    if (p->d_tiles) (void)hipFree(p->d_tiles);
+    if (p->d_fac) (void)hipFree(p->d_fac);
+    delete p;
+    return set_err(FA_E_HIP, "fa_plan_create_order: %s", hipGetErrorString(e));
+  }
+  *out = p;
+  return FA_OK;
+}
+
 int fa_plan_build_host(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_seg* seg64,
                        int nseg64, int64_t i64_numel, int tile_elems, unsigned flags,
                        fa_tile_desc* tiles, int cap, fa_plan_info* info) {
@@ -1118,6 +1344,7 @@ int fa_plan_create_from_tiles(const fa_tile_desc* tiles, int ntiles, int64_t f32
 
 int fa_plan_destroy(fa_plan* plan) {
   if (!plan) return FA_OK;
+  if (plan->d_fac) HIP_TRY(hipFree(plan->d_fac));
   if (plan->d_tiles) HIP_TRY(hipFree(plan->d_tiles));
   if (plan->d_tiles_alt) HIP_TRY(hipFree(plan->d_tiles_alt));
   delete plan;
@@ -1138,6 +1365,8 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
   if (n > FA_MAX_CLIENTS)
     return set_err(FA_E_RANGE, "fa_reduce: n=%d exceeds FA_MAX_CLIENTS=%d", n, FA_MAX_CLIENTS);
   if (flags & ~(FA_F_BCAST | FA_F_SUM_ONLY)) return set_err(FA_E_INVAL, "fa_reduce: bad flags");
+  if (plan->order == FA_ORDER_TORCH_GPU && weights)
+    return set_err(FA_E_INVAL, "fa_reduce: the torch-GPU order is the reference's unweighted mean");
   const fa_plan_info& in = plan->info;
   if (plan->info.ntiles == 0) return FA_OK;
   ReduceArgs a;
@@ -1193,6 +1422,23 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
     a.tab32 = (const float* const*)table;
     a.tab64 = (const int64_t* const*)((const void**)table + n);
     a.tabw = (const float*)((const void**)table + 2 * n);
+  }
+  if (plan->order == FA_ORDER_TORCH_GPU) {
+    if (n != plan->order_n) {
+      if (table) (void)hipFreeAsync(table, st);
+      return set_err(FA_E_INVAL, "fa_reduce: torch-GPU-order plan cut for n=%d, called with n=%d",
+                     plan->order_n, n);
+    }
+    a.ntiles = in.ntiles;
+    a.tfac = plan->d_fac;
+    hipLaunchKernelGGL(tgpu_kernel, dim3(in.ntiles), dim3(kBlock), 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (table) {
+      hipError_t e2 = hipFreeAsync(table, st);
+      if (e == hipSuccess) e = e2;
+    }
+    if (e != hipSuccess) return set_err(FA_E_HIP, "torch-GPU-order launch: %s", hipGetErrorString(e));
+    return FA_OK;
   }
   int ntiles = in.ntiles, vec_u = plan->vec_u;
   a.nscalar = in.ntiles_tail;

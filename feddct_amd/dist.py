@@ -89,6 +89,29 @@ def stripe_p2p_schedule(ranges, shards, me):
     return out
 
 
+def p2p(ops, group=None):
+    """Post one round of point-to-point ops [(dist.isend | dist.irecv,
+    tensor, peer)] together and wait for all of them.  Over gloo (a CPU
+    transport, used to rehearse ranks without RCCL) device tensors are staged
+    through host copies — gloo would otherwise read device memory from the
+    CPU a word at a time; over RCCL the tensors go as they are."""
+    if not ops:
+        return
+    stage = dist.get_backend(group) == "gloo" and any(t.is_cuda for _, t, _ in ops)
+    post, back = [], []
+    for fn, t, peer in ops:
+        if stage and t.is_cuda:
+            h = t.cpu() if fn is dist.isend else torch.empty(t.shape, dtype=t.dtype)
+            if fn is dist.irecv:
+                back.append((t, h))
+            t = h
+        post.append(dist.P2POp(fn, t, peer, group))
+    for req in dist.batch_isend_irecv(post):
+        req.wait()
+    for t, h in back:
+        t.copy_(h)
+
+
 def chunk_segments(layout: BucketLayout, nchunks: int):
     """Split the fp32 segments into <= nchunks consecutive groups of roughly
     equal bytes.  Returns [(segs ndarray, lo, hi)] with [lo, hi) the bucket
@@ -318,16 +341,10 @@ class StripedAggregator:
             lo, hi = self.ranges[r]
             sends, recvs = [], []
             if self.hi > self.lo and (self.final == "allreduce" or r == self.root):
-                sends.append(dist.P2POp(dist.isend, self.out32[self.lo:self.hi], self._peer(r),
-                                        self.group))
+                sends.append((dist.isend, self.out32[self.lo:self.hi], self._peer(r)))
             if hi > lo and (self.final == "allreduce" or me == self.root):
-                recvs.append(dist.P2POp(dist.irecv, self.out32[lo:hi], self._peer(r), self.group))
-            self._run(sends + recvs if me < r else recvs + sends)
-
-    def _run(self, ops):
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+                recvs.append((dist.irecv, self.out32[lo:hi], self._peer(r)))
+            p2p(sends + recvs if me < r else recvs + sends, self.group)
 
     def _i64(self, local64):
         if not self.layout.i64_numel:
@@ -353,13 +370,11 @@ class StripedAggregator:
             while i < len(sched) and sched[i][1] == peer:
                 kind, _, slot, off, cnt = sched[i]
                 if kind == "send":
-                    ops.append(dist.P2POp(dist.isend, local32[slot - a][off:off + cnt],
-                                          self._peer(peer), self.group))
+                    ops.append((dist.isend, local32[slot - a][off:off + cnt], self._peer(peer)))
                 else:
-                    ops.append(dist.P2POp(dist.irecv, self.recv[slot, :cnt], self._peer(peer),
-                                          self.group))
+                    ops.append((dist.irecv, self.recv[slot, :cnt], self._peer(peer)))
                 i += 1
-            self._run(ops)
+            p2p(ops, self.group)
         sources = []
         for k in range(self.n_total):
             if a <= k < b:
@@ -548,19 +563,21 @@ class ChainAggregator:
             pred = me > 0 and self.lev_in
             succ = me < F and self.lev_out
             dst = None if me < F else (self.out32 if result else self.fin)
+            staged = dist.get_backend(self.group) == "gloo" and self.state.is_cuda
             for c, (lo, hi, _) in enumerate(self.chunks):
                 if pred:
-                    for req in dist.batch_isend_irecv(
-                            [dist.P2POp(dist.irecv, p, self._peer(me - 1), self.group)
-                             for p in self._planes(self.lev_in, lo, hi)]):
-                        req.wait()
+                    p2p([(dist.irecv, p, self._peer(me - 1))
+                         for p in self._planes(self.lev_in, lo, hi)], self.group)
                 if n_loc:
                     self.backend.chain(c, local32, self.first[me], self.n_total, self.state,
                                        bool(pred), dst, self.plane, weights)
                 if succ:
+                    planes = self._planes(self.lev_out, lo, hi)
+                    if staged:     # (gloo rehearsal: host copies, see p2p)
+                        planes = [p.cpu() for p in planes]
                     sends += dist.batch_isend_irecv(
                         [dist.P2POp(dist.isend, p, self._peer(me + 1), self.group)
-                         for p in self._planes(self.lev_out, lo, hi)])
+                         for p in planes])
         for req in sends:
             req.wait()
         if self.chunks:
@@ -569,9 +586,9 @@ class ChainAggregator:
                 dist.broadcast(self.out32[lo:hi], src=self._peer(F), group=self.group)
             elif self.root != F:
                 if me == F:
-                    dist.send(self.fin[lo:hi], self._peer(self.root), group=self.group)
+                    p2p([(dist.isend, self.fin[lo:hi], self._peer(self.root))], self.group)
                 elif me == self.root:
-                    dist.recv(self.out32[lo:hi], self._peer(F), group=self.group)
+                    p2p([(dist.irecv, self.out32[lo:hi], self._peer(F))], self.group)
         if result:
             if self.T:
                 self.backend.tails([self.gather32[r] for r in self.rows], self.tidx, self.out32,

@@ -142,6 +142,27 @@ int fa_plan_create_from_tiles(const fa_tile_desc *tiles, int ntiles,
                               int64_t f32_numel, int64_t i64_numel,
                               int tile_elems, unsigned flags, fa_plan **out);
 
+/* ---- summation order ------------------------------------------------------
+ * FA_ORDER_TORCH_CPU (every plan's default): torch's CPU stack(...).mean(0),
+ *   the order above — the reference's BASELINE config 1 and the
+ *   device-independent definition.
+ * FA_ORDER_TORCH_GPU (opt-in): torch-ROCm's own GPU stack(...).mean(0)
+ *   (ATen/native/hip/Reduce.cuh + MeanOps as built into this torch): what the
+ *   reference's original runs computed with their models on the GPU
+ *   (train_fedavg.py:244-250).  Per tensor of M elements: the N rows split
+ *   S ways, 4 round-robin accumulators, block_y tree, times the factor
+ *   float(M)/float(N*M); M == 1 keys: lane split + the intra-wave shuffle
+ *   tree.  The cut depends on N, so the plan is made for one client count;
+ *   unweighted only.  fa_torch_gpu_config() says whether (N, M) is inside
+ *   the restated configurations (no cross-block split: ceil(N/S) < 256,
+ *   S <= 16; M == 1 needs N < 128) and gives S. */
+#define FA_ORDER_TORCH_CPU 0
+#define FA_ORDER_TORCH_GPU 1
+int fa_torch_gpu_config(int n, int64_t m, int *stride);
+int fa_plan_create_order(const fa_seg *seg32, int nseg32, int64_t f32_numel,
+                         const fa_seg *seg64, int nseg64, int64_t i64_numel,
+                         int n, int order, unsigned flags, fa_plan **out);
+
 /* The hot path: every key of N client buckets -> global bucket, one launch
  * (FA_F_BCAST: plus one broadcast launch over the same tiles).
  *   c32[i] / c64[i]  : client i's fp32 / int64 bucket (slot order 0..n-1)
