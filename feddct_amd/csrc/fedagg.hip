@@ -736,23 +736,16 @@ __global__ __launch_bounds__(kBlock) void bcast_kernel(BcastArgs a,
     for (int i = 0; i < a.n; ++i) a.dst[i][4 * nv + threadIdx.x] = a.src[4 * nv + threadIdx.x];
 }
 
-// Streaming copy (the roofline's calibration).  Four 16-B loads per lane in
-// flight before their stores (one float4 per lane per trip left each wave a
-// single load outstanding: 5.0 TB/s on the box against the guide's 6.29).
+// Streaming copy (the roofline's calibration): one 16-B non-temporal load and
+// store per lane, one 256-lane tile per workgroup, no loop — the fastest of
+// the copy forms measured (tools/copylab.hip, profiles/r02_copylab.jsonl:
+// 6.62-6.66 TB/s on 1 GiB, against 5.0 TB/s for a grid-stride loop with one
+// float4 per lane and 4.4-5.2 TB/s with four in flight per lane).
 __global__ __launch_bounds__(kBlock) void copy_kernel(const float* __restrict__ src,
                                                       float* __restrict__ dst, int64_t numel) {
   const int64_t nv = numel / 4;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x;
-  for (; v + 3 * stride < nv; v += 4 * stride) {
-    const f4 a = ld4<true>(src + 4 * v), b = ld4<true>(src + 4 * (v + stride));
-    const f4 c = ld4<true>(src + 4 * (v + 2 * stride)), d = ld4<true>(src + 4 * (v + 3 * stride));
-    st4<true>(dst + 4 * v, a);
-    st4<true>(dst + 4 * (v + stride), b);
-    st4<true>(dst + 4 * (v + 2 * stride), c);
-    st4<true>(dst + 4 * (v + 3 * stride), d);
-  }
-  for (; v < nv; v += stride) st4<true>(dst + 4 * v, ld4<true>(src + 4 * v));
+  const int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  if (v < nv) st4<true>(dst + 4 * v, ld4<true>(src + 4 * v));
   if (blockIdx.x == 0 && threadIdx.x < numel - 4 * nv)
     dst[4 * nv + threadIdx.x] = src[4 * nv + threadIdx.x];
 }
@@ -1672,10 +1665,10 @@ int fa_copy_f32(const float* src, float* dst, int64_t numel, void* stream) {
   if (numel < 0 || (numel > 0 && (!src || !dst))) return set_err(FA_E_INVAL, "fa_copy_f32: bad args");
   if (numel == 0) return FA_OK;
   if (!aligned16(src) || !aligned16(dst)) return set_err(FA_E_ALIGN, "fa_copy_f32: unaligned");
-  // 8 workgroups per CU, each lane 4 float4 per trip
-  const int grid = (int)std::min<int64_t>(2048, std::max<int64_t>(1, numel / (16 * kBlock)));
-  hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, src, dst,
-                     numel);
+  const int64_t grid = std::max<int64_t>(1, (numel / 4 + kBlock - 1) / kBlock);
+  if (grid > 0x7fffffff) return set_err(FA_E_RANGE, "fa_copy_f32: %lld floats", (long long)numel);
+  hipLaunchKernelGGL(copy_kernel, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream, src,
+                     dst, numel);
   HIP_TRY(hipGetLastError());
   return FA_OK;
 }
