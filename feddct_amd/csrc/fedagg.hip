@@ -153,13 +153,26 @@ __device__ __forceinline__ const float* vptr32(KArgs& a, int i) {
   if constexpr (TAB) return ((const FA_CONST f32p*)a.tab32)[i];
   else return cptr32(a, i);
 }
-template <bool TAB>
-__device__ __forceinline__ float vw(KArgs& a, int i) {
-  if constexpr (TAB) return ((const FA_CONST float*)a.tabw)[i];
-  else return cw(a, i);
-}
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+
+// The weights of clients b0..b0+nb-1, read once per batch BEFORE its data
+// loads are issued, through scalar loads only (kernarg array, or the device
+// table through the constant address space: read-only for the launch).
+// Reading each weight in the add phase instead put a load round trip and a
+// vmcnt/lgkmcnt(0) wait between consecutive clients' adds (the weighted
+// kernel ran 4-6 % behind the mean, r02 profiles).
+template <int NB>
+__device__ __forceinline__ void load_weights(KArgs& a, int b0, int nb, float (&wb)[NB]) {
+  if (a.n <= kInline) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) wb[b] = b < nb ? a.w[b0 + b] : 0.f;
+  } else {
+    const FA_CONST float* t = (const FA_CONST float*)a.tabw;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) wb[b] = b < nb ? t[b0 + b] : 0.f;
+  }
+}
 
 constexpr unsigned kWaveContig = 0x200u;  // internal a.flags bit (FA_PLAN_TUNE_WAVE_CONTIG)
 
@@ -273,9 +286,11 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t
                                       const uint32_t (&vi)[U], const bool (&ok)[U],
                                       int lp, int mask, int r0) {
   f4 x[NB][U];
+  float wb[NB];
+  if constexpr (WEIGHTED) load_weights<NB>(a, b0, NB, wb);
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const float* p = vptr32<TAB>(a, b0 + b) + start;
+    const float* p = bptr<TAB, POL>(a, b0 + b) + start;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
@@ -287,11 +302,22 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       f4 v = x[b][u];
-      if constexpr (WEIGHTED) v = mul4s(v, vw<TAB>(a, b0 + b));
+      if constexpr (WEIGHTED) v = mul4s(v, wb[b]);
       A.l0[u] = add4(A.l0[u], v);
     }
     promote<U, DEEP>(A, r0 + b0 + b + 1, lp, mask);
   }
+}
+
+// Pointer source of a batch's loads.  POL bit 3 (tuning, n <= the inline
+// count only): the kernarg pointer array read directly, which lets the
+// compiler issue the whole batch's loads back to back instead of one
+// client's loads behind a vmcnt(0) wait (slower at N = 20, r01; swept for
+// small N, r02).
+template <bool TAB, int POL>
+__device__ __forceinline__ const float* bptr(KArgs& a, int i) {
+  if constexpr ((POL & 8) != 0) return a.c32[i];
+  else return vptr32<TAB>(a, i);
 }
 
 // The last, partial batch (nb < NB clients): same issue-all-then-add shape,
@@ -301,10 +327,12 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
                                            int64_t start, const uint32_t (&vi)[U],
                                            const bool (&ok)[U], int lp, int mask, int r0) {
   f4 x[NB][U];
+  float wb[NB];
+  if constexpr (WEIGHTED) load_weights<NB>(a, b0, nb, wb);
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     if (b < nb) {
-      const float* p = vptr32<TAB>(a, b0 + b) + start;
+      const float* p = bptr<TAB, POL>(a, b0 + b) + start;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
@@ -318,7 +346,7 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         f4 v = x[b][u];
-        if constexpr (WEIGHTED) v = mul4s(v, vw<TAB>(a, b0 + b));
+        if constexpr (WEIGHTED) v = mul4s(v, wb[b]);
         A.l0[u] = add4(A.l0[u], v);
       }
       promote<U, DEEP>(A, r0 + b0 + b + 1, lp, mask);
@@ -1018,6 +1046,15 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   // DEEP (n >= 256): cascade levels 2-3 and the constant-space table loads
   const bool deep = a.n >= 256;
   const bool w = a.flags & 0x100u;  // internal: weighted
+  if ((pflags & FA_PLAN_TUNE_ISSUE_ALL) && a.n <= kInline && vec_u == 2) {
+    t_dyn_lds = 0;
+    t_grid_cap = 0;
+    const bool b4 = pflags & FA_PLAN_TUNE_BATCH4;
+    if (w) return b4 ? launch_one<2, 4, false, true, 11>(a, ntiles, st)
+                     : launch_one<2, 8, false, true, 11>(a, ntiles, st);
+    return b4 ? launch_one<2, 4, false, false, 11>(a, ntiles, st)
+              : launch_one<2, 8, false, false, 11>(a, ntiles, st);
+  }
   int nt = (pflags & FA_PLAN_TUNE_NO_NT) ? 0 : 3;
   if (pflags & FA_PLAN_TUNE_ST_PLAIN) nt &= ~2;
   if (pflags & FA_PLAN_TUNE_LD_PLAIN) nt &= ~1;

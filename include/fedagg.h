@@ -84,6 +84,9 @@ extern "C" {
 #define FA_PLAN_TUNE_BATCH1 0x20000u /* tuning: 1 client per load batch         */
 #define FA_PLAN_TUNE_BATCH4 0x40000u /* tuning: 4 clients per load batch        */
 #define FA_PLAN_TUNE_FUSED_BCAST 0x80000u /* tuning: FA_F_BCAST inside the reduce */
+#define FA_PLAN_TUNE_ISSUE_ALL 0x100000u /* tuning: a batch's loads back to back
+                                            (n <= FA_INLINE_CLIENTS, 2048-float tiles,
+                                            BATCH4 or 8 clients per batch)     */
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
 #define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
 /* tuning: persistent grid of 256*k workgroups striding over the tiles */

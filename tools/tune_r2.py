@@ -32,6 +32,13 @@ def variants(lay, sets, w, us, bs):
             reds = [Reducer(lay, cl, torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1]),
                             plan=plan, weights=w) for cl in sets]
             out.append((f"U{u}_B{b}", reds))
+    for b in (4, 8):   # the batch's loads issued back to back (FA_PLAN_TUNE_ISSUE_ALL)
+        fl = _lib.FA_PLAN_GAPS_ARE_PADDING | BATCH[b] | _lib.FA_PLAN_TUNE_ISSUE_ALL
+        plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
+                         tile_elems=2048, flags=fl)
+        out.append((f"U2_B{b}_issue_all", [Reducer(lay, cl, torch.zeros_like(cl[0][0]),
+                                                    torch.zeros_like(cl[0][1]), plan=plan,
+                                                    weights=w) for cl in sets]))
     auto = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel)
     out.append(("auto", [Reducer(lay, cl, torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1]),
                                  plan=auto, weights=w) for cl in sets]))
