@@ -155,7 +155,7 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
     # The box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool).  The
     # affinity mask lists every core of the machine (256), but the process
     # only gets its share: measured r02, the loop at 256 torch threads took
-    # 64.1 s against 0.40 s at 16 (profiles/r02_bench_n1.json), so the
+    # 64.1 s against 0.40 s at 16 (profiles/r02_cpu_threads.json), so the
     # baseline runs on the share, and on 1 thread.
     all_cores = len(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", all_cores) or all_cores)
@@ -850,6 +850,9 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
                         nchunks=args.chain_chunks)), last, True, steps=max(5, args.steps // 2))
     run_mode("e1/torch.distributed", lambda o32, o64: ShardedAggregator(
         layout, l32, l64, n_total, o32, o64, nchunks=args.chunks, final="reduce").step, 0, False)
+    run_mode("e1/torch.distributed/rs_gather", lambda o32, o64: ShardedAggregator(
+        layout, l32, l64, n_total, o32, o64, nchunks=args.chunks, final="reduce",
+        exchange="rs_gather").step, 0, False)
     striped_host = None
     if not args.no_exact and not args.kernel_only:
         try:
@@ -1009,8 +1012,10 @@ def main():
             wo32, wo64 = torch.zeros_like(out32), torch.zeros_like(out64)
             wred = Reducer(layout, clients, wo32, wo64, weights=w, plan=reducer.plan)
             wper = []
-            tw, _ = timed_launches(wred, max(10, args.steps // 2), 3, per_launch=wper)
+            tw, _ = timed_launches(wred, max(10, args.steps // 2), 3)
             extra["weighted_GBps"] = round(nbytes_rank / tw / 1e9, 1)
+            extra["weighted_us"] = round(tw * 1e6, 2)
+            timed_launches(wred, max(10, args.steps // 2), 0, per_launch=wper)
             extra["weighted_launch"] = launch_stats(wper)
             extra["weighted_parity"] = weighted_digest_check("wrn16_8_c10/n20/sizes_1_20",
                                                              layout, wo32, wo64)

@@ -179,14 +179,22 @@ class ShardedAggregator:
     ``final="reduce"`` (default): the north_star's final RCCL reduce — the
     global state lands on ``root`` (the server), like the single-process
     reference where the global model is one module; ``final="allreduce"``:
-    every rank gets it (reduce + the cross-GPU half of the broadcast)."""
+    every rank gets it (reduce + the cross-GPU half of the broadcast).
+
+    ``exchange="reduce"``: one reduce / all-reduce per chunk;
+    ``"rs_gather"``: a reduce-scatter (each rank sums 1/W of the chunk) then
+    a gather to the root / all-gather — the native FA_XCHG_RS_GATHER; the
+    chunk's last len % W floats take the plain reduce."""
 
     def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
                  local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
                  out64: torch.Tensor, nchunks: int = 8, backend=None, group=None,
-                 final: str = "reduce", root: int = 0):
+                 final: str = "reduce", root: int = 0, exchange: str = "reduce"):
         if final not in ("reduce", "allreduce"):
             raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
+        if exchange not in ("reduce", "rs_gather"):
+            raise ValueError(f"exchange must be 'reduce' or 'rs_gather', not {exchange!r}")
+        self.exchange = exchange
         self.final = final
         self.root = root
         self.rank = dist.get_rank(group)
@@ -199,6 +207,14 @@ class ShardedAggregator:
         self.chunks = chunk_segments(layout, nchunks)
         self.backend = backend or HipBackend(layout, self.chunks, len(local32), n_total)
         self.partial = torch.zeros_like(out32)
+        # rs_gather: this rank's share of each chunk's sum
+        self.shares = []
+        off = 0
+        for _, lo, hi in self.chunks:
+            q = (hi - lo) // self.world if exchange == "rs_gather" else 0
+            self.shares.append((off, q))
+            off += q
+        self.share = torch.zeros(max(off, 1), dtype=out32.dtype, device=out32.device)
         # int64 keys: every rank's buckets gathered raw; shards may be uneven,
         # so each rank sends max-shard rows and only the real ones are used
         nmax = -(-n_total // self.world)
@@ -216,28 +232,61 @@ class ShardedAggregator:
         works = []
         to_root = self.final == "reduce"
         gdst = self.root if self.group is None else dist.get_global_rank(self.group, self.root)
+        has_result = not to_root or self.rank == self.root
+        W, me = self.world, self.rank
         for c, (_, lo, hi) in enumerate(self.chunks):
             self.backend.partial_sum(c, self.local32, self.partial)
-            if to_root:
-                works.append(dist.reduce(self.partial[lo:hi], dst=gdst, op=dist.ReduceOp.SUM,
-                                         group=self.group, async_op=True))
-            else:
-                works.append(dist.all_reduce(self.partial[lo:hi], op=dist.ReduceOp.SUM,
-                                             group=self.group, async_op=True))
+            so, q = self.shares[c]
+            if q:
+                # reduce-scatter (completed before its gather is queued: a
+                # gloo group may run queued collectives on several threads)
+                mine = self.share[so:so + q]
+                dist.reduce_scatter_tensor(mine, self.partial[lo:lo + W * q],
+                                           op=dist.ReduceOp.SUM, group=self.group)
+                if to_root:
+                    dst = ([self.out32[lo + r * q:lo + (r + 1) * q] for r in range(W)]
+                           if has_result else None)
+                    works.append(dist.gather(mine, dst, dst=gdst, group=self.group,
+                                             async_op=True))
+                else:
+                    works.append(dist.all_gather_into_tensor(self.out32[lo:lo + W * q], mine,
+                                                             group=self.group, async_op=True))
+            rlo = lo + W * q
+            if rlo < hi:
+                if to_root:
+                    works.append(dist.reduce(self.partial[rlo:hi], dst=gdst,
+                                             op=dist.ReduceOp.SUM, group=self.group,
+                                             async_op=True))
+                else:
+                    works.append(dist.all_reduce(self.partial[rlo:hi], op=dist.ReduceOp.SUM,
+                                                 group=self.group, async_op=True))
+            works.append(None)   # chunk boundary
         w64 = None
         if self.layout.i64_numel:
             for j, t in enumerate(self.local64):
                 self.stack64[j].copy_(t)
             w64 = dist.all_gather_into_tensor(self.gather64, self.stack64, group=self.group,
                                               async_op=True)
-        has_result = not to_root or self.rank == self.root
         # finish chunk c (/N_total) as soon as its exchange lands, while the
         # exchanges of the later chunks are still on the wire
-        for w, (_, lo, hi) in zip(works, self.chunks):
-            w.wait()
+        c = 0
+        for w in works:
+            if w is not None:
+                w.wait()
+                continue
+            _, lo, hi = self.chunks[c]
+            so, q = self.shares[c]
             if has_result:
-                self.backend.divide(self.partial[lo:hi], float(self.n_total),
-                                    self.out32[lo:hi])
+                if q == 0:      # the reduced chunk sits in partial (root / all-reduce)
+                    self.backend.divide(self.partial[lo:hi], float(self.n_total),
+                                        self.out32[lo:hi])
+                else:           # shares gathered into out32; the remainder in partial
+                    rlo = lo + W * q
+                    if rlo < hi:
+                        self.out32[rlo:hi].copy_(self.partial[rlo:hi])
+                    self.backend.divide(self.out32[lo:hi], float(self.n_total),
+                                        self.out32[lo:hi])
+            c += 1
         if w64 is not None:
             w64.wait()
             if has_result:

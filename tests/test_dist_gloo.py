@@ -51,7 +51,7 @@ def _bucket(layout, state):
     return f32, i64
 
 
-def _worker(rank, world, port, n_total, q, final="allreduce"):
+def _worker(rank, world, port, n_total, q, final="allreduce", exchange="reduce"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     layout = BucketLayout.from_manifest(MAN)
@@ -61,7 +61,8 @@ def _worker(rank, world, port, n_total, q, final="allreduce"):
     out64 = torch.zeros(max(1, layout.i64_numel), dtype=torch.int64)
     chunks = chunk_segments(layout, 3)
     agg = ShardedAggregator(layout, [b[0] for b in bk], [b[1] for b in bk], n_total, out32,
-                            out64, nchunks=3, backend=OracleBackend(layout, chunks), final=final)
+                            out64, nchunks=3, backend=OracleBackend(layout, chunks), final=final,
+                            exchange=exchange)
     agg.step()
     # what each rank contributed, to rebuild the expected cross-rank sum
     part = torch.zeros(layout.f32_numel)
@@ -83,13 +84,15 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,n_total,final", [(2, 20, "allreduce"), (3, 7, "allreduce"),
-                                               (2, 20, "reduce"), (3, 7, "reduce")])
-def test_sharded_round_gloo(world, n_total, final):
+@pytest.mark.parametrize("world,n_total,final,exchange", [
+    (2, 20, "allreduce", "reduce"), (3, 7, "allreduce", "reduce"), (2, 20, "reduce", "reduce"),
+    (3, 7, "reduce", "reduce"), (2, 20, "reduce", "rs_gather"), (3, 7, "allreduce", "rs_gather"),
+    (3, 7, "reduce", "rs_gather")])
+def test_sharded_round_gloo(world, n_total, final, exchange):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q, final))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q, final, exchange))
              for r in range(world)]
     for p in procs:
         p.start()
