@@ -781,6 +781,34 @@ def weighted_digest_check(case, layout, o32, o64):
             "bit_exact": digest_of(layout, o32, o64) == want}
 
 
+def torch_gpu_order_mode(layout, clients, steps=20):
+    """The opt-in FA_ORDER_TORCH_GPU plan (torch-ROCm's own GPU
+    stack(...).mean(0) order, the reference's .cuda() runs) on the cfg2
+    workload: launch time and bit-exactness against torch's cuda mean of
+    every key, computed here by torch itself."""
+    n = len(clients)
+    plan = _lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
+                     order=_lib.FA_ORDER_TORCH_GPU, n=n)
+    o32, o64 = torch.zeros_like(clients[0][0]), torch.zeros_like(clients[0][1])
+    red = Reducer(layout, clients, o32, o64, plan=plan)
+    t, _ = timed_launches(red, steps, 3)
+    ok = True
+    for s in layout.slots:
+        src = 1 if s.kind == "i64" else 0
+        ref = torch.stack([c[src][s.offset:s.offset + s.numel].view(s.shape).float()
+                           for c in clients], 0).mean(0)
+        if s.kind == "i64":
+            want = torch.zeros(s.shape, dtype=torch.int64, device=ref.device)
+            want.copy_(ref)
+            ok &= bool(torch.equal(o64[s.offset:s.offset + s.numel].view(s.shape), want))
+        else:
+            got = o32[s.offset:s.offset + s.numel].view(s.shape)
+            ok &= bool(torch.equal(got.view(torch.int32), ref.view(torch.int32)))
+    nb = layout.algorithmic_bytes(n)
+    return {"us": round(t * 1e6, 1), "GBps": round(nb / t / 1e9, 1),
+            "bit_exact_vs_torch_cuda_mean": ok}
+
+
 def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, out64, reducer,
               nbytes_rank, extra):
     """N>1 (weak scaling: 20 client slots per GPU, slot order = rank order).
@@ -1035,6 +1063,10 @@ def main():
             extra["parity"] = {"vs": "reference server_aggregate SHA-256 (tests/golden)",
                                "bit_exact": got == want}
             extra["host_inclusive"] = host_inclusive(layout, clients, reducer, out32, out64)
+            try:
+                extra["torch_gpu_order_mode"] = torch_gpu_order_mode(layout, clients)
+            except Exception as e:  # noqa: BLE001
+                extra["torch_gpu_order_mode"] = {"error": repr(e)}
             # the round with its broadcast (FA_F_BCAST: reduce launch + broadcast
             # launch over the same tiles), N*B read + (N+1)*B written — after
             # every measurement that needs the clients' own values

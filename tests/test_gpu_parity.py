@@ -670,6 +670,19 @@ def test_distance_to_torch_gpu_mean(lib, record_property):
     print(f"vs torch GPU mean: bit-identical {same}/{total}, max ULP {worst_ulp}, "
           f"max error {worst_rel:.2f} eps x mean|x|")
     assert worst_rel <= 2 * n
+    # and the opt-in torch-GPU order IS torch's GPU mean: 0 ULP everywhere
+    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
+                    order=lib.FA_ORDER_TORCH_GPU, n=n)
+    g32 = torch.zeros_like(out32)
+    g64 = torch.zeros_like(cl[0][1])
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    lib.check(lib.lib.fa_reduce(plan.handle, lib.ptr_array([c[0].data_ptr() for c in cl]),
+                                lib.ptr_array([c[1].data_ptr() for c in cl]), n, None,
+                                g32.data_ptr(), g64.data_ptr(), 0, s))
+    torch.cuda.synchronize()
+    for o, m in layout.segs32:
+        gpu = torch.stack([c[0][o:o + m] for c in cl], 0).mean(0)
+        assert _max_ulp(g32[o:o + m].cpu().numpy(), gpu.cpu().numpy()) == 0
 
 
 def test_shim_empty_and_unit_tensors():
