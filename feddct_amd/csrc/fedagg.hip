@@ -66,6 +66,7 @@ enum TileKind : int32_t {
   K_I64_TGPU = 8,
   K_F32_TGPU_IN = 9,  // M == 1: lane split + intra-wave shuffle tree, 1 element/wave
   K_I64_TGPU_IN = 10,
+  K_F32_TGPU_V = 11,  // [N, M>=2], 16-B aligned run: 4 elements per lane, up to 1024
 };
 
 __host__ __device__ inline bool kind_is64(int kind) {
@@ -686,6 +687,51 @@ __device__ float tgpu_outer_any(const Src& src, int64_t e, int n, int ls) {
   }
 }
 
+// The same order for 4 consecutive elements of one tensor per lane (the
+// order depends only on (N, M), so the 4 lanes of a float4 are 4 independent
+// copies of it): 16-B non-temporal loads, the rows' loads of one round-robin
+// step issued together.  Vector adds are per-component IEEE adds (no
+// multiply feeds them, so contraction cannot apply).
+template <int S>
+__device__ __forceinline__ f4 tgpu_outer4(KArgs& a, int64_t start, uint32_t v, int n) {
+  f4 val[S];
+#pragma unroll
+  for (int y = 0; y < S; ++y) {
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    f4 a0 = z, a1 = z, a2 = z, a3 = z;
+    int r = y;
+    for (; r + 3 * S < n; r += 4 * S) {
+      const f4 x0 = ldg4<true>(cptr32(a, r) + start, v);
+      const f4 x1 = ldg4<true>(cptr32(a, r + S) + start, v);
+      const f4 x2 = ldg4<true>(cptr32(a, r + 2 * S) + start, v);
+      const f4 x3 = ldg4<true>(cptr32(a, r + 3 * S) + start, v);
+      a0 += x0;
+      a1 += x1;
+      a2 += x2;
+      a3 += x3;
+    }
+    if (r < n) a0 += ldg4<true>(cptr32(a, r) + start, v);
+    if (r + S < n) a1 += ldg4<true>(cptr32(a, r + S) + start, v);
+    if (r + 2 * S < n) a2 += ldg4<true>(cptr32(a, r + 2 * S) + start, v);
+    val[y] = ((a0 + a1) + a2) + a3;
+  }
+#pragma unroll
+  for (int off = S / 2; off > 0; off /= 2)
+#pragma unroll
+    for (int y = 0; y < off; ++y) val[y] = val[y] + val[y + off];
+  return val[0];
+}
+
+__device__ f4 tgpu_outer4_any(KArgs& a, int64_t start, uint32_t v, int n, int ls) {
+  switch (ls) {
+    case 0: return tgpu_outer4<1>(a, start, v, n);
+    case 1: return tgpu_outer4<2>(a, start, v, n);
+    case 2: return tgpu_outer4<4>(a, start, v, n);
+    case 3: return tgpu_outer4<8>(a, start, v, n);
+    default: return tgpu_outer4<16>(a, start, v, n);
+  }
+}
+
 // lane value of the inner order; the wave then runs the shuffle tree
 template <class Src>
 __device__ __forceinline__ float tgpu_inner(const Src& src, int64_t e, int n, int bw, int lane) {
@@ -705,6 +751,17 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   const int base = t.kind & 0xFF, ls = (t.kind >> 8) & 0xFF;
   const bool sum_only = a.flags & FA_F_SUM_ONLY;
   const int n = a.n;
+  if (base == K_F32_TGPU_V) {
+    const uint32_t v = threadIdx.x;
+    if ((int)(v * 4) >= t.count) return;
+    f4 r = tgpu_outer4_any(a, t.start, v, n, ls);
+    if (!sum_only)
+      r = f4{__fmul_rn(r.x, fac), __fmul_rn(r.y, fac), __fmul_rn(r.z, fac), __fmul_rn(r.w, fac)};
+    stg4<true>(a.out32 + t.start, v, r);
+    if (a.flags & FA_F_BCAST)
+      for (int i = 0; i < n; ++i) stg4<true>(const_cast<float*>(cptr32(a, i)) + t.start, v, r);
+    return;
+  }
   if (base == K_F32_TGPU || base == K_I64_TGPU) {
     const int j = threadIdx.x;
     if (j >= t.count) return;
@@ -1244,17 +1301,34 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
         fac.push_back(f);
         continue;
       }
-      for (int64_t c = 0; c < g.numel; c += kBlock) {
-        t.push_back(Tile{g.offset + c, (int32_t)std::min<int64_t>(kBlock, g.numel - c),
-                         (pass ? K_I64_TGPU : K_F32_TGPU) | (ls << 8)});
+      auto scalar = [&](int64_t lo, int64_t hi) {
+        for (int64_t c = lo; c < hi; c += kBlock) {
+          t.push_back(Tile{g.offset + c, (int32_t)std::min<int64_t>(kBlock, hi - c),
+                           (pass ? K_I64_TGPU : K_F32_TGPU) | (ls << 8)});
+          fac.push_back(f);
+        }
+      };
+      if (pass) {
+        scalar(0, g.numel);
+        continue;
+      }
+      // fp32: the 16-B aligned body in 4-element-per-lane tiles, the <= 3
+      // element head and tail one element per lane (same order, same factor)
+      const int64_t head = std::min<int64_t>((4 - g.offset % 4) % 4, g.numel);
+      const int64_t body = (g.numel - head) / 4 * 4;
+      scalar(0, head);
+      for (int64_t c = head; c < head + body; c += 4 * kBlock) {
+        t.push_back(Tile{g.offset + c, (int32_t)std::min<int64_t>(4 * kBlock, head + body - c),
+                         K_F32_TGPU_V | (ls << 8)});
         fac.push_back(f);
       }
+      scalar(head + body, g.numel);
     }
   }
   fa_plan* p = new fa_plan();
   p->info.f32_numel = f32_numel;
   p->info.i64_numel = i64_numel;
-  p->info.tile_elems = kBlock;
+  p->info.tile_elems = 4 * kBlock;
   p->info.ntiles = (int32_t)t.size();
   p->info.ntiles_tail = (int32_t)t.size();
   p->flags = flags;

@@ -645,8 +645,12 @@ def _max_ulp(a: np.ndarray, b: np.ndarray) -> int:
 def test_distance_to_torch_gpu_mean(lib, record_property):
     """The reference's original runs averaged CUDA tensors; torch-ROCm's GPU
     mean uses another summation order than torch's CPU mean (which the engine
-    reproduces exactly).  On realistic wrn16_8 data the two stay within a few
-    ULP; recorded for DESIGN.md."""
+    reproduces exactly).  Measured on the box for this seeded cfg2 state
+    (profiles/r02_distance_to_torch_gpu_mean.txt): 46.1 % of
+    elements bit-identical, max 13,107 ULP (at a near-cancelling element),
+    max error 3.63 eps x mean|x_i|.  Inputs and both orders are deterministic,
+    so the bounds below are tight pins, not tolerances; the opt-in
+    FA_ORDER_TORCH_GPU plan must be 0 ULP."""
     from feddct_amd.workload import make_clients
     man = load_manifest("wrn16_8_c10")
     layout = BucketLayout.from_manifest(man)
@@ -669,7 +673,8 @@ def test_distance_to_torch_gpu_mean(lib, record_property):
     record_property("max_err_eps_of_mean_abs_vs_torch_gpu_mean", worst_rel)
     print(f"vs torch GPU mean: bit-identical {same}/{total}, max ULP {worst_ulp}, "
           f"max error {worst_rel:.2f} eps x mean|x|")
-    assert worst_rel <= 2 * n
+    assert worst_ulp <= 13107
+    assert worst_rel <= 3.7
     # and the opt-in torch-GPU order IS torch's GPU mean: 0 ULP everywhere
     plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
                     order=lib.FA_ORDER_TORCH_GPU, n=n)

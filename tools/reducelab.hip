@@ -1,0 +1,156 @@
+// reducelab.hip — where the write stream's cost comes from in an N-client
+// tile reduction (cfg3: N=5, cfg2: N=20), against the copy kernel on the
+// same allocation scheme.  Standalone lab binary (not the product):
+//   hipcc --offload-arch=gfx950 -O3 -o tools/reducelab tools/reducelab.hip
+// One JSON line per (variant, N, round); GB/s counts N inputs + 1 output.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                   \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const f4 gcf4;
+typedef __attribute__((address_space(1))) f4 gf4;
+
+constexpr int MAXN = 20;
+struct Ptrs {
+  const float* c[MAXN];
+};
+
+__device__ __forceinline__ f4 ld(const float* p, int64_t v) {
+  return __builtin_nontemporal_load((gcf4*)p + v);
+}
+__device__ __forceinline__ void st(float* p, int64_t v, f4 x) {
+  __builtin_nontemporal_store(x, (gf4*)p + v);
+}
+
+// MODE 0: client by client (U loads, wait, add); 1: all N*U loads issued
+// first; 2: like 0 but no store (read-only); 3: like 0 with the tile order
+// strided across the grid (block b -> tile (b * S) mod T).
+template <int N, int U, int MODE>
+__global__ __launch_bounds__(256) void nsum(Ptrs p, float* out, int64_t nv, int ntiles, int S) {
+  int t = blockIdx.x;
+  if constexpr (MODE == 3) t = (int)(((int64_t)blockIdx.x * S) % ntiles);
+  const int64_t b = (int64_t)t * U * 256 + threadIdx.x;
+  f4 acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = f4{0, 0, 0, 0};
+  if constexpr (MODE == 1) {
+    f4 x[N][U];
+#pragma unroll
+    for (int c = 0; c < N; ++c)
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[c][u] = ld(p.c[c], b + u * 256);
+#pragma unroll
+    for (int c = 0; c < N; ++c)
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] += x[c][u];
+  } else {
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+      f4 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = ld(p.c[c], b + u * 256);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] += x[u];
+    }
+  }
+  if constexpr (MODE == 2) {
+    // keep the sum live without storing it (one lane of 2^20 writes)
+    f4 all = acc[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u) all += acc[u];
+    if (all.x == 1.2345e-30f && all.y == 6.789e-31f) st(out, b, all);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) st(out, b + u * 256, acc[u]);
+  }
+}
+
+__global__ __launch_bounds__(256) void copy1(const float* s, float* d, int64_t nv) {
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v < nv) st(d, v, ld(s, v));
+}
+
+template <class F>
+float time_us(F f, int reps) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) f();
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) f();
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  return ms * 1e3f / reps;
+}
+
+int main() {
+  const int64_t m = 10971136;  // floats per client: ~ the wrn16_8 bucket, 4096-aligned
+  const int64_t nv = m / 4;
+  std::vector<float*> bufs(MAXN);
+  for (auto& q : bufs) {
+    CK(hipMalloc(&q, m * 4));
+    CK(hipMemset(q, 0, m * 4));
+  }
+  float* out;
+  CK(hipMalloc(&out, m * 4));
+  CK(hipMemset(out, 0, m * 4));
+  Ptrs p;
+  for (int c = 0; c < MAXN; ++c) p.c[c] = bufs[c];
+  auto rep = [&](const char* name, int n, float us, int nw) {
+    double bytes = (double)m * 4 * (n + nw);
+    printf("{\"variant\": \"%s\", \"n\": %d, \"us\": %.2f, \"GBps\": %.1f}\n", name, n, us,
+           bytes / (us * 1e-6) / 1e9);
+    fflush(stdout);
+  };
+  const int t1 = (int)(nv / 256), t2 = (int)(nv / 512);
+  // a second, disjoint set for rotation (the bench's cfg3 form: 2 sets > MALL)
+  std::vector<float*> bufs2(MAXN);
+  for (auto& q : bufs2) {
+    CK(hipMalloc(&q, m * 4));
+    CK(hipMemset(q, 0, m * 4));
+  }
+  float* out2;
+  CK(hipMalloc(&out2, m * 4));
+  Ptrs p2;
+  for (int c = 0; c < MAXN; ++c) p2.c[c] = bufs2[c];
+  int flip = 0;
+#define RUN(N)                                                                                   \
+  rep("rw_U1", N, time_us([&] { nsum<N, 1, 0><<<t1, 256>>>(p, out, nv, t1, 1); }, 20), 1);       \
+  rep("rw_U2", N, time_us([&] { nsum<N, 2, 0><<<t2, 256>>>(p, out, nv, t2, 1); }, 20), 1);       \
+  rep("issue_all_U1", N, time_us([&] { nsum<N, 1, 1><<<t1, 256>>>(p, out, nv, t1, 1); }, 20), 1); \
+  rep("ro_U1", N, time_us([&] { nsum<N, 1, 2><<<t1, 256>>>(p, out, nv, t1, 1); }, 20), 0);       \
+  rep("ro_U2", N, time_us([&] { nsum<N, 2, 2><<<t2, 256>>>(p, out, nv, t2, 1); }, 20), 0);       \
+  rep("strided_U1_S257", N,                                                                      \
+      time_us([&] { nsum<N, 1, 3><<<t1, 256>>>(p, out, nv, t1, 257); }, 20), 1);                 \
+  rep("strided_U1_S9", N, time_us([&] { nsum<N, 1, 3><<<t1, 256>>>(p, out, nv, t1, 9); }, 20), 1); \
+  rep("rw_U1_rot2", N, time_us([&] {                                                             \
+        flip ^= 1;                                                                               \
+        nsum<N, 1, 0><<<t1, 256>>>(flip ? p2 : p, flip ? out2 : out, nv, t1, 1);                 \
+      }, 20), 1);                                                                                \
+  rep("rw_U2_rot2", N, time_us([&] {                                                             \
+        flip ^= 1;                                                                               \
+        nsum<N, 2, 0><<<t2, 256>>>(flip ? p2 : p, flip ? out2 : out, nv, t2, 1);                 \
+      }, 20), 1);
+  for (int r = 0; r < 2; ++r) {
+    rep("copy1", 1, time_us([&] { copy1<<<t1, 256>>>(bufs[0], out, nv); }, 20), 1);
+    RUN(5) RUN(20)
+  }
+  return 0;
+}
