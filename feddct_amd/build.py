@@ -76,6 +76,7 @@ def build(force: bool = False, extra=()) -> str:
         os.replace(COMM_OUT + ".tmp", COMM_OUT)
     build_shim(force)
     build_example(force)
+    build_loopback(force)
     return OUT
 
 
@@ -98,3 +99,37 @@ def build_example(force: bool = False) -> str:
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv))
+
+
+# Test infrastructure: the native multi-rank rounds on one GPU.  fedcomm.hip
+# compiled unchanged, linked against an in-process loopback of the RCCL
+# subset it calls (tests/loopback/loopccl.hip) instead of librccl, and a C++
+# driver (tests/loopback/loop_round.cpp) run by tests/test_gpu_loopback.py.
+# Nothing in the package links or loads these.
+LOOP_DIR = os.path.join(HERE, "..", "tests", "loopback")
+
+
+def build_loopback(force: bool = False) -> str:
+    inc = "-I" + os.path.join(HERE, "..", "include")
+    ccl_src = os.path.join(LOOP_DIR, "loopccl.hip")
+    ccl = os.path.join(LOOP_DIR, "libloopccl.so")
+    comm = os.path.join(LOOP_DIR, "libfedagg_comm_loop.so")
+    drv_src = os.path.join(LOOP_DIR, "loop_round.cpp")
+    drv = os.path.join(LOOP_DIR, "loop_round")
+    if force or _stale(ccl, [ccl_src]):
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC", "-shared",
+                        "-Wall", "-Wl,-soname,libloopccl.so", "-o", ccl + ".tmp", ccl_src],
+                       check=True)
+        os.replace(ccl + ".tmp", ccl)
+    if force or _stale(comm, COMM_DEPS + [OUT, ccl]):
+        subprocess.run([HIPCC, *FLAGS, "-Wl,-soname,libfedagg_comm_loop.so", "-o", comm + ".tmp",
+                        COMM_SRC, "-L" + HERE, "-lfedagg", "-L" + LOOP_DIR, "-lloopccl",
+                        "-Wl,-rpath,$ORIGIN:$ORIGIN/../../feddct_amd"], check=True)
+        os.replace(comm + ".tmp", comm)
+    if force or _stale(drv, [drv_src, comm, os.path.join(HERE, "..", "include", "fedagg_comm.h")]):
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O2", "-std=c++17", inc, "-o",
+                        drv + ".tmp", drv_src, "-L" + HERE, "-lfedagg", "-L" + LOOP_DIR,
+                        "-lfedagg_comm_loop", "-lloopccl", "-pthread",
+                        "-Wl,-rpath,$ORIGIN:$ORIGIN/../../feddct_amd"], check=True)
+        os.replace(drv + ".tmp", drv)
+    return drv

@@ -1,0 +1,124 @@
+"""GPU: the native multi-rank rounds of libfedagg_comm (fedcomm.hip, unchanged)
+with W = 2..8 ranks on the one GPU of the box, over an in-process loopback of
+the RCCL calls it makes (tests/loopback/loopccl.hip; RCCL itself refuses two
+ranks on one device).  The C++ driver (tests/loopback/loop_round.cpp) builds
+the clients with the portable synthetic state, runs one round per case and
+compares every result rank with one GPU's fa_reduce over all clients:
+chained and striped bit for bit, sharded (e1) within the forward error bound
+of two N-term sums; int64 keys bit for bit everywhere.
+
+Both process models of fedcomm run: one thread + communicator per rank
+(fa_comm_init_rank — the product's one-process-per-GPU model, ranks progress
+independently) for every mode, and one thread driving every rank
+(fa_comm_init) for the sharded rounds.  The chained and striped schedules
+pair a send in one step with its receive in a later step of another rank;
+RCCL matches those on the device, a host-side loopback driven by one thread
+cannot (the receive would wait for a send the same thread has not issued),
+so their single-thread form is left to tests/schedsim.py.  Cases cover
+uneven counts, a rank without clients, every root (first, middle, last, all),
+weighted rounds, 1..13 column chunks, N >= 256 (the deep cascade's four state
+planes) and the layouts of BASELINE configs 3 and 5."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from conftest import load_manifest
+from feddct_amd.layout import BucketLayout
+from feddct_amd.workload import joint_manifest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "tests", "loopback", "loop_round")
+
+
+def _write_layout(layout, path):
+    with open(path, "w") as f:
+        f.write(f"{layout.f32_numel} {layout.i64_numel} {len(layout.segs32)} "
+                f"{len(layout.segs64)}\n")
+        for o, m in list(layout.segs32) + list(layout.segs64):
+            f.write(f"{int(o)} {int(m)}\n")
+
+
+def _run(layout, cases, tmp_path, timeout=240):
+    assert os.path.exists(DRIVER), "tests/loopback/loop_round is not built (run build())"
+    lf = str(tmp_path / "layout.txt")
+    _write_layout(layout, lf)
+    env = dict(os.environ, FA_LOOP_TIMEOUT_S="30")
+    p = subprocess.run([DRIVER, lf, *cases], capture_output=True, text=True, timeout=timeout,
+                       env=env)
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    for r in rows:
+        print(json.dumps(r))
+    assert len(rows) == len(cases), (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    bad = [r for r in rows if not r["ok"]]
+    assert not bad, (bad, p.stderr[-2000:])
+    assert p.returncode == 0, p.stderr[-2000:]
+    return rows
+
+
+def _small_layout():
+    """Every column class the schedules treat separately: vector runs, ILP-4
+    tails, 0-d fp32 keys between vector keys, unaligned sizes, int64 keys."""
+    return BucketLayout([("a", (37, 3), "float32"), ("s", (), "float32"),
+                         ("b", (4101,), "float32"), ("t", (), "float32"),
+                         ("c", (70000,), "float32"), ("d", (3,), "float32"),
+                         ("e", (193,), "float32"), ("n1", (), "int64"),
+                         ("f", (65, 65), "float32"), ("n2", (), "int64")])
+
+
+@pytest.fixture(scope="module")
+def cfg3_layout():
+    mm, pm = load_manifest("wrnsl16_8_sf4_c10_main"), load_manifest("wrnsl16_8_sf4_c10_proxy")
+    return BucketLayout.from_manifest(joint_manifest([mm, pm]))
+
+
+def test_loopback_small_layout_all_modes(tmp_path):
+    cases = [
+        "chained:2:3,2:-1:threads:0:1",
+        "chained:3:2,0,3:0:threads:0:4",
+        "chained:3:4,5,3:1:threads:1:3",
+        "chained:5:4,4,4,4,4:4:threads:1:13",
+        "chained:8:1,2,1,3,1,1,2,9:-1:threads:0:8",
+        "chained:4:65,65,65,65:3:threads:0:4",          # N=260: four state planes
+        "striped:2:3,2:0:threads:0:0",
+        "striped:3:2,0,3:-1:threads:0:0",
+        "striped:8:1,2,1,3,1,1,2,9:5:threads:0:0",
+        "striped:4:65,65,65,65:-1:threads:0:0",          # N=260: device pointer tables
+        "sharded:4:65,65,65,65:0:threads:1:4",
+        "sharded:2:3,2:0:threads:0:8",
+        "sharded:4:5,0,2,1:-1:threads:1:4",
+        "sharded:3:4,5,3:2:single:0:1",
+        "sharded_rs:2:3,2:0:threads:0:8",
+        "sharded_rs:4:5,1,2,1:-1:threads:1:4",
+        "sharded_rs:8:1,2,1,3,1,1,2,9:7:threads:0:13",
+        "sharded_rs:3:4,5,3:-1:single:0:2",
+    ]
+    _run(_small_layout(), cases, tmp_path)
+
+
+def test_loopback_cfg3_layout(cfg3_layout, tmp_path):
+    """BASELINE config 3's joint FedDCT bucket (main + proxy, 11.0 M floats),
+    5 client slots over 2..5 ranks."""
+    cases = [
+        "chained:2:3,2:-1:threads:0:8",
+        "chained:5:1,1,1,1,1:4:threads:0:8",
+        "chained:3:2,1,2:0:threads:1:4",
+        "striped:2:3,2:1:threads:0:0",
+        "striped:4:2,1,1,1:-1:threads:0:0",
+        "sharded:2:3,2:0:threads:0:8",
+        "sharded_rs:4:2,1,1,1:-1:threads:1:8",
+    ]
+    _run(cfg3_layout, cases, tmp_path)
+
+
+def test_loopback_cfg5_sharded_chain(tmp_path):
+    """BASELINE config 5's shape: 24 FedDCT slots (wrnsl16_8 sf4 C100) over
+    8 ranks of 3 slots, chained to the last rank and to every rank."""
+    mm, pm = load_manifest("wrnsl16_8_sf4_c100_main"), load_manifest("wrnsl16_8_sf4_c100_proxy")
+    lay = BucketLayout.from_manifest(joint_manifest([mm, pm]))
+    cases = ["chained:8:3,3,3,3,3,3,3,3:7:threads:0:8",
+             "chained:8:3,3,3,3,3,3,3,3:-1:threads:0:8"]
+    _run(lay, cases, tmp_path, timeout=300)
