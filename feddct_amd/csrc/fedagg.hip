@@ -1176,6 +1176,48 @@ int cached_plan(const fa_seg* s32, int n32, int64_t numel32, const fa_seg* s64, 
 }  // namespace
 
 // =================================================================== ABI ==
+namespace {
+// Client pointer tables (N > kInline) come from a private stream-ordered pool
+// whose freed blocks are reused only by the stream that freed them: cross-
+// stream reuse (opportunistic or internal-dependency) is switched off, so a
+// table still read by a kernel on one stream can never be handed to another
+// stream (the executor in fedcomm.hip drives two).  The loopback test of the
+// multi-rank rounds saw payload corruption with cross-stream frees on the
+// default pool (tests/loopback/loopccl.hip).
+hipError_t table_alloc(void** p, size_t bytes, hipStream_t st) {
+  static std::mutex mu;
+  static std::map<int, hipMemPool_t> pools;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  hipMemPool_t pool = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = pools.find(dev);
+    if (it != pools.end()) {
+      pool = it->second;
+    } else {
+      hipMemPoolProps props{};
+      props.allocType = hipMemAllocationTypePinned;
+      props.location.type = hipMemLocationTypeDevice;
+      props.location.id = dev;
+      e = hipMemPoolCreate(&pool, &props);
+      if (e != hipSuccess) return e;
+      int off = 0;
+      for (hipMemPoolAttr a : {hipMemPoolReuseFollowEventDependencies,
+                               hipMemPoolReuseAllowOpportunistic,
+                               hipMemPoolReuseAllowInternalDependencies})
+        if ((e = hipMemPoolSetAttribute(pool, a, &off)) != hipSuccess) return e;
+      uint64_t keep = UINT64_MAX;  // keep freed blocks for the next round
+      if ((e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep)) != hipSuccess)
+        return e;
+      pools[dev] = pool;
+    }
+  }
+  return hipMallocFromPoolAsync(p, bytes, pool, st);
+}
+}  // namespace
+
 extern "C" {
 
 const char* fa_version(void) { return FA_VERSION_STR; }
@@ -1521,7 +1563,7 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
       h64[i] = need64 ? (const void*)c64[i] : nullptr;
       hw[i] = weights ? weights[i] : 0.f;
     }
-    HIP_TRY(hipMallocAsync(&table, host.size(), st));
+    HIP_TRY(table_alloc(&table, host.size(), st));
     HIP_TRY(hipMemcpyAsync(table, host.data(), host.size(), hipMemcpyHostToDevice, st));
     a.tab32 = (const float* const*)table;
     a.tab64 = (const int64_t* const*)((const void**)table + n);
@@ -1660,7 +1702,7 @@ int fa_reduce_chain(const fa_plan* plan, const float* const* c32, int n, const f
       h32[n + i] = nullptr;
       hw[i] = weights ? weights[i] : 0.f;
     }
-    HIP_TRY(hipMallocAsync(&table, host.size(), s));
+    HIP_TRY(table_alloc(&table, host.size(), s));
     HIP_TRY(hipMemcpyAsync(table, host.data(), host.size(), hipMemcpyHostToDevice, s));
     a.tab32 = (const float* const*)table;
     a.tab64 = (const int64_t* const*)((const void**)table + n);
