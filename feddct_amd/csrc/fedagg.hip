@@ -676,60 +676,47 @@ __device__ __forceinline__ float tgpu_outer(const Src& src, int64_t e, int n) {
   return v[0];
 }
 
-template <class Src>
-__device__ float tgpu_outer_any(const Src& src, int64_t e, int n, int ls) {
-  switch (ls) {
-    case 0: return tgpu_outer<Src, 1>(src, e, n);
-    case 1: return tgpu_outer<Src, 2>(src, e, n);
-    case 2: return tgpu_outer<Src, 4>(src, e, n);
-    case 3: return tgpu_outer<Src, 8>(src, e, n);
-    default: return tgpu_outer<Src, 16>(src, e, n);
-  }
-}
-
 // The same order for 4 consecutive elements of one tensor per lane (the
 // order depends only on (N, M), so the 4 lanes of a float4 are 4 independent
-// copies of it): 16-B non-temporal loads, the rows' loads of one round-robin
-// step issued together.  Vector adds are per-component IEEE adds (no
-// multiply feeds them, so contraction cannot apply).
+// copies of it): 16-B non-temporal loads, up to eight rows' loads (two
+// round-robin steps) in flight per lane.  Vector adds are per-component IEEE
+// adds (no multiply feeds them, so contraction cannot apply).
 template <int S>
 __device__ __forceinline__ f4 tgpu_outer4(KArgs& a, int64_t start, uint32_t v, int n) {
   f4 val[S];
 #pragma unroll
   for (int y = 0; y < S; ++y) {
+    // part y's p-th row is y + p*S; row p goes into accumulator p % 4.  Rows
+    // are loaded B at a time, then added in row order, so every accumulator
+    // still sees its rows in increasing order.
     const f4 z = {0.f, 0.f, 0.f, 0.f};
-    f4 a0 = z, a1 = z, a2 = z, a3 = z;
-    int r = y;
-    for (; r + 3 * S < n; r += 4 * S) {
-      const f4 x0 = ldg4<true>(cptr32(a, r) + start, v);
-      const f4 x1 = ldg4<true>(cptr32(a, r + S) + start, v);
-      const f4 x2 = ldg4<true>(cptr32(a, r + 2 * S) + start, v);
-      const f4 x3 = ldg4<true>(cptr32(a, r + 3 * S) + start, v);
-      a0 += x0;
-      a1 += x1;
-      a2 += x2;
-      a3 += x3;
+    f4 acc[4] = {z, z, z, z};
+    const int np = (n - y + S - 1) / S;
+    constexpr int B = S >= 8 ? 4 : 8;  // rows in flight (register budget of val[S])
+    int p = 0;
+    for (; p + B <= np; p += B) {
+      f4 x[B];
+#pragma unroll
+      for (int i = 0; i < B; ++i) x[i] = ldg4<true>(cptr32(a, y + (p + i) * S) + start, v);
+#pragma unroll
+      for (int i = 0; i < B; ++i) acc[i & 3] += x[i];
     }
-    if (r < n) a0 += ldg4<true>(cptr32(a, r) + start, v);
-    if (r + S < n) a1 += ldg4<true>(cptr32(a, r + S) + start, v);
-    if (r + 2 * S < n) a2 += ldg4<true>(cptr32(a, r + 2 * S) + start, v);
-    val[y] = ((a0 + a1) + a2) + a3;
+    if (p < np) {  // p % 4 == 0 here: row p + i goes into accumulator i & 3
+      f4 x[B];
+#pragma unroll
+      for (int i = 0; i < B; ++i)
+        if (p + i < np) x[i] = ldg4<true>(cptr32(a, y + (p + i) * S) + start, v);
+#pragma unroll
+      for (int i = 0; i < B; ++i)
+        if (p + i < np) acc[i & 3] += x[i];
+    }
+    val[y] = ((acc[0] + acc[1]) + acc[2]) + acc[3];
   }
 #pragma unroll
   for (int off = S / 2; off > 0; off /= 2)
 #pragma unroll
     for (int y = 0; y < off; ++y) val[y] = val[y] + val[y + off];
   return val[0];
-}
-
-__device__ f4 tgpu_outer4_any(KArgs& a, int64_t start, uint32_t v, int n, int ls) {
-  switch (ls) {
-    case 0: return tgpu_outer4<1>(a, start, v, n);
-    case 1: return tgpu_outer4<2>(a, start, v, n);
-    case 2: return tgpu_outer4<4>(a, start, v, n);
-    case 3: return tgpu_outer4<8>(a, start, v, n);
-    default: return tgpu_outer4<16>(a, start, v, n);
-  }
 }
 
 // lane value of the inner order; the wave then runs the shuffle tree
@@ -743,8 +730,15 @@ __device__ __forceinline__ float tgpu_inner(const Src& src, int64_t e, int n, in
   return v;
 }
 
+// One instantiation per row split S = 1 << LS (the plan groups its tiles by
+// S and launches each group): a single S per kernel keeps the register
+// budget of the parts' values to that S (a runtime switch over S = 1..16 in
+// one kernel needed 300 VGPRs and spilled).  Inner tiles (M == 1) ride in
+// the LS = 0 group; their own field is the lane count exponent.
+template <int LS>
 __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   (void)args;
+  constexpr int S = 1 << LS;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const Tile t = a.tiles[blockIdx.x];
   const float fac = a.tfac[blockIdx.x];
@@ -754,7 +748,7 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   if (base == K_F32_TGPU_V) {
     const uint32_t v = threadIdx.x;
     if ((int)(v * 4) >= t.count) return;
-    f4 r = tgpu_outer4_any(a, t.start, v, n, ls);
+    f4 r = tgpu_outer4<S>(a, t.start, v, n);
     if (!sum_only)
       r = f4{__fmul_rn(r.x, fac), __fmul_rn(r.y, fac), __fmul_rn(r.z, fac), __fmul_rn(r.w, fac)};
     stg4<true>(a.out32 + t.start, v, r);
@@ -767,13 +761,13 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
     if (j >= t.count) return;
     const int64_t e = t.start + j;
     if (base == K_F32_TGPU) {
-      const float s = tgpu_outer_any(SrcF32{a, false}, e, n, ls);
+      const float s = tgpu_outer<SrcF32, S>(SrcF32{a, false}, e, n);
       const float r = sum_only ? s : __fmul_rn(s, fac);
       a.out32[e] = r;
       if (a.flags & FA_F_BCAST)
         for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
     } else {
-      const int64_t r = (int64_t)__fmul_rn(tgpu_outer_any(SrcI64{a}, e, n, ls), fac);
+      const int64_t r = (int64_t)__fmul_rn(tgpu_outer<SrcI64, S>(SrcI64{a}, e, n), fac);
       a.out64[e] = r;
       if (a.flags & FA_F_BCAST)
         for (int i = 0; i < n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
@@ -921,6 +915,7 @@ struct fa_plan {
   int order = FA_ORDER_TORCH_CPU;
   int order_n = 0;        // FA_ORDER_TORCH_GPU: the client count it was cut for
   float* d_fac = nullptr; // ... and its per-tile mean factors
+  int tg_lo[6] = {0, 0, 0, 0, 0, 0};  // ... tiles grouped by row split S = 1..16
 };
 
 namespace {
@@ -1326,6 +1321,7 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
   if (rc) return rc;
   std::vector<Tile> t;
   std::vector<float> fac;
+  std::vector<int> order_groups_tmp;
   for (int pass = 0; pass < 2; ++pass) {
     for (const fa_seg& g : pass ? s64 : s32) {
       if (g.numel == 0) continue;
@@ -1367,7 +1363,31 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
       scalar(head + body, g.numel);
     }
   }
+  // group the tiles by row split (inner tiles with S = 1): one launch each
+  {
+    std::vector<int> grp(t.size());
+    for (size_t i = 0; i < t.size(); ++i) {
+      const int b = t[i].kind & 0xFF;
+      grp[i] = (b == K_F32_TGPU_IN || b == K_I64_TGPU_IN) ? 0 : (t[i].kind >> 8) & 0xFF;
+    }
+    std::vector<size_t> ord(t.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return grp[x] < grp[y]; });
+    std::vector<Tile> t2;
+    std::vector<float> f2;
+    for (size_t i : ord) {
+      t2.push_back(t[i]);
+      f2.push_back(fac[i]);
+    }
+    t.swap(t2);
+    fac.swap(f2);
+    int lo[6] = {0, 0, 0, 0, 0, 0};
+    for (size_t i = 0; i < ord.size(); ++i) lo[grp[ord[i]] + 1]++;
+    for (int g = 0; g < 5; ++g) lo[g + 1] += lo[g];
+    order_groups_tmp.assign(lo, lo + 6);
+  }
   fa_plan* p = new fa_plan();
+  for (int g = 0; g < 6; ++g) p->tg_lo[g] = order_groups_tmp[g];
   p->info.f32_numel = f32_numel;
   p->info.i64_numel = i64_numel;
   p->info.tile_elems = 4 * kBlock;
@@ -1575,10 +1595,22 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
       return set_err(FA_E_INVAL, "fa_reduce: torch-GPU-order plan cut for n=%d, called with n=%d",
                      plan->order_n, n);
     }
-    a.ntiles = in.ntiles;
-    a.tfac = plan->d_fac;
-    hipLaunchKernelGGL(tgpu_kernel, dim3(in.ntiles), dim3(kBlock), 0, st, a);
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipSuccess;
+    for (int g = 0; g < 5 && e == hipSuccess; ++g) {
+      const int lo = plan->tg_lo[g], cnt = plan->tg_lo[g + 1] - lo;
+      if (cnt == 0) continue;
+      a.tiles = plan->d_tiles + lo;
+      a.tfac = plan->d_fac + lo;
+      a.ntiles = cnt;
+      switch (g) {
+        case 0: hipLaunchKernelGGL(tgpu_kernel<0>, dim3(cnt), dim3(kBlock), 0, st, a); break;
+        case 1: hipLaunchKernelGGL(tgpu_kernel<1>, dim3(cnt), dim3(kBlock), 0, st, a); break;
+        case 2: hipLaunchKernelGGL(tgpu_kernel<2>, dim3(cnt), dim3(kBlock), 0, st, a); break;
+        case 3: hipLaunchKernelGGL(tgpu_kernel<3>, dim3(cnt), dim3(kBlock), 0, st, a); break;
+        default: hipLaunchKernelGGL(tgpu_kernel<4>, dim3(cnt), dim3(kBlock), 0, st, a); break;
+      }
+      e = hipGetLastError();
+    }
     if (table) {
       hipError_t e2 = hipFreeAsync(table, st);
       if (e == hipSuccess) e = e2;
