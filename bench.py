@@ -814,6 +814,10 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
     """N>1 (weak scaling: 20 client slots per GPU, slot order = rank order).
     Every round form is timed over the same K steps (max over ranks):
 
+    * blocked (exact client shards, native fa_reduce_blocked): block sums
+      where the slots lie, the few partials cut by a shard boundary relayed
+      through the column-stripe owners, the owners fold — no rank-to-rank
+      pipeline;
     * chained (exact client shards; native fa_reduce_chained and the
       torch.distributed ChainAggregator): the shards stay put, the cascade
       state hops rank to rank — the north_star's client-sharded partitioning
@@ -855,8 +859,14 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
         except Exception as e:  # noqa: BLE001
             extra["native_comm_error"] = repr(e)
     if ncomm is not None:
-        from feddct_amd.comm import (FA_XCHG_RS_GATHER, NativeChainedAggregator,
-                                     NativeShardedAggregator, NativeStripedAggregator)
+        from feddct_amd.comm import (FA_XCHG_RS_GATHER, NativeBlockedAggregator,
+                                     NativeChainedAggregator, NativeShardedAggregator,
+                                     NativeStripedAggregator)
+        run_mode("blocked/native", lambda o32, o64: NativeBlockedAggregator(
+            layout, l32, l64, n_total, o32, o64, ncomm, final="reduce", root=0).step, 0, True)
+        run_mode("blocked/native/allreduce", lambda o32, o64: NativeBlockedAggregator(
+            layout, l32, l64, n_total, o32, o64, ncomm, final="allreduce").step, -1, True,
+            steps=max(5, args.steps // 2))
         run_mode("chained/native", lambda o32, o64: NativeChainedAggregator(
             layout, l32, l64, n_total, o32, o64, ncomm, nchunks=args.chain_chunks,
             final="reduce", root=last).step, last, True)

@@ -33,14 +33,16 @@ COMM_EXPORTS = ["fa_comm_unique_id", "fa_comm_init_rank", "fa_comm_init", "fa_co
                 "fa_shard_plan_destroy", "fa_reduce_sharded", "fa_mean_f32_multi",
                 "fa_stripe_plan_create", "fa_stripe_plan_destroy", "fa_reduce_striped",
                 "fa_chain_plan_create", "fa_chain_plan_destroy", "fa_reduce_chained",
+                "fa_block_plan_create", "fa_block_plan_destroy", "fa_reduce_blocked",
                 "fa_describe_round"]
 
 FA_XCHG_REDUCE, FA_XCHG_RS_GATHER = 0, 1
-FA_MODE_SHARDED, FA_MODE_STRIPED, FA_MODE_CHAINED = 0, 1, 2
+FA_MODE_SHARDED, FA_MODE_STRIPED, FA_MODE_CHAINED, FA_MODE_BLOCKED = 0, 1, 2, 3
 X = dict(SEND=1, RECV=2, REDUCE=3, ALLREDUCE=4, REDUCE_SCATTER=5, GATHER=6, ALLGATHER=7, BCAST=8,
          K_SUM=16, K_ZERO=17, K_DIV=18, K_COPY=19, K_STRIPE=20, K_CHAIN=21, K_STACK=22,
-         K_TAILS=23)
-B = dict(NONE=0, CLIENT=1, OUT=2, PARTIAL=4, RECV=5, STRIPE=6, STATE=7, FIN=8, STACK=9, GATHER=10)
+         K_TAILS=23, K_PART=24, K_CONT=25, K_BLOCK=26, K_FOLD=27)
+B = dict(NONE=0, CLIENT=1, OUT=2, PARTIAL=4, RECV=5, STRIPE=6, STATE=7, FIN=8, STACK=9, GATHER=10,
+         PIN=11, TAILP=12, CONT=13, BSUM=14, BLK=15, RELAY=16)
 XNAME = {v: k for k, v in X.items()}
 BNAME = {v: k for k, v in B.items()}
 
@@ -85,6 +87,10 @@ def _load():
                                  ctypes.c_uint, ctypes.POINTER(_P)],
         "fa_chain_plan_destroy": [_P],
         "fa_reduce_chained": [ctypes.POINTER(_P), _I, ctypes.POINTER(FaShardIO), _I],
+        "fa_block_plan_create": [_P, _P, _I, _I64, _P, _I, _I64, ctypes.POINTER(_I),
+                                 ctypes.c_uint, ctypes.POINTER(_P)],
+        "fa_block_plan_destroy": [_P],
+        "fa_reduce_blocked": [ctypes.POINTER(_P), _I, ctypes.POINTER(FaShardIO), _I],
         "fa_describe_round": [_I, _I, _I, ctypes.POINTER(_I), _P, _I, _I64, _P, _I, _I64, _I, _I,
                               ctypes.c_uint, _I, _I, ctypes.POINTER(FaXfer), _I,
                               ctypes.POINTER(_I)],
@@ -386,3 +392,71 @@ class NativeChainedAggregator(NativeShardedAggregator):
         self.io.stream = s
         _lib.check(lib().fa_reduce_chained(self._plans, 1, ctypes.byref(self.io), self.root),
                    "fa_reduce_chained")
+
+
+class BlockPlan:
+    """This rank's blocked-mode plan (block-sum planes, the stripe it owns,
+    relay rows, the raw scalar-column gather buffers)."""
+
+    def __init__(self, comm: Comm, layout: BucketLayout, counts: Sequence[int]):
+        a32, n32, a64, n64 = _segs(layout)
+        c = (_I * len(counts))(*map(int, counts))
+        h = _P()
+        _lib.check(lib().fa_block_plan_create(comm.handle, a32, n32, int(layout.f32_numel), a64,
+                                              n64, int(layout.i64_numel), c,
+                                              _lib.FA_PLAN_GAPS_ARE_PADDING, ctypes.byref(h)),
+                   "fa_block_plan_create")
+        self.handle = h
+        self.comm = comm
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                lib().fa_block_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+class NativeBlockedAggregator(NativeChainedAggregator):
+    """The exact client-sharded round (fa_reduce_blocked): every rank sums the
+    cascade blocks it holds; a block cut by a shard boundary carries its
+    level-0 partial (one plane, relayed through the column-stripe owners) to
+    the next rank; the block sums go to the stripe owners, which fold them in
+    block order — train_feddct.py:42-50's order over all slots, without the
+    chained round's rank-to-rank pipeline.  Same arguments as the chained
+    form; requires every 16-slot block to lie on at most two ranks."""
+
+    def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
+                 local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
+                 out64: torch.Tensor, comm: Comm, final: str = "reduce", root: int = 0,
+                 weights: Optional[Sequence[float]] = None,
+                 counts: Optional[Sequence[int]] = None):
+        if final not in ("reduce", "allreduce"):
+            raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
+        world, rank, _ = comm.info()
+        if counts is None:
+            counts = [b - a for a, b in (shard_range(n_total, world, r) for r in range(world))]
+        if len(local32) != counts[rank] or sum(counts) != n_total:
+            raise ValueError(f"rank {rank} holds {len(local32)} clients, shard is {counts[rank]}")
+        self.plan = BlockPlan(comm, layout, counts)
+        self.root = root if final == "reduce" else -1
+        self._a32 = _lib.ptr_array([t.data_ptr() for t in local32])
+        self._a64 = _lib.ptr_array([t.data_ptr() for t in local64])
+        self._w = (None if weights is None
+                   else (ctypes.c_float * max(1, len(weights)))(*map(float, weights)))
+        self._plans = (_P * 1)(self.plan.handle.value)
+        self.io = FaShardIO()
+        self.io.c32 = ctypes.cast(self._a32, _P)
+        self.io.c64 = ctypes.cast(self._a64, _P) if layout.i64_numel else None
+        self.io.weights = ctypes.cast(self._w, _P) if self._w is not None else None
+        self.io.out32 = out32.data_ptr()
+        self.io.out64 = out64.data_ptr() if layout.i64_numel else None
+        self._keep = (local32, local64, out32, out64)
+
+    def step(self, stream=None) -> None:
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self.io.stream = s
+        _lib.check(lib().fa_reduce_blocked(self._plans, 1, ctypes.byref(self.io), self.root),
+                   "fa_reduce_blocked")

@@ -109,6 +109,45 @@ __global__ void scatter_f32_kernel(const float* __restrict__ src, const int64_t*
     dst[idx[e]] = src[e];
 }
 
+// Blocked mode: an owner's fold of the block sums of its column stripe, in
+// block order, with the cascade's promotions after every 2^lp-th block
+// (levels 1-3 of fa_reduce's accumulators: the block after row i = (k+1)<<lp
+// promotes exactly as reduce_kernel's `promote` does at row i), then the
+// finish ((rem + l1) + l2) + l3 and the division.  blk: nblk + has_rem rows
+// of `row` floats (the remainder block's partial last).
+struct FoldArgs {
+  const float* blk;
+  int64_t row;
+  int64_t count;
+  float* out;
+  int nblk;
+  int has_rem;
+  int lp;
+  int n_total;
+  int divide;
+};
+__global__ void fold_kernel(FoldArgs a) {
+  const int mask = (1 << a.lp) - 1;
+  const float fn = (float)a.n_total;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < a.count;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float l1 = 0.f, l2 = 0.f, l3 = 0.f;
+    for (int k = 0; k < a.nblk; ++k) {
+      l1 = __fadd_rn(l1, a.blk[(size_t)k * a.row + e]);
+      const int i = (k + 1) << a.lp;
+      if ((i & (mask << a.lp)) != 0) continue;
+      l2 = __fadd_rn(l2, l1);
+      l1 = 0.f;
+      if ((i & (mask << (2 * a.lp))) != 0) continue;
+      l3 = __fadd_rn(l3, l2);
+      l2 = 0.f;
+    }
+    const float l0 = a.has_rem ? a.blk[(size_t)a.nblk * a.row + e] : 0.f;
+    const float s = __fadd_rn(__fadd_rn(__fadd_rn(l0, l1), l2), l3);
+    a.out[e] = a.divide ? __fdiv_rn(s, fn) : s;
+  }
+}
+
 int launch_stack(bool f32, const void* const* src, const float* w, int n_local, void* dst,
                  const int64_t* idx, int64_t width, int64_t stride, hipStream_t s) {
   for (int j0 = 0; j0 < n_local; j0 += kStackPtrs) {
@@ -382,6 +421,22 @@ struct ChainGeo {
   int64_t t32_row = 0;                             // their stack row stride (64-aligned)
 };
 
+// Blocked mode geometry (host-only, the same on every rank).  Pieces are the
+// cascade's blocks of 2^lp slots (0..K-1) and the remainder block (K, when
+// n_total % 2^lp); a piece's slots lie on its starter and holder ranks.
+struct BlockGeo {
+  int lp = 4;
+  int K = 0, P = 0;                       // complete blocks, pieces (K + remainder)
+  std::vector<int> s0, s1;                // piece rows [s0, s1)
+  std::vector<int> starter, holder;       // first / last row's rank
+  std::vector<int> bsum_slot;             // local pieces: BSUM index on the holder (-1: spans)
+  std::vector<int> plane;                 // spanning complete blocks: CONT plane of the sum
+  int tail_piece = -1, head_piece = -1;   // this rank's spanning piece it starts / ends
+  int nbsum = 0;                          // local pieces of this rank
+  std::vector<int64_t> slo, shi;          // owner column stripes (vector tiles)
+  int64_t row = 0;                        // stripe row stride (floats, 64-aligned)
+};
+
 void sched_chained(const Geo& g, const ChainGeo& cg, int root, Sched* S) {
   const int me = g.rank, F = cg.finisher;
   const bool result = root < 0 || root == me;
@@ -440,6 +495,113 @@ void sched_chained(const Geo& g, const ChainGeo& cg, int root, Sched* S) {
   S->next();
 }
 
+// Blocked: block sums where they lie, spanning blocks' partials relayed
+// through the stripe owners, block sums to the owners, fold, results out.
+void sched_blocked(const Geo& g, const ChainGeo& cg, const BlockGeo& bg, int root, Sched* S) {
+  const int me = g.rank, W = g.nranks;
+  const bool result = root < 0 || root == me;
+  const bool i64 = !g.t64.empty();
+  auto w_of = [&](int s) { return bg.shi[s] - bg.slo[s]; };
+  // step 0: local work, the partial a neighbour waits for first
+  if ((i64 || cg.t32_width) && g.n_local > 0)
+    S->add(FA_X_K_STACK, -1, FA_B_CLIENT, -1, FA_B_STACK, -1, 0, 0, -1, g.lo_slot, g.n_local);
+  if (bg.tail_piece >= 0) {
+    const int i = bg.tail_piece;
+    S->add(FA_X_K_PART, -1, FA_B_PIN, -1, FA_B_TAILP, 0, 0, 0, -1, bg.s0[i],
+           g.lo_slot + g.n_local - bg.s0[i]);
+  }
+  for (int i = 0; i < bg.P; ++i)
+    if (bg.bsum_slot[i] >= 0)
+      S->add(FA_X_K_BLOCK, -1, FA_B_CLIENT, -1, FA_B_BSUM, bg.bsum_slot[i], 0, 0, i, bg.s0[i],
+             bg.s1[i] - bg.s0[i]);
+  S->next();
+  // step 1: raw columns gathered; each spanning partial split into stripes,
+  // to its holder directly (the starter's and the holder's own stripes) or
+  // to the stripe's owner
+  if (cg.t32_width)
+    S->add(FA_X_ALLGATHER, -1, FA_B_STACK, 0, FA_B_GATHER, 0, 0, (int64_t)g.nmax * cg.t32_row);
+  if (i64)
+    S->add(FA_X_ALLGATHER, -1, FA_B_STACK, 1, FA_B_GATHER, 1, 0, (int64_t)g.nmax * g.i64_numel);
+  for (int i = 0; i < bg.P; ++i) {
+    const int r1 = bg.starter[i], r2 = bg.holder[i];
+    if (r1 == r2) continue;
+    for (int s = 0; s < W; ++s) {
+      const int64_t w = w_of(s);
+      if (w == 0) continue;
+      const int64_t off = bg.slo[s];
+      const bool direct = s == r1 || s == r2;
+      if (me == r1) S->add(FA_X_SEND, direct ? r2 : s, FA_B_TAILP, 0, FA_B_NONE, -1, off, w);
+      if (direct && me == r2) S->add(FA_X_RECV, r1, FA_B_NONE, -1, FA_B_PIN, 0, off, w);
+      if (!direct && me == s) S->add(FA_X_RECV, r1, FA_B_NONE, -1, FA_B_RELAY, r1, off, w);
+    }
+  }
+  S->next();
+  // step 2: the owners forward their stripes of the partials
+  for (int i = 0; i < bg.P; ++i) {
+    const int r1 = bg.starter[i], r2 = bg.holder[i];
+    if (r1 == r2) continue;
+    for (int s = 0; s < W; ++s) {
+      const int64_t w = w_of(s);
+      if (w == 0 || s == r1 || s == r2) continue;
+      if (me == s) S->add(FA_X_SEND, r2, FA_B_RELAY, r1, FA_B_NONE, -1, bg.slo[s], w);
+      if (me == r2) S->add(FA_X_RECV, s, FA_B_NONE, -1, FA_B_PIN, 0, bg.slo[s], w);
+    }
+  }
+  S->next();
+  // step 3: the holder finishes the spanning block (or the remainder)
+  if (bg.head_piece >= 0) {
+    const int i = bg.head_piece;
+    S->add(FA_X_K_CONT, -1, FA_B_PIN, -1, FA_B_CONT, bg.plane[i], 0, 0, i, g.lo_slot,
+           bg.s1[i] - g.lo_slot);
+  }
+  S->next();
+  // step 4: every piece's stripes to their owners, in piece order
+  for (int i = 0; i < bg.P; ++i) {
+    const int h = bg.holder[i];
+    const bool local = bg.starter[i] == h;
+    for (int s = 0; s < W; ++s) {
+      const int64_t w = w_of(s);
+      if (w == 0 || s == h) continue;
+      if (me == h) {
+        if (local) S->add(FA_X_SEND, s, FA_B_BSUM, bg.bsum_slot[i], FA_B_NONE, -1, bg.slo[s], w);
+        else S->add(FA_X_SEND, s, FA_B_CONT, bg.plane[i], FA_B_NONE, -1, bg.slo[s], w);
+      }
+      if (me == s) S->add(FA_X_RECV, h, FA_B_NONE, -1, FA_B_BLK, i, bg.slo[s], w);
+    }
+  }
+  S->next();
+  // step 5: own pieces into the stripe, then the fold
+  const int64_t wme = w_of(me);
+  if (wme > 0) {
+    for (int i = 0; i < bg.P; ++i) {
+      if (bg.holder[i] != me) continue;
+      if (bg.bsum_slot[i] >= 0)
+        S->add(FA_X_K_COPY, -1, FA_B_BSUM, bg.bsum_slot[i], FA_B_BLK, i, bg.slo[me], wme);
+      else
+        S->add(FA_X_K_COPY, -1, FA_B_CONT, bg.plane[i], FA_B_BLK, i, bg.slo[me], wme);
+    }
+    S->add(FA_X_K_FOLD, -1, FA_B_BLK, -1, result ? FA_B_OUT : FA_B_FIN, -1, bg.slo[me], wme, me,
+           0, bg.P);
+  }
+  S->next();
+  // step 6: the folded stripes to the result ranks
+  for (int s = 0; s < W; ++s) {
+    const int64_t w = w_of(s);
+    if (w == 0) continue;
+    for (int r = 0; r < W; ++r) {
+      if (r == s || !(root < 0 || root == r)) continue;
+      const bool s_result = root < 0 || root == s;
+      if (me == s)
+        S->add(FA_X_SEND, r, s_result ? FA_B_OUT : FA_B_FIN, -1, FA_B_NONE, -1, bg.slo[s], w);
+      if (me == r) S->add(FA_X_RECV, s, FA_B_NONE, -1, FA_B_OUT, -1, bg.slo[s], w);
+    }
+  }
+  S->next();
+  if (result && (i64 || cg.t32_width))
+    S->add(FA_X_K_TAILS, -1, FA_B_GATHER, -1, FA_B_OUT, -1, 0, 0, -1, 0, g.n_total);
+  S->next();
+}
+
 // The chained mode's cut of the layout: vector tiles chunked, scalar fp32
 // columns compacted (their bucket index per compact column).
 void chain_geo(const Geo& g, int nchunks, ChainGeo* cg, std::vector<fa_tile_desc>* vec,
@@ -476,6 +638,77 @@ void chain_geo(const Geo& g, int nchunks, ChainGeo* cg, std::vector<fa_tile_desc
     if (g.counts[r] > 0) cg->finisher = r;
   cg->lev_in = fa_chain_levels(g.lo_slot, g.n_total);
   cg->lev_out = fa_chain_levels(g.lo_slot + g.n_local, g.n_total);
+}
+
+int rank_of_row(const Geo& g, int i) {
+  for (int r = 0; r < g.nranks; ++r)
+    if (i >= g.first[r] && i < g.first[r] + g.counts[r]) return r;
+  return -1;
+}
+
+int block_geo(const Geo& g, const std::vector<fa_tile_desc>& vec, BlockGeo* bg) {
+  const int n = g.n_total;
+  int lp = 4;
+  {
+    int c = 0;
+    while ((1ll << c) < n) ++c;
+    lp = std::max(4, c / 4);
+  }
+  bg->lp = lp;
+  const int Q = 1 << lp, mask = Q - 1;
+  bg->K = n / Q;
+  bg->P = bg->K + (n % Q ? 1 : 0);
+  bg->s0.clear(); bg->s1.clear(); bg->starter.clear(); bg->holder.clear();
+  bg->bsum_slot.clear(); bg->plane.clear();
+  bg->tail_piece = bg->head_piece = -1;
+  bg->nbsum = 0;
+  for (int i = 0; i < bg->P; ++i) {
+    const int a = i * Q, b = std::min(n, a + Q);
+    const int r0 = rank_of_row(g, a), r1 = rank_of_row(g, b - 1);
+    if (r0 != r1) {
+      // the holder must be the next rank holding slots after the starter
+      int nxt = -1;
+      for (int r = r0 + 1; r < g.nranks && nxt < 0; ++r)
+        if (g.counts[r] > 0) nxt = r;
+      if (nxt != r1 || g.first[r1] + g.counts[r1] < b)
+        return set_err(FA_E_RANGE,
+                       "blocked round: slots %d..%d (one cascade block) lie on more than two "
+                       "ranks; use the chained round",
+                       a, b - 1);
+    }
+    bg->s0.push_back(a);
+    bg->s1.push_back(b);
+    bg->starter.push_back(r0);
+    bg->holder.push_back(r1);
+    int j = 0;
+    if (r0 != r1 && i < bg->K && b < n) {
+      j = 1;
+      if ((b & (mask << lp)) == 0) j = (b & (mask << (2 * lp))) == 0 ? 3 : 2;
+    }
+    bg->plane.push_back(j);  // 0: a finishing continuation writes CONT plane 0
+    if (r0 == r1) {
+      bg->bsum_slot.push_back(r1 == g.rank ? bg->nbsum++ : -1);
+    } else {
+      bg->bsum_slot.push_back(-1);
+      if (r0 == g.rank) bg->tail_piece = i;
+      if (r1 == g.rank) bg->head_piece = i;
+    }
+  }
+  // owner stripes over the vector tiles
+  std::vector<size_t> cut;
+  cut_tiles(vec, g.nranks, &cut);
+  bg->slo.assign(g.nranks, 0);
+  bg->shi.assign(g.nranks, 0);
+  int64_t w = 0;
+  for (int s = 0; s < g.nranks; ++s) {
+    if (cut[s] == cut[s + 1]) continue;
+    bg->slo[s] = vec[cut[s]].start;
+    const fa_tile_desc& t = vec[cut[s + 1] - 1];
+    bg->shi[s] = t.start + t.count;
+    w = std::max(w, bg->shi[s] - bg->slo[s]);
+  }
+  bg->row = (w + 63) / 64 * 64;
+  return FA_OK;
 }
 
 // e1 chunk ranges over the whole bucket.
@@ -547,6 +780,14 @@ struct fa_round_plan {
   float* state = nullptr;    // nplanes * plane floats
   int64_t plane = 0;
   float* fin = nullptr;      // the finisher's result when it is not a result rank
+  // blocked
+  BlockGeo bg;
+  float* pin = nullptr;      // 4 planes: incoming partial (plane 0), zero planes 1-3
+  float* tailp = nullptr;    // 4 planes: outgoing partial
+  float* cont = nullptr;     // 4 planes: the continuation's state / finished sum
+  float* bsum = nullptr;     // nbsum planes: local block sums
+  float* blk = nullptr;      // P stripe rows: the owner's stripe of every piece
+  float* relay = nullptr;    // nranks stripe rows: partials in transit
   // raw scalar columns (int64 keys; chained: also the fp32 tails)
   fa_plan* plan64 = nullptr;
   fa_plan* plan_t32 = nullptr;  // compact tail tiles
@@ -572,8 +813,10 @@ void free_round(fa_round_plan* p) {
   fa_plan_destroy(p->stripe);
   fa_plan_destroy(p->plan64);
   fa_plan_destroy(p->plan_t32);
-  void* bufs[] = {p->partial, p->recv,      p->sbuf,    p->state,     p->fin,       p->tidx,
-                  p->t32_stack, p->t32_gather, p->t32_out, p->i64_stack, p->i64_gather};
+  void* bufs[] = {p->partial,   p->recv,       p->sbuf,    p->state,     p->fin,
+                  p->tidx,      p->t32_stack,  p->t32_gather, p->t32_out, p->i64_stack,
+                  p->i64_gather, p->pin,       p->tailp,   p->cont,      p->bsum,
+                  p->blk,       p->relay};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
@@ -593,9 +836,13 @@ int build_round(fa_round_plan* p, int nchunks, std::vector<fa_tile_desc>* vec_ou
     cut_tiles(g.t32, g.nranks, &cut);
     p->lo = cut_bounds(g.t32, cut, g.f32_numel);
     *cut_out = cut;
-  } else {
+  } else if (p->mode == FA_MODE_CHAINED) {
     chain_geo(g, nchunks, &p->cg, vec_out, cut_out, tails_out, tidx_out);
     p->range = p->cg.range;
+  } else {
+    chain_geo(g, 1, &p->cg, vec_out, cut_out, tails_out, tidx_out);
+    p->range = p->cg.range;
+    return block_geo(g, *vec_out, &p->bg);
   }
   return FA_OK;
 }
@@ -637,11 +884,11 @@ int make_round(fa_comm* comm, int mode, const fa_seg* seg32, int nseg32, int64_t
   std::vector<fa_tile_desc> vec, tails;
   std::vector<size_t> cut;
   std::vector<int64_t> tidx;
-  build_round(p, nchunks, &vec, &cut, &tails, &tidx);
   auto fail = [&](int code) {
     free_round(p);
     return code;
   };
+  if ((rc = build_round(p, nchunks, &vec, &cut, &tails, &tidx))) return fail(rc);
   // tile plans
   if (mode == FA_MODE_SHARDED) {
     for (size_t c = 0; c + 1 < cut.size(); ++c) {
@@ -674,13 +921,28 @@ int make_round(fa_comm* comm, int mode, const fa_seg* seg32, int nseg32, int64_t
       if (rc) return fail(rc);
       p->chunk.push_back(sub);
     }
-    const int nplanes = g.n_total >= 256 ? 4 : 2;
     p->plane = (f32_numel + 63) / 64 * 64;
-    if (!p->chunk.empty()) {
+    if (mode == FA_MODE_CHAINED && !p->chunk.empty()) {
+      const int nplanes = g.n_total >= 256 ? 4 : 2;
       if ((rc = alloc((void**)&p->state, (size_t)nplanes * p->plane * 4, true))) return fail(rc);
       if (g.rank == p->cg.finisher &&
           (rc = alloc((void**)&p->fin, (size_t)f32_numel * 4, true)))
         return fail(rc);
+    }
+    if (mode == FA_MODE_BLOCKED && !p->chunk.empty()) {
+      const BlockGeo& bg = p->bg;
+      const size_t pl = (size_t)p->plane * 4;
+      if (bg.tail_piece >= 0 || bg.head_piece >= 0) {
+        if ((rc = alloc((void**)&p->pin, 4 * pl, true))) return fail(rc);  // planes 1-3 stay 0
+      }
+      if (bg.tail_piece >= 0 && (rc = alloc((void**)&p->tailp, 4 * pl, true))) return fail(rc);
+      if (bg.head_piece >= 0 && (rc = alloc((void**)&p->cont, 4 * pl, true))) return fail(rc);
+      if (bg.nbsum > 0 && (rc = alloc((void**)&p->bsum, (size_t)bg.nbsum * pl, true)))
+        return fail(rc);
+      const size_t rowb = (size_t)bg.row * 4;
+      if ((rc = alloc((void**)&p->blk, (size_t)std::max(1, bg.P) * rowb, true))) return fail(rc);
+      if ((rc = alloc((void**)&p->relay, (size_t)g.nranks * rowb, true))) return fail(rc);
+      if ((rc = alloc((void**)&p->fin, (size_t)f32_numel * 4, true))) return fail(rc);
     }
     if (!tails.empty()) {
       const int64_t T = p->cg.t32_width;
@@ -729,7 +991,8 @@ const std::vector<fa_xfer>& schedule(fa_round_plan* p, int root, bool weighted) 
   Sched S;
   if (p->mode == FA_MODE_SHARDED) sched_sharded(p->g, p->range, p->xchg, root, weighted, &S);
   else if (p->mode == FA_MODE_STRIPED) sched_striped(p->g, p->lo, root, &S);
-  else sched_chained(p->g, p->cg, root, &S);
+  else if (p->mode == FA_MODE_CHAINED) sched_chained(p->g, p->cg, root, &S);
+  else sched_blocked(p->g, p->cg, p->bg, root, &S);
   return p->sched[key] = S.ops;
 }
 
@@ -761,6 +1024,12 @@ void* addr(Local& L, int buf, int index, int64_t off) {
     case FA_B_STACK: return index == 1 ? (void*)(p->i64_stack + off) : (void*)(p->t32_stack + off);
     case FA_B_GATHER:
       return index == 1 ? (void*)(p->i64_gather + off) : (void*)(p->t32_gather + off);
+    case FA_B_PIN: return p->pin + (size_t)index * p->plane + off;
+    case FA_B_TAILP: return p->tailp + (size_t)index * p->plane + off;
+    case FA_B_CONT: return p->cont + (size_t)index * p->plane + off;
+    case FA_B_BSUM: return p->bsum + (size_t)index * p->plane + off;
+    case FA_B_BLK: return p->blk + (size_t)index * p->bg.row + (off - p->bg.slo[p->g.rank]);
+    case FA_B_RELAY: return p->relay + (size_t)index * p->bg.row + (off - p->bg.slo[p->g.rank]);
     default: return nullptr;
   }
 }
@@ -770,7 +1039,9 @@ bool on_comm_stream(const fa_xfer& x) {
   switch (x.op) {
     case FA_X_K_SUM:
     case FA_X_K_ZERO:
-    case FA_X_K_STACK: return false;                 // read local inputs only
+    case FA_X_K_STACK:
+    case FA_X_K_PART:                                // (the zero planes of PIN only)
+    case FA_X_K_BLOCK: return false;                 // read local inputs only
     case FA_X_K_CHAIN: return x.src == FA_B_STATE;   // after the state's hop
     default: return true;                            // read exchanged data
   }
@@ -902,6 +1173,44 @@ int issue_local(Local& L, const fa_xfer& x, hipStream_t s) {
                            dim3(256), 0, s, p->t32_out, p->tidx, io->out32, T);
         FA_HIP_TRY(hipGetLastError());
       }
+      return FA_OK;
+    }
+    case FA_X_K_PART:
+    case FA_X_K_CONT: {
+      const int j = x.row0 - g.lo_slot;  // first local client of the rows
+      fa_chain ch;
+      ch.row0 = x.row0;
+      ch.n_total = g.n_total;
+      ch.state_in = p->pin;
+      ch.plane = p->plane;
+      const bool finishes = x.row0 + x.nrows == g.n_total;
+      ch.state_out = x.op == FA_X_K_PART ? p->tailp : (finishes ? nullptr : p->cont);
+      float* out = ch.state_out ? nullptr : p->cont;  // a finishing continuation: plane 0
+      return fa_reduce_chain(p->chunk[0], io->c32 + j, x.nrows, io->weights ? io->weights + j
+                                                                            : nullptr,
+                             &ch, out, FA_F_SUM_ONLY, s);
+    }
+    case FA_X_K_BLOCK: {
+      const int j = x.row0 - g.lo_slot;
+      return fa_reduce(p->chunk[0], io->c32 + j, nullptr, x.nrows,
+                       io->weights ? io->weights + j : nullptr,
+                       p->bsum + (size_t)x.dst_index * p->plane, nullptr, FA_F_SUM_ONLY, s);
+    }
+    case FA_X_K_FOLD: {
+      const BlockGeo& bg = p->bg;
+      FoldArgs f;
+      f.blk = p->blk;
+      f.row = bg.row;
+      f.count = x.count;
+      f.out = (x.dst == FA_B_OUT ? io->out32 : p->fin) + x.offset;
+      f.nblk = bg.K;
+      f.has_rem = bg.P > bg.K;
+      f.lp = bg.lp;
+      f.n_total = g.n_total;
+      f.divide = io->weights == nullptr;
+      const unsigned grid = (unsigned)std::min<int64_t>(2048, (x.count + 255) / 256);
+      hipLaunchKernelGGL(fold_kernel, dim3(std::max(1u, grid)), dim3(256), 0, s, f);
+      FA_HIP_TRY(hipGetLastError());
       return FA_OK;
     }
     default: return set_err(FA_E_INVAL, "schedule: op %d is not local", x.op);
@@ -1205,6 +1514,25 @@ int fa_reduce_chained(fa_chain_plan* const* plans, int nlocal, const fa_shard_io
                    "fa_reduce_chained");
 }
 
+// =========================================================== blocked ======
+int fa_block_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
+                         const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
+                         unsigned flags, fa_block_plan** out) {
+  return make_round(comm, FA_MODE_BLOCKED, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel,
+                    counts, 1, FA_XCHG_REDUCE, flags, "fa_block_plan_create",
+                    (fa_round_plan**)out);
+}
+
+int fa_block_plan_destroy(fa_block_plan* p) {
+  free_round((fa_round_plan*)p);
+  return FA_OK;
+}
+
+int fa_reduce_blocked(fa_block_plan* const* plans, int nlocal, const fa_shard_io* io, int root) {
+  return run_round((fa_round_plan* const*)plans, nlocal, io, root, FA_MODE_BLOCKED,
+                   "fa_reduce_blocked");
+}
+
 // ====================================================== host-only view =====
 int fa_describe_round(int mode, int nranks, int rank, const int* counts, const fa_seg* seg32,
                       int nseg32, int64_t f32_numel, const fa_seg* seg64, int nseg64,
@@ -1212,7 +1540,8 @@ int fa_describe_round(int mode, int nranks, int rank, const int* counts, const f
                       int weighted, fa_xfer* ops, int cap, int* nops) {
   if (!nops) return set_err(FA_E_INVAL, "fa_describe_round: nops is NULL");
   *nops = 0;
-  if (mode != FA_MODE_SHARDED && mode != FA_MODE_STRIPED && mode != FA_MODE_CHAINED)
+  if (mode != FA_MODE_SHARDED && mode != FA_MODE_STRIPED && mode != FA_MODE_CHAINED &&
+      mode != FA_MODE_BLOCKED)
     return set_err(FA_E_INVAL, "fa_describe_round: mode %d", mode);
   if (nchunks == 0) nchunks = 8;
   if (nchunks < 1 || nchunks > FA_COMM_MAX_CHUNKS)
@@ -1229,7 +1558,7 @@ int fa_describe_round(int mode, int nranks, int rank, const int* counts, const f
   std::vector<fa_tile_desc> vec, tails;
   std::vector<size_t> cut;
   std::vector<int64_t> tidx;
-  build_round(&p, nchunks, &vec, &cut, &tails, &tidx);
+  if ((rc = build_round(&p, nchunks, &vec, &cut, &tails, &tidx))) return rc;
   const std::vector<fa_xfer>& s = schedule(&p, root, weighted != 0);
   *nops = (int)s.size();
   if (ops) {

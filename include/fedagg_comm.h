@@ -167,6 +167,31 @@ int fa_chain_plan_destroy(fa_chain_plan *plan);
 int fa_reduce_chained(fa_chain_plan *const *plans, int nlocal,
                       const fa_shard_io *io, int root);
 
+/* ---- blocked mode: client shards, exact order, block sums to stripe owners -
+ * torch's cascade sums the slots in blocks of 16 (level 0) and folds the
+ * block sums in order (levels 1-3).  A block sum depends only on its own 16
+ * rows, so every rank computes the block sums of the blocks it holds
+ * entirely, independently; a block cut by a shard boundary needs the
+ * level-0 partial of its first rank's rows (ONE plane) on the next rank,
+ * which travels split into column stripes, each through the stripe's owner
+ * (every link of a full xGMI mesh carries a share, not just r -> r+1).  The
+ * block sums (and the remainder block's partial) then go to the column
+ * stripe owners, which fold them in block order with torch's promotions
+ * (fa_reduce's own arithmetic), divide, and send the result stripes to
+ * `root` (or every rank).  Scalar columns and int64 keys as in the chained
+ * mode.  Bit-identical to one GPU's fa_reduce over all clients; requires
+ * every block's slots to lie on at most two ranks (fa_block_plan_create
+ * returns FA_E_RANGE otherwise, e.g. for fewer than ~8 slots per rank: use
+ * the chained round).  nchunks is unused (0). */
+typedef struct fa_block_plan fa_block_plan;
+int fa_block_plan_create(fa_comm *comm, const fa_seg *seg32, int nseg32,
+                         int64_t f32_numel, const fa_seg *seg64, int nseg64,
+                         int64_t i64_numel, const int *counts, unsigned flags,
+                         fa_block_plan **out);
+int fa_block_plan_destroy(fa_block_plan *plan);
+int fa_reduce_blocked(fa_block_plan *const *plans, int nlocal,
+                      const fa_shard_io *io, int root);
+
 /* ---- schedules, host-only -------------------------------------------------
  * Every round above runs a schedule: a list of operations per rank, built on
  * the host from the layout, the counts and the rank.  fa_describe_round
@@ -180,6 +205,7 @@ int fa_reduce_chained(fa_chain_plan *const *plans, int nlocal,
 #define FA_MODE_SHARDED 0
 #define FA_MODE_STRIPED 1
 #define FA_MODE_CHAINED 2
+#define FA_MODE_BLOCKED 3
 
 #define FA_X_SEND 1           /* ncclSend of src[offset, +count) to peer         */
 #define FA_X_RECV 2           /* ncclRecv into dst[offset, +count) from peer     */
@@ -197,6 +223,10 @@ int fa_reduce_chained(fa_chain_plan *const *plans, int nlocal,
 #define FA_X_K_CHAIN 21       /* fa_reduce_chain: rows row0..row0+nrows-1        */
 #define FA_X_K_STACK 22       /* local clients' scalar columns / int64 keys      */
 #define FA_X_K_TAILS 23       /* reduce the gathered rows into the result        */
+#define FA_X_K_PART 24        /* blocked: level-0 partial of rows row0.. -> TAILP  */
+#define FA_X_K_CONT 25        /* blocked: continue PIN over rows row0.. -> CONT    */
+#define FA_X_K_BLOCK 26       /* blocked: block sum of local rows -> BSUM[dst_index] */
+#define FA_X_K_FOLD 27        /* blocked: fold BLK[0..nrows) of this stripe       */
 
 #define FA_B_NONE 0
 #define FA_B_CLIENT 1         /* local client src_index's fp32 bucket            */
@@ -208,6 +238,12 @@ int fa_reduce_chained(fa_chain_plan *const *plans, int nlocal,
 #define FA_B_FIN 8            /* chained: the finisher's result (not a result rank) */
 #define FA_B_STACK 9          /* raw scalar columns, this rank's rows            */
 #define FA_B_GATHER 10        /* ... every rank's rows                           */
+#define FA_B_PIN 11           /* blocked: incoming partial (plane 0; 1-3 stay 0) */
+#define FA_B_TAILP 12         /* blocked: outgoing partial, plane `index`        */
+#define FA_B_CONT 13          /* blocked: continuation result, plane `index`     */
+#define FA_B_BSUM 14          /* blocked: local block sum `index`                */
+#define FA_B_BLK 15           /* blocked: owner's stripe of block `index`        */
+#define FA_B_RELAY 16         /* blocked: owner's relay of rank `index`'s partial */
 
 typedef struct fa_xfer {
   int32_t step;

@@ -2,19 +2,19 @@
 // libfedagg_comm (chained, striped, sharded with either e1 exchange) run with
 // W ranks on one GPU over the loopback communicator (loopccl.hip), checked
 // against one GPU's fa_reduce over all clients:
-//   chained / striped: bit-identical (fp32 and int64);
+//   chained / striped / blocked: bit-identical (fp32 and int64);
 //   sharded (e1): int64 bit-identical, fp32 within the forward error bound of
 //   two N-term sums, 2N * 2^-24 * sum_i |w_i x_i| (any summation order).
 // Usage: loop_round LAYOUT CASE...
 //   LAYOUT: "f32_numel i64_numel nseg32 nseg64" then one "offset numel" line
 //           per segment (fp32 first), as BucketLayout.segs32 / segs64.
 //   CASE:   mode:W:counts:root:model:weighted:nchunks
-//           mode   chained | striped | sharded | sharded_rs
+//           mode   chained | striped | blocked | sharded | sharded_rs
 //           counts comma-separated client slots per rank (sum = N)
 //           root   result rank, or -1 for every rank
 //           model  threads (one thread + comm per rank: fa_comm_init_rank)
 //                  | single (one thread drives all ranks: fa_comm_init; only
-//                    for schedules whose p2p pairs share a step, i.e. sharded)
+//                    for schedules whose p2p pairs share a step: sharded, blocked)
 // One JSON line per case; exit status 0 iff every case passed.
 #include <hip/hip_runtime.h>
 
@@ -109,6 +109,10 @@ int create_plan(const Case& c, const Layout& L, Rank& r) {
     return fa_stripe_plan_create(r.comm, L.s32.data(), (int)L.s32.size(), L.f32_numel, s64,
                                  (int)L.s64.size(), L.i64_numel, c.counts.data(), fl,
                                  (fa_stripe_plan**)&r.plan);
+  if (c.mode == "blocked")
+    return fa_block_plan_create(r.comm, L.s32.data(), (int)L.s32.size(), L.f32_numel, s64,
+                                (int)L.s64.size(), L.i64_numel, c.counts.data(), fl,
+                                (fa_block_plan**)&r.plan);
   return fa_shard_plan_create_ex(r.comm, L.s32.data(), (int)L.s32.size(), L.f32_numel, s64,
                                  (int)L.s64.size(), L.i64_numel, c.counts.data(), c.nchunks,
                                  c.mode == "sharded_rs" ? FA_XCHG_RS_GATHER : FA_XCHG_REDUCE, fl,
@@ -121,6 +125,8 @@ int run_round(const Case& c, std::vector<void*>& plans, std::vector<fa_shard_io>
     return fa_reduce_chained((fa_chain_plan* const*)plans.data(), nl, io.data(), c.root);
   if (c.mode == "striped")
     return fa_reduce_striped((fa_stripe_plan* const*)plans.data(), nl, io.data(), c.root);
+  if (c.mode == "blocked")
+    return fa_reduce_blocked((fa_block_plan* const*)plans.data(), nl, io.data(), c.root);
   return fa_reduce_sharded((fa_shard_plan* const*)plans.data(), nl, io.data(), c.root);
 }
 
@@ -128,6 +134,7 @@ void destroy_plan(const Case& c, void* p) {
   if (!p) return;
   if (c.mode == "chained") fa_chain_plan_destroy((fa_chain_plan*)p);
   else if (c.mode == "striped") fa_stripe_plan_destroy((fa_stripe_plan*)p);
+  else if (c.mode == "blocked") fa_block_plan_destroy((fa_block_plan*)p);
   else fa_shard_plan_destroy((fa_shard_plan*)p);
 }
 
@@ -275,7 +282,7 @@ bool run_case(const Case& c, const Layout& L) {
   std::vector<int64_t> ref_i(I), got_i(I);
   HIPC(hipMemcpy(ref.data(), ref32, F * 4, hipMemcpyDeviceToHost));
   HIPC(hipMemcpy(ref_i.data(), ref64, I * 8, hipMemcpyDeviceToHost));
-  const bool exact = c.mode == "chained" || c.mode == "striped";
+  const bool exact = c.mode == "chained" || c.mode == "striped" || c.mode == "blocked";
   std::vector<double> bound;
   if (!exact && !failed) {
     // forward error bound: 2N * 2^-24 * sum |w_i x_i| (/N for the mean)

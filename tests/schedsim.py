@@ -82,7 +82,14 @@ class Sim:
                  "STACK": [np.full(self.nmax * self.trow, np.nan, F32),
                            np.zeros(self.nmax * max(1, layout.i64_numel), np.int64)],
                  "GATHER": [np.full(self.W * self.nmax * self.trow, np.nan, F32),
-                            np.zeros(self.W * self.nmax * max(1, layout.i64_numel), np.int64)]}
+                            np.zeros(self.W * self.nmax * max(1, layout.i64_numel), np.int64)],
+                 # blocked mode (bucket offsets everywhere, stripes included)
+                 "PIN": [np.zeros(N32, F32) for _ in range(4)],
+                 "TAILP": [np.full(N32, np.nan, F32) for _ in range(4)],
+                 "CONT": [np.full(N32, np.nan, F32) for _ in range(4)],
+                 "BSUM": defaultdict(lambda: np.full(N32, np.nan, F32)),
+                 "BLK": defaultdict(lambda: np.full(N32, np.nan, F32)),
+                 "RELAY": defaultdict(lambda: np.full(N32, np.nan, F32))}
             self.buf.append(b)
 
     # ------------------------------------------------------------ buffers --
@@ -94,8 +101,8 @@ class Sim:
             return b[name][off:off + cnt]
         if name == "RECV":
             return b["RECV"][index][off:off + cnt]
-        if name == "STATE":
-            return b["STATE"][index][off:off + cnt]
+        if name in ("STATE", "PIN", "TAILP", "CONT", "BSUM", "BLK", "RELAY"):
+            return b[name][index][off:off + cnt]
         if name in ("STACK", "GATHER"):
             return b[name][index][off:off + cnt]
         raise KeyError(name)
@@ -162,6 +169,52 @@ class Sim:
                     s = O.cascade_finish(acc)
                     res = s if wt is not None else (s / F32(self.n)).astype(F32)
                     b[x["dst"]][st:st + cnt] = res
+        elif op in ("K_PART", "K_CONT"):
+            # fa_reduce_chain: PIN (plane 0 = the incoming partial, 1-3 zero) in
+            row0, nr = x["row0"], x["nrows"]
+            lin = O.chain_levels(row0, self.n)
+            lout = O.chain_levels(row0 + nr, self.n)
+            finishes = row0 + nr == self.n
+            assert op == "K_CONT" or not finishes
+            for st, cnt, kind in self.t32[self.t32[:, 2] == 0]:
+                acc = [b["PIN"][l][st:st + cnt].copy() if lin & (1 << l) else np.zeros(cnt, F32)
+                       for l in range(4)]
+                acc = O.cascade_state([val(s, st, cnt) for s in range(row0, row0 + nr)], row0,
+                                      self.n, acc)
+                if finishes:   # sum only, into CONT plane 0
+                    b["CONT"][0][st:st + cnt] = O.cascade_finish(acc)
+                else:
+                    dst = b["TAILP" if op == "K_PART" else "CONT"]
+                    for l in range(4):
+                        if lout & (1 << l):
+                            dst[l][st:st + cnt] = acc[l]
+        elif op == "K_BLOCK":
+            row0, nr = x["row0"], x["nrows"]
+            for st, cnt, kind in self.t32[self.t32[:, 2] == 0]:
+                b["BSUM"][x["dst_index"]][st:st + cnt] = O.cascade(
+                    [val(s, st, cnt) for s in range(row0, row0 + nr)])
+        elif op == "K_FOLD":
+            off, cnt, P = x["offset"], x["count"], x["nrows"]
+            lp = O.level_power(self.n)
+            Q, mask = 1 << lp, (1 << lp) - 1
+            K = self.n // Q
+            l1 = np.zeros(cnt, F32)
+            l2 = np.zeros(cnt, F32)
+            l3 = np.zeros(cnt, F32)
+            for k in range(K):
+                l1 = (l1 + b["BLK"][k][off:off + cnt]).astype(F32)
+                i = (k + 1) << lp
+                if i & (mask << lp):
+                    continue
+                l2, l1 = (l2 + l1).astype(F32), np.zeros(cnt, F32)
+                if i & (mask << (2 * lp)):
+                    continue
+                l3, l2 = (l3 + l2).astype(F32), np.zeros(cnt, F32)
+            l0 = b["BLK"][K][off:off + cnt] if P > K else np.zeros(cnt, F32)
+            res = (((l0 + l1).astype(F32) + l2).astype(F32) + l3).astype(F32)
+            if wt is None:
+                res = (res / F32(self.n)).astype(F32)
+            b[x["dst"]][off:off + cnt] = res
         elif op == "K_STACK":
             for j, s in enumerate(slots):
                 if len(self.tidx):

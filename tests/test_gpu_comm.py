@@ -253,6 +253,35 @@ def test_native_chained_weighted(comm):
     assert torch.equal(out64, want64)
 
 
+@pytest.mark.parametrize("lay", ["wrn16_8_c10", "wrnsl16_8_sf4_c10_proxy"])
+@pytest.mark.parametrize("final", ["reduce", "allreduce"])
+@pytest.mark.parametrize("n,weighted", [(20, False), (5, False), (300, False), (33, True)])
+def test_native_blocked_one_rank_is_bit_exact(comm, lay, final, n, weighted):
+    """fa_reduce_blocked on a real RCCL communicator with one rank: every
+    block is local (fa_reduce per 16 slots), the rank owns the one stripe and
+    folds the block sums with the cascade's promotions (n=300: level 2) —
+    the single-GPU reduction bit for bit.  Multi-rank: tests/test_schedule.py
+    (CPU replay) and tests/test_gpu_loopback.py (2..8 ranks on this GPU)."""
+    from feddct_amd.comm import NativeBlockedAggregator
+    man = load_manifest(lay)
+    layout = BucketLayout.from_manifest(man)
+    clients = make_clients(layout, man, range(n), DEV, mode=synth.MODE_ADVERSARIAL)
+    w = [float(np.float32(k / (n * (n + 1) / 2))) for k in range(1, n + 1)] if weighted else None
+    want32, want64 = _single_gpu(layout, clients, weights=w)
+    out32 = torch.full_like(clients[0][0], float("nan"))
+    out64 = torch.full_like(clients[0][1], -7)
+    agg = NativeBlockedAggregator(layout, [c[0] for c in clients], [c[1] for c in clients], n,
+                                  out32, out64, comm, final=final, weights=w)
+    for _ in range(2):
+        agg.step()
+    torch.cuda.synchronize()
+    mask = _layout_pad_mask(layout)
+    nan = torch.isnan(want32[mask])
+    assert torch.equal(torch.isnan(out32[mask]), nan)
+    assert torch.equal(out32[mask].view(torch.int32)[~nan], want32[mask].view(torch.int32)[~nan])
+    assert torch.equal(out64, want64)
+
+
 @pytest.mark.parametrize("final", ["reduce", "allreduce"])
 def test_native_rs_gather_exchange_one_rank(comm, final):
     """e1 with the reduce-scatter + gather exchange (FA_XCHG_RS_GATHER): one

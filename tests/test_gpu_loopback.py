@@ -4,13 +4,13 @@ the RCCL calls it makes (tests/loopback/loopccl.hip; RCCL itself refuses two
 ranks on one device).  The C++ driver (tests/loopback/loop_round.cpp) builds
 the clients with the portable synthetic state, runs one round per case and
 compares every result rank with one GPU's fa_reduce over all clients:
-chained and striped bit for bit, sharded (e1) within the forward error bound
+chained, striped and blocked bit for bit, sharded (e1) within the forward error bound
 of two N-term sums; int64 keys bit for bit everywhere.
 
 Both process models of fedcomm run: one thread + communicator per rank
 (fa_comm_init_rank — the product's one-process-per-GPU model, ranks progress
 independently) for every mode, and one thread driving every rank
-(fa_comm_init) for the sharded rounds.  The chained and striped schedules
+(fa_comm_init) for the sharded and blocked rounds.  The chained and striped schedules
 pair a send in one step with its receive in a later step of another rank;
 RCCL matches those on the device, a host-side loopback driven by one thread
 cannot (the receive would wait for a send the same thread has not issued),
@@ -95,6 +95,14 @@ def test_loopback_small_layout_all_modes(tmp_path):
         "sharded_rs:4:5,1,2,1:-1:threads:1:4",
         "sharded_rs:8:1,2,1,3,1,1,2,9:7:threads:0:13",
         "sharded_rs:3:4,5,3:-1:single:0:2",
+        "blocked:1:20:0:threads:0:0",
+        "blocked:2:10,10:1:threads:0:0",
+        "blocked:3:7,0,13:-1:threads:1:0",
+        "blocked:3:16,16,1:0:single:0:0",
+        "blocked:8:20,20,20,20,20,20,20,20:0:threads:0:0",
+        "blocked:8:20,20,20,20,20,20,20,20:-1:single:1:0",
+        "blocked:6:12,9,30,0,14,8:4:threads:0:0",
+        "blocked:3:100,156,44:-1:threads:0:0",            # N=300: the fold's level 2
     ]
     _run(_small_layout(), cases, tmp_path)
 
@@ -110,6 +118,8 @@ def test_loopback_cfg3_layout(cfg3_layout, tmp_path):
         "striped:4:2,1,1,1:-1:threads:0:0",
         "sharded:2:3,2:0:threads:0:8",
         "sharded_rs:4:2,1,1,1:-1:threads:1:8",
+        "blocked:2:3,2:0:threads:0:0",
+        "blocked:2:20,20:-1:threads:1:0",
     ]
     _run(cfg3_layout, cases, tmp_path)
 
@@ -121,4 +131,15 @@ def test_loopback_cfg5_sharded_chain(tmp_path):
     lay = BucketLayout.from_manifest(joint_manifest([mm, pm]))
     cases = ["chained:8:3,3,3,3,3,3,3,3:7:threads:0:8",
              "chained:8:3,3,3,3,3,3,3,3:-1:threads:0:8"]
+    _run(lay, cases, tmp_path, timeout=300)
+
+
+def test_loopback_blocked_bench_shape(tmp_path):
+    """The bench's N>1 shape: 20 wrn16_8 clients per rank, 4 and 8 ranks
+    (160 slots: 10 blocks, six of them cut by a shard boundary), the
+    result on rank 0 and on every rank."""
+    lay = BucketLayout.from_manifest(load_manifest("wrn16_8_c10"))
+    cases = ["blocked:4:20,20,20,20:0:threads:0:0",
+             "blocked:8:20,20,20,20,20,20,20,20:0:threads:0:0",
+             "blocked:8:20,20,20,20,20,20,20,20:-1:threads:0:0"]
     _run(lay, cases, tmp_path, timeout=300)

@@ -235,3 +235,66 @@ def test_deadlock_is_detected():
              "row0": 0, "nrows": 0}] for r in range(2)]
     with pytest.raises(Deadlock):
         Sim(layout, tiles, counts, c32, c64).run(bad)
+
+
+BLOCK_COUNTS = [[20], [10, 10], [7, 0, 13], [16, 16, 1], [20, 20, 20], [20] * 8,
+                [12, 9, 30, 0, 14, 8], [100, 156, 44]]
+
+
+@pytest.mark.parametrize("counts", BLOCK_COUNTS)
+@pytest.mark.parametrize("root", [0, -1, "last", 1])
+def test_blocked_schedule_is_exact(counts, root):
+    """Block sums where they lie, spanning partials relayed through the
+    stripe owners, the owners' folds: the single-process reference's bits
+    (incl. n_total >= 256: the fold's level-2 promotion)."""
+    W = len(counts)
+    root = W - 1 if root == "last" else root
+    if root >= W:
+        pytest.skip("root beyond the world")
+    layout, states, _, bufs, _ = _run(C.FA_MODE_BLOCKED, counts, root)
+    want = _expected(states, None)
+    for r in _result_ranks(W, root):
+        for s in layout.slots:
+            src = bufs[r]["OUT64"] if s.kind == "i64" else bufs[r]["OUT"]
+            got = src[s.offset:s.offset + s.numel].reshape(s.shape)
+            assert got.tobytes() == np.asarray(want[s.key]).tobytes(), (r, s.key)
+
+
+@pytest.mark.parametrize("counts", [[10, 10], [20] * 8, [12, 9, 30, 0, 14, 8], [100, 156, 44]])
+def test_blocked_schedule_weighted_is_exact(counts):
+    layout, states, w, bufs, _ = _run(C.FA_MODE_BLOCKED, counts, -1, weighted=True)
+    want = _expected(states, w)
+    for r in range(len(counts)):
+        for s in layout.slots:
+            src = bufs[r]["OUT64"] if s.kind == "i64" else bufs[r]["OUT"]
+            got = src[s.offset:s.offset + s.numel].reshape(s.shape)
+            assert got.tobytes() == np.asarray(want[s.key]).tobytes(), (r, s.key)
+
+
+@pytest.mark.parametrize("counts", [[4, 9, 0, 2, 5], [1, 1, 1, 17], [3] * 8])
+def test_blocked_refuses_blocks_over_three_ranks(counts):
+    from feddct_amd._lib import FedaggError
+    layout = BucketLayout.from_manifest(MAN)
+    with pytest.raises(FedaggError, match="more than two"):
+        C.describe(C.FA_MODE_BLOCKED, layout, counts, 0, root=0)
+
+
+def test_blocked_relays_spread_over_owners():
+    """W=8, 20 slots per rank: every spanning partial leaves its starter in
+    W-1 pieces (2 direct to the holder, W-3 through the other owners), and no
+    rank sends more than one piece to any peer per step."""
+    layout = BucketLayout.from_manifest(MAN)
+    W = 8
+    counts = [20] * W
+    for r in range(W):
+        ops = C.describe(C.FA_MODE_BLOCKED, layout, counts, r, root=0)
+        parts = [x for x in ops if x["op"] == "SEND" and x["src"] == "TAILP"]
+        if parts:
+            peers = [x["peer"] for x in parts]
+            assert sorted(set(peers)) == sorted(set(range(W)) - {r}), peers
+        by_step = {}
+        for x in ops:
+            if x["op"] == "SEND" and x["src"] in ("TAILP", "RELAY"):
+                key = (x["step"], x["peer"], x["src"])
+                by_step[key] = by_step.get(key, 0) + 1
+        assert all(v <= 2 for v in by_step.values())
