@@ -1050,7 +1050,7 @@ def main():
             wo32, wo64 = torch.zeros_like(out32), torch.zeros_like(out64)
             wred = Reducer(layout, clients, wo32, wo64, weights=w, plan=reducer.plan)
             wper = []
-            tw, _ = timed_launches(wred, max(10, args.steps // 2), 3)
+            tw, _ = timed_launches(wred, max(10, args.steps // 2), args.warmup)
             extra["weighted_GBps"] = round(nbytes_rank / tw / 1e9, 1)
             extra["weighted_us"] = round(tw * 1e6, 2)
             timed_launches(wred, max(10, args.steps // 2), 0, per_launch=wper)

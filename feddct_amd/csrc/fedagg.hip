@@ -1111,7 +1111,10 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   if (pflags & FA_PLAN_TUNE_ST_PLAIN) nt &= ~2;
   if (pflags & FA_PLAN_TUNE_LD_PLAIN) nt &= ~1;
   if (pflags & FA_PLAN_TUNE_ST_SC1) nt |= 4;
-  const bool small = w || a.n < 16;
+  // weighted reductions take the mean's 16-client batches too since the
+  // batch's weights are read once up front (r02 sweep, same box: weighted
+  // U2xB16 140.5 us vs U2xB8 143.3 us, unweighted 143.0 us)
+  const bool small = a.n < 16;
   const int b_env = (pflags & FA_PLAN_TUNE_BATCH1)    ? 1
                     : (pflags & FA_PLAN_TUNE_BATCH4)  ? 4
                     : (pflags & FA_PLAN_TUNE_BATCH8)  ? 8
