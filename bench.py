@@ -134,19 +134,30 @@ def ulp_hist(a: torch.Tensor, b: torch.Tensor) -> dict:
 
 
 def pmc_traffic(n_gpus):
-    """HBM bytes per launch of the reduce kernel from the committed rocprofv3
-    PMC summary (profiles/*pmc*.json written by tools/pmc_summary.py)."""
+    """HBM bytes per launch of the reduce kernel, with where they come from.
+    PMC counters cannot be read from inside the timed process (rocprofv3
+    --pmc is its own run), so this is the committed summary of separate
+    FETCH_SIZE / WRITE_SIZE passes over THIS bench command's reduce launches
+    (tools/gpu_profile.sh -> profiles/reduce_pmc.json, gfx950 FETCH_SIZE x2
+    correction applied) — returned with its source and that run's average
+    launch time, so the line shows what the counters were taken on."""
     path = os.path.join(ROOT, "profiles", "reduce_pmc.json")
     if n_gpus != 1 or not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get("workload") == f"{LAYOUT}/n{N_CLIENTS}":
-            return d.get("hbm_bytes_per_launch")
+            return d.get("hbm_bytes_per_launch"), {
+                "source": "profiles/reduce_pmc.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                          "passes (separate runs) of bench.py --kernel-only",
+                "profile_kernel_avg_us": round(d["avg_ns"] / 1e3, 2) if "avg_ns" in d else None,
+                "traffic_over_algorithmic": round(d["hbm_bytes_per_launch"]
+                                                  / d["algorithmic_bytes_per_launch"], 4)
+                if d.get("algorithmic_bytes_per_launch") else None}
     except Exception:
         pass
-    return None
+    return None, None
 
 
 def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
@@ -1103,7 +1114,7 @@ def main():
                                             clients, out32, out64, reducer, nbytes_rank, extra)
 
     achieved = nbytes_rank / t_kernel / 1e9
-    traffic = pmc_traffic(world)
+    traffic, traffic_src = pmc_traffic(world)
     line = {
         "metric": METRIC,
         "value": round(nbytes_rank * world / t_step / 1e9, 2),
@@ -1126,7 +1137,8 @@ def main():
                                    if world > 1 else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel_us": round(t_kernel * 1e6, 2)},
+                     "traffic": traffic, "traffic_pmc": traffic_src,
+                     "kernel_us": round(t_kernel * 1e6, 2)},
         "cpu_baseline": None,
     }
     line.update(extra)
