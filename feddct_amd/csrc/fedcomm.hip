@@ -502,7 +502,7 @@ void sched_blocked(const Geo& g, const ChainGeo& cg, const BlockGeo& bg, int roo
   const bool result = root < 0 || root == me;
   const bool i64 = !g.t64.empty();
   auto w_of = [&](int s) { return bg.shi[s] - bg.slo[s]; };
-  // step 0: local work, the partial a neighbour waits for first
+  // step 0: the partial a neighbour waits for, alone
   if ((i64 || cg.t32_width) && g.n_local > 0)
     S->add(FA_X_K_STACK, -1, FA_B_CLIENT, -1, FA_B_STACK, -1, 0, 0, -1, g.lo_slot, g.n_local);
   if (bg.tail_piece >= 0) {
@@ -510,10 +510,6 @@ void sched_blocked(const Geo& g, const ChainGeo& cg, const BlockGeo& bg, int roo
     S->add(FA_X_K_PART, -1, FA_B_PIN, -1, FA_B_TAILP, 0, 0, 0, -1, bg.s0[i],
            g.lo_slot + g.n_local - bg.s0[i]);
   }
-  for (int i = 0; i < bg.P; ++i)
-    if (bg.bsum_slot[i] >= 0)
-      S->add(FA_X_K_BLOCK, -1, FA_B_CLIENT, -1, FA_B_BSUM, bg.bsum_slot[i], 0, 0, i, bg.s0[i],
-             bg.s1[i] - bg.s0[i]);
   S->next();
   // step 1: raw columns gathered; each spanning partial split into stripes,
   // to its holder directly (the starter's and the holder's own stripes) or
@@ -535,6 +531,13 @@ void sched_blocked(const Geo& g, const ChainGeo& cg, const BlockGeo& bg, int roo
       if (!direct && me == s) S->add(FA_X_RECV, r1, FA_B_NONE, -1, FA_B_RELAY, r1, off, w);
     }
   }
+  // the local block sums on the compute stream, behind the partial's
+  // scatter and overlapping it and the forwarding step (which reads only
+  // relayed data)
+  for (int i = 0; i < bg.P; ++i)
+    if (bg.bsum_slot[i] >= 0)
+      S->add(FA_X_K_BLOCK, -1, FA_B_CLIENT, -1, FA_B_BSUM, bg.bsum_slot[i], 0, 0, i, bg.s0[i],
+             bg.s1[i] - bg.s0[i]);
   S->next();
   // step 2: the owners forward their stripes of the partials
   for (int i = 0; i < bg.P; ++i) {
@@ -1047,6 +1050,20 @@ bool on_comm_stream(const fa_xfer& x) {
   }
 }
 
+// Buffers that kernels on the caller's (compute) stream write: partial sums,
+// stacked raw columns, the blocked mode's outgoing partial and local block
+// sums, and the state / result of a chain segment without a predecessor.
+// An exchange or a comm-stream kernel that reads one of them waits for the
+// compute stream first; the others (partials in transit, received planes,
+// owners' block stripes, gathered rows, client buckets) need not, so they
+// overlap the local kernels.  No exchange writes a buffer a compute-stream
+// kernel reads or writes (received planes and stripes are comm-side only).
+bool user_written(int b) {
+  return b == FA_B_PARTIAL || b == FA_B_STACK || b == FA_B_TAILP || b == FA_B_BSUM ||
+         b == FA_B_STATE || b == FA_B_OUT || b == FA_B_FIN;
+}
+bool needs_compute(const fa_xfer& x) { return user_written(x.src); }
+
 int issue_comm(Local& L, const fa_xfer& x) {
   fa_comm* c = L.p->comm;
   const int64_t n = x.count;
@@ -1233,20 +1250,25 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
   int step = 0;
   for (;;) {
     bool any = false, comm = false;
+    std::vector<char> join(nl, 0);
     for (size_t d = 0; d < nl; ++d) {
       const std::vector<fa_xfer>& o = *scheds[d];
       for (size_t i = pos[d]; i < o.size() && o[i].step == step; ++i) {
         any = true;
-        comm |= is_comm(o[i].op);
+        if (is_comm(o[i].op)) {
+          comm = true;
+          join[d] |= needs_compute(o[i]);
+        }
       }
       if (pos[d] < o.size()) any = true;
     }
     if (!any) break;
-    // comm stream joins the compute stream before this step's exchanges
+    // comm stream joins the compute stream before this step's exchanges when
+    // one of them reads compute-stream output
     if (comm) {
       for (size_t d = 0; d < nl; ++d) {
         Local& L = locals[d];
-        if (!L.comp_dirty) continue;
+        if (!L.comp_dirty || !join[d]) continue;
         FA_HIP_TRY(hipSetDevice(L.p->comm->device));
         FA_HIP_TRY(hipEventRecord(L.p->ev[1], L.user));
         FA_HIP_TRY(hipStreamWaitEvent(L.p->comm->cs, L.p->ev[1], 0));
@@ -1275,7 +1297,7 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
         const fa_xfer& x = o[pos[d]];
         if (is_comm(x.op)) continue;
         const bool cs = on_comm_stream(x);
-        if (cs && L.comp_dirty) {
+        if (cs && L.comp_dirty && needs_compute(x)) {
           FA_HIP_TRY(hipEventRecord(L.p->ev[1], L.user));
           FA_HIP_TRY(hipStreamWaitEvent(L.p->comm->cs, L.p->ev[1], 0));
           L.comp_dirty = false;
