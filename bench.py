@@ -1052,7 +1052,7 @@ def main():
             def copy_big():
                 _lib.check(_lib.lib.fa_copy_f32(big.data_ptr(), big2.data_ptr(), big.numel(),
                                                 torch.cuda.current_stream().cuda_stream))
-            tc, _ = timed_launches(copy_big, 20, 3)
+            tc, _ = timed_launches(copy_big, 100, 3)   # ~33 ms of streaming
             extra["copy_ceiling_GBps"] = round(2 * big.numel() * 4 / tc / 1e9, 1)
             del big, big2
             # weighted variant (client-size weights, BASELINE config 4's extension)
@@ -1061,10 +1061,10 @@ def main():
             wo32, wo64 = torch.zeros_like(out32), torch.zeros_like(out64)
             wred = Reducer(layout, clients, wo32, wo64, weights=w, plan=reducer.plan)
             wper = []
-            tw, _ = timed_launches(wred, max(10, args.steps // 2), args.warmup)
+            tw, _ = timed_launches(wred, max(100, args.steps // 2), max(20, args.warmup))
             extra["weighted_GBps"] = round(nbytes_rank / tw / 1e9, 1)
             extra["weighted_us"] = round(tw * 1e6, 2)
-            timed_launches(wred, max(10, args.steps // 2), 0, per_launch=wper)
+            timed_launches(wred, max(100, args.steps // 2), 0, per_launch=wper)
             extra["weighted_launch"] = launch_stats(wper)
             extra["weighted_parity"] = weighted_digest_check("wrn16_8_c10/n20/sizes_1_20",
                                                              layout, wo32, wo64)
