@@ -502,10 +502,11 @@ void sched_blocked(const Geo& g, const ChainGeo& cg, const BlockGeo& bg, int roo
   const bool result = root < 0 || root == me;
   const bool i64 = !g.t64.empty();
   auto w_of = [&](int s) { return bg.shi[s] - bg.slo[s]; };
+  const bool vec = !cg.range.empty();  // a layout of scalar columns only has no blocks
   // step 0: the partial a neighbour waits for, alone
   if ((i64 || cg.t32_width) && g.n_local > 0)
     S->add(FA_X_K_STACK, -1, FA_B_CLIENT, -1, FA_B_STACK, -1, 0, 0, -1, g.lo_slot, g.n_local);
-  if (bg.tail_piece >= 0) {
+  if (vec && bg.tail_piece >= 0) {
     const int i = bg.tail_piece;
     S->add(FA_X_K_PART, -1, FA_B_PIN, -1, FA_B_TAILP, 0, 0, 0, -1, bg.s0[i],
            g.lo_slot + g.n_local - bg.s0[i]);
@@ -534,7 +535,7 @@ void sched_blocked(const Geo& g, const ChainGeo& cg, const BlockGeo& bg, int roo
   // the local block sums on the compute stream, behind the partial's
   // scatter and overlapping it and the forwarding step (which reads only
   // relayed data)
-  for (int i = 0; i < bg.P; ++i)
+  for (int i = 0; i < bg.P && vec; ++i)
     if (bg.bsum_slot[i] >= 0)
       S->add(FA_X_K_BLOCK, -1, FA_B_CLIENT, -1, FA_B_BSUM, bg.bsum_slot[i], 0, 0, i, bg.s0[i],
              bg.s1[i] - bg.s0[i]);
@@ -552,7 +553,7 @@ void sched_blocked(const Geo& g, const ChainGeo& cg, const BlockGeo& bg, int roo
   }
   S->next();
   // step 3: the holder finishes the spanning block (or the remainder)
-  if (bg.head_piece >= 0) {
+  if (vec && bg.head_piece >= 0) {
     const int i = bg.head_piece;
     S->add(FA_X_K_CONT, -1, FA_B_PIN, -1, FA_B_CONT, bg.plane[i], 0, 0, i, g.lo_slot,
            bg.s1[i] - g.lo_slot);
@@ -575,7 +576,7 @@ void sched_blocked(const Geo& g, const ChainGeo& cg, const BlockGeo& bg, int roo
   S->next();
   // step 5: own pieces into the stripe, then the fold
   const int64_t wme = w_of(me);
-  if (wme > 0) {
+  if (vec && wme > 0) {
     for (int i = 0; i < bg.P; ++i) {
       if (bg.holder[i] != me) continue;
       if (bg.bsum_slot[i] >= 0)

@@ -298,3 +298,26 @@ def test_blocked_relays_spread_over_owners():
                 key = (x["step"], x["peer"], x["src"])
                 by_step[key] = by_step.get(key, 0) + 1
         assert all(v <= 2 for v in by_step.values())
+
+
+def test_blocked_and_chained_scalar_only_layout():
+    """A layout with no vector columns (0-d keys, 3-element tensors, int64):
+    no blocks to sum, only the raw stacked columns — still exact."""
+    man = {"keys": [{"key": "a", "shape": [], "dtype": "float32"},
+                    {"key": "b", "shape": [3], "dtype": "float32"},
+                    {"key": "n", "shape": [], "dtype": "int64"}]}
+    layout = BucketLayout.from_manifest(man)
+    for mode in (C.FA_MODE_BLOCKED, C.FA_MODE_CHAINED):
+        counts = [10, 10, 5]
+        n = sum(counts)
+        states = [synth.gen_state(man, c, synth.MODE_ADVERSARIAL) for c in range(n)]
+        c32, c64 = _buckets(layout, states)
+        _, tiles = layout_tiles(layout)
+        scheds = [C.describe(mode, layout, counts, r, root=-1) for r in range(3)]
+        bufs = Sim(layout, tiles, counts, c32, c64, None, -1).run(scheds)
+        want = _expected(states, None)
+        for r in range(3):
+            for s in layout.slots:
+                src = bufs[r]["OUT64"] if s.kind == "i64" else bufs[r]["OUT"]
+                got = src[s.offset:s.offset + s.numel].reshape(s.shape)
+                assert got.tobytes() == np.asarray(want[s.key]).tobytes(), (mode, r, s.key)
