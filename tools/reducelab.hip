@@ -77,6 +77,31 @@ __global__ __launch_bounds__(256) void nsum(Ptrs p, float* out, int64_t nv, int 
   }
 }
 
+// G consecutive tiles per workgroup (U=1: 1024 floats each); each tile's
+// result parked in LDS, the G results stored back to back after the last
+// tile's reads (writes clustered in time, reads unchanged).
+template <int N, int G>
+__global__ __launch_bounds__(256) void nsum_park(Ptrs p, float* out, int64_t nv, int ntiles) {
+  __shared__ f4 park[G][256];
+  const int t0 = blockIdx.x * G;
+#pragma unroll 1
+  for (int g = 0; g < G; ++g) {
+    const int t = t0 + g;
+    if (t >= ntiles) break;
+    const int64_t b = (int64_t)t * 256 + threadIdx.x;
+    f4 acc = f4{0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < N; ++c) acc += ld(p.c[c], b);
+    park[g][threadIdx.x] = acc;
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int t = t0 + g;
+    if (t >= ntiles) break;
+    st(out, (int64_t)t * 256 + threadIdx.x, park[g][threadIdx.x]);
+  }
+}
+
 __global__ __launch_bounds__(256) void copy1(const float* s, float* d, int64_t nv) {
   const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (v < nv) st(d, v, ld(s, v));
@@ -148,9 +173,14 @@ int main() {
         flip ^= 1;                                                                               \
         nsum<N, 2, 0><<<t2, 256>>>(flip ? p2 : p, flip ? out2 : out, nv, t2, 1);                 \
       }, 20), 1);
+#define PARK(N, G)                                                                               \
+  rep("park_G" #G, N,                                                                            \
+      time_us([&] { nsum_park<N, G><<<(t1 + G - 1) / G, 256>>>(p, out, nv, t1); }, 20), 1);
   for (int r = 0; r < 2; ++r) {
     rep("copy1", 1, time_us([&] { copy1<<<t1, 256>>>(bufs[0], out, nv); }, 20), 1);
     RUN(5) RUN(20)
+    PARK(20, 1) PARK(20, 2) PARK(20, 4) PARK(20, 8) PARK(20, 16)
+    PARK(5, 1) PARK(5, 4) PARK(5, 16)
   }
   return 0;
 }
