@@ -11,9 +11,10 @@ global state — the reference's ``server_aggregate`` arithmetic
 ``value`` = algorithmic bytes (N·B read + B written, SURVEY.md §8 d) / time.
 
 N>1 (launched by torch.distributed.run, one rank per GPU): weak scaling,
-every rank holds 20 client slots; a step is the client-sharded round of
-feddct_amd/dist.py (local partial sums, RCCL all-reduce, /N_total); value =
-all ranks' algorithmic bytes / max-over-ranks time.
+every rank holds 20 client slots; a step is one client-sharded round over all
+N·20 slots (every round form of feddct_amd/comm.py and dist.py is timed, see
+``multi_gpu``); value = all ranks' algorithmic bytes / max-over-ranks time of
+the fastest form whose result is bit-identical to the single-GPU reduction.
 
 Also reported on the same JSON line: the roofline of the reduce kernel
 (HIP-event launch time vs the 8 TB/s HBM3E peak), the CPU baseline (the
@@ -792,17 +793,18 @@ def weighted_digest_check(case, layout, o32, o64):
             "bit_exact": digest_of(layout, o32, o64) == want}
 
 
-def torch_gpu_order_mode(layout, clients, steps=20):
+def torch_gpu_order_mode(layout, clients, steps=20, warmup=3, plan_flags=None):
     """The opt-in FA_ORDER_TORCH_GPU plan (torch-ROCm's own GPU
     stack(...).mean(0) order, the reference's .cuda() runs) on the cfg2
     workload: launch time and bit-exactness against torch's cuda mean of
     every key, computed here by torch itself."""
     n = len(clients)
+    fl = _lib.FA_PLAN_GAPS_ARE_PADDING if plan_flags is None else plan_flags
     plan = _lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
-                     order=_lib.FA_ORDER_TORCH_GPU, n=n)
+                     order=_lib.FA_ORDER_TORCH_GPU, n=n, flags=fl)
     o32, o64 = torch.zeros_like(clients[0][0]), torch.zeros_like(clients[0][1])
     red = Reducer(layout, clients, o32, o64, plan=plan)
-    t, _ = timed_launches(red, steps, 3)
+    t, _ = timed_launches(red, steps, warmup)
     ok = True
     for s in layout.slots:
         src = 1 if s.kind == "i64" else 0
@@ -852,12 +854,63 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt.item())
 
+    # kernel-only launch time for the roofline: this rank's 20-client reduce
+    # (first, so a run cut short by a phase deadline still has it)
+    kred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
+                   flags=_lib.FA_F_SUM_ONLY, plan=reducer.plan)
+    t_kernel, _ = timed_launches(kred, max(10, args.steps // 2), 3)
+    del kred
+
+    deadline_s = float(os.environ.get("FA_BENCH_PHASE_DEADLINE_S", "150"))
+
+    def abort_run(phase):
+        """A phase that outlives its deadline (a collective that never
+        completes) ends the run on every rank — each rank's own timer, same
+        deadline — instead of leaving the job hung until the launcher's limit.
+        Rank 0 first prints the line from the forms that finished, flagged
+        (parity unchecked, the phase named)."""
+        import faulthandler
+        log(f"[rank {rank}] phase '{phase}' exceeded {deadline_s:.0f} s; stacks follow")
+        faulthandler.dump_traceback(all_threads=True)
+        if rank == 0:
+            done = {n: m for n, m in modes.items() if "t" in m}
+            cands = [n for n in done if done[n]["exact_class"]] or list(done)
+            extra["modes"] = {n: ({"ms_per_step": round(m["t"] * 1e3, 4),
+                                   "GBps": round(nbytes_rank * world / m["t"] / 1e9, 2),
+                                   "bit_exact": None} if "t" in m else {"error": m["error"]})
+                              for n, m in modes.items()}
+            extra["aborted"] = {"phase": phase, "deadline_s": deadline_s,
+                                "note": "phase did not finish on every rank; results unchecked"}
+            extra["headline_not_verified_exact"] = True
+            if cands:
+                best = min(cands, key=lambda n: done[n]["t"])
+                extra["selected_mode"] = best
+                print(json.dumps(build_line(args, world, nbytes_rank, layout.state_bytes(),
+                                            done[best]["t"], t_kernel, extra)), flush=True)
+        sys.stderr.flush()
+        os._exit(0)
+
+    class phase:
+        def __init__(self, name):
+            self.name = name
+
+        def __enter__(self):
+            import threading
+            self.timer = threading.Timer(deadline_s, abort_run, args=(self.name,))
+            self.timer.daemon = True
+            self.timer.start()
+
+        def __exit__(self, *exc):
+            self.timer.cancel()
+            return False
+
     def run_mode(name, make, root, exact_class, steps=None, warm=None):
         log(f"[rank {rank}] {name}")
         try:
-            o32, o64 = torch.full_like(out32, float("nan")), torch.zeros_like(out64)
-            fn = make(o32, o64)
-            t = tmax(fn, steps or args.steps, args.warmup if warm is None else warm)
+            with phase(name):
+                o32, o64 = torch.full_like(out32, float("nan")), torch.zeros_like(out64)
+                fn = make(o32, o64)
+                t = tmax(fn, steps or args.steps, args.warmup if warm is None else warm)
             modes[name] = {"t": t, "root": root, "out": (o32, o64), "exact_class": exact_class}
         except Exception as e:  # noqa: BLE001  (reported in the line, every rank alike)
             modes[name] = {"error": repr(e)}
@@ -905,67 +958,64 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
     striped_host = None
     if not args.no_exact and not args.kernel_only:
         try:
-            striped, striped_host, hbufs = exact_modes(
-                layout, manifest, clients, out32, out64, world, group, dev, nbytes_rank,
-                max(3, min(5, args.steps // 10)))
+            with phase("e2/torch.distributed"):
+                striped, striped_host, hbufs = exact_modes(
+                    layout, manifest, clients, out32, out64, world, group, dev, nbytes_rank,
+                    max(3, min(5, args.steps // 10)))
             modes["e2/torch.distributed"] = {"t": striped["ms_per_step"] / 1e3, "root": 0,
                                              "out": hbufs[0:2], "exact_class": True}
         except Exception as e:  # noqa: BLE001
             modes["e2/torch.distributed"] = {"error": repr(e)}
-    # kernel-only launch time for the roofline: this rank's 20-client reduce
-    kred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
-                   flags=_lib.FA_F_SUM_ONLY, plan=reducer.plan)
-    t_kernel, _ = timed_launches(kred, max(10, args.steps // 2), 3)
-
     # parity of every mode on rank 0 (results on another rank travel there)
-    ex32 = ex64 = None
-    if rank == 0:
-        allc = make_clients(layout, manifest, range(n_total), dev)
-        ex32, ex64 = torch.zeros_like(out32), torch.zeros_like(out64)
-        Reducer(layout, allc, ex32, ex64)()
-        torch.cuda.synchronize()
-        del allc
-    segmask = torch.zeros(out32.numel(), dtype=torch.bool, device=dev)
-    for o, m in layout.segs32:
-        segmask[int(o):int(o + m)] = True
-    report = {}
-    for name in sorted(modes):
-        m = modes[name]
-        if "error" in m:
-            report[name] = {"error": m["error"]}
-            continue
-        o32, o64 = m["out"]
-        src = 0 if m["root"] < 0 else m["root"]
-        if src != 0:
-            from feddct_amd.dist import p2p
-            if rank == src:
-                p2p([(dist.isend, o32, 0), (dist.isend, o64, 0)], group)
-            elif rank == 0:
-                p2p([(dist.irecv, o32, src), (dist.irecv, o64, src)], group)
-        r = {"ms_per_step": round(m["t"] * 1e3, 4),
-             "GBps": round(nbytes_rank * world / m["t"] / 1e9, 2),
-             "result_on": "every rank" if m["root"] < 0 else f"rank {m['root']}"}
+    with phase("parity"):
+        ex32 = ex64 = None
         if rank == 0:
-            # every element of every key (the padding between keys is no
-            # tensor's and each mode leaves it as it likes)
-            a32, b32 = o32[segmask].view(torch.int32), ex32[segmask].view(torch.int32)
-            same = bool(torch.equal(a32, b32) and torch.equal(o64, ex64))
-            r["bit_exact"] = same
-            if not same:
-                r["max_ulp_fp32"] = ulp_dist(o32[segmask], ex32[segmask])
-                r["ulp_histogram_fp32"] = ulp_hist(o32[segmask], ex32[segmask])
-                r["int64_bit_exact"] = bool(torch.equal(o64, ex64))
-        report[name] = r
-    # the headline: the fastest mode whose result is the reference's bits
-    # (decided on rank 0, shared so every rank agrees)
-    best_t, best = float("inf"), ""
-    if rank == 0:
-        for name, r in report.items():
-            if r.get("bit_exact") and modes[name]["t"] < best_t:
-                best_t, best = modes[name]["t"], name
-    sel = [best, best_t]
-    dist.broadcast_object_list(sel, src=0, group=group)
-    best, best_t = sel
+            allc = make_clients(layout, manifest, range(n_total), dev)
+            ex32, ex64 = torch.zeros_like(out32), torch.zeros_like(out64)
+            Reducer(layout, allc, ex32, ex64)()
+            torch.cuda.synchronize()
+            del allc
+        segmask = torch.zeros(out32.numel(), dtype=torch.bool, device=dev)
+        for o, m in layout.segs32:
+            segmask[int(o):int(o + m)] = True
+        report = {}
+        for name in sorted(modes):
+            m = modes[name]
+            if "error" in m:
+                report[name] = {"error": m["error"]}
+                continue
+            o32, o64 = m["out"]
+            src = 0 if m["root"] < 0 else m["root"]
+            if src != 0:
+                from feddct_amd.dist import p2p
+                if rank == src:
+                    p2p([(dist.isend, o32, 0), (dist.isend, o64, 0)], group)
+                elif rank == 0:
+                    p2p([(dist.irecv, o32, src), (dist.irecv, o64, src)], group)
+            r = {"ms_per_step": round(m["t"] * 1e3, 4),
+                 "GBps": round(nbytes_rank * world / m["t"] / 1e9, 2),
+                 "result_on": "every rank" if m["root"] < 0 else f"rank {m['root']}"}
+            if rank == 0:
+                # every element of every key (the padding between keys is no
+                # tensor's and each mode leaves it as it likes)
+                a32, b32 = o32[segmask].view(torch.int32), ex32[segmask].view(torch.int32)
+                same = bool(torch.equal(a32, b32) and torch.equal(o64, ex64))
+                r["bit_exact"] = same
+                if not same:
+                    r["max_ulp_fp32"] = ulp_dist(o32[segmask], ex32[segmask])
+                    r["ulp_histogram_fp32"] = ulp_hist(o32[segmask], ex32[segmask])
+                    r["int64_bit_exact"] = bool(torch.equal(o64, ex64))
+            report[name] = r
+        # the headline: the fastest mode whose result is the reference's bits
+        # (decided on rank 0, shared so every rank agrees)
+        best_t, best = float("inf"), ""
+        if rank == 0:
+            for name, r in report.items():
+                if r.get("bit_exact") and modes[name]["t"] < best_t:
+                    best_t, best = modes[name]["t"], name
+        sel = [best, best_t]
+        dist.broadcast_object_list(sel, src=0, group=group)
+        best, best_t = sel
     if not best:   # no exact mode ran: report the exact class's fastest, flagged
         cands = [n for n, m in modes.items() if "t" in m and m["exact_class"]]
         best = min(cands, key=lambda n: modes[n]["t"]) if cands else min(
@@ -979,12 +1029,46 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
     if not args.kernel_only:
         log(f"[rank {rank}] config 5 sharded")
         try:
-            extra["cfg5_feddct_c100_n24_sharded"] = cfg5_sharded(dev, world, rank, group,
-                                                                  max(10, args.steps // 2),
-                                                                  ncomm, args.chain_chunks)
+            with phase("config 5 sharded"):
+                extra["cfg5_feddct_c100_n24_sharded"] = cfg5_sharded(
+                    dev, world, rank, group, max(10, args.steps // 2), ncomm, args.chain_chunks)
         except Exception as e:  # noqa: BLE001
             extra["cfg5_feddct_c100_n24_sharded"] = {"error": repr(e)}
     return best_t, t_kernel, ncomm
+
+def build_line(args, world, nbytes_rank, bytes_per_client, t_step, t_kernel, extra):
+    """The one JSON line (bench contract) from the measured times + extras."""
+    achieved = nbytes_rank / t_kernel / 1e9
+    traffic, traffic_src = pmc_traffic(world)
+    line = {
+        "metric": METRIC,
+        "value": round(nbytes_rank * world / t_step / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t_step * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (portable integer-hash PRNG, feddct_amd/synth.py; seeds 1000+client)",
+        "config": {"workload": f"FedAvg {N_CLIENTS} clients/GPU x wide_resnet16_8 CIFAR-10 "
+                               "(82 fp32 + 16 int64 keys), unweighted mean (reference semantics)",
+                   "clients_per_gpu": N_CLIENTS, "bytes_per_client": bytes_per_client,
+                   "algorithmic_bytes_per_step": nbytes_rank * world,
+                   "parallelism": (f"client shards x{world}: {extra.get('selected_mode')} "
+                                   "(fastest bit-exact round form; all forms in 'modes')"
+                                   if world > 1 else "single GPU")},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "traffic_pmc": traffic_src,
+                     "kernel_us": round(t_kernel * 1e6, 2)},
+        "cpu_baseline": None,
+    }
+    line.update(extra)
+    return line
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -1113,35 +1197,7 @@ def main():
         t_step, t_kernel, ncomm = multi_gpu(args, world, rank, dev, group, layout, manifest,
                                             clients, out32, out64, reducer, nbytes_rank, extra)
 
-    achieved = nbytes_rank / t_kernel / 1e9
-    traffic, traffic_src = pmc_traffic(world)
-    line = {
-        "metric": METRIC,
-        "value": round(nbytes_rank * world / t_step / 1e9, 2),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(t_step * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (portable integer-hash PRNG, feddct_amd/synth.py; seeds 1000+client)",
-        "config": {"workload": f"FedAvg {N_CLIENTS} clients/GPU x wide_resnet16_8 CIFAR-10 "
-                               "(82 fp32 + 16 int64 keys), unweighted mean (reference semantics)",
-                   "clients_per_gpu": N_CLIENTS, "bytes_per_client": layout.state_bytes(),
-                   "algorithmic_bytes_per_step": nbytes_rank * world,
-                   "parallelism": (f"client shards x{world}: {extra.get('selected_mode')} "
-                                   "(fastest bit-exact round form; all forms in 'modes')"
-                                   if world > 1 else "single GPU")},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "traffic_pmc": traffic_src,
-                     "kernel_us": round(t_kernel * 1e6, 2)},
-        "cpu_baseline": None,
-    }
-    line.update(extra)
+    line = build_line(args, world, nbytes_rank, layout.state_bytes(), t_step, t_kernel, extra)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.kernel_only:
         try:
             line["cpu_baseline"] = run_cpu_baseline(layout, manifest, clients, args.cpu_budget)

@@ -67,6 +67,7 @@ enum TileKind : int32_t {
   K_F32_TGPU_IN = 9,  // M == 1: lane split + intra-wave shuffle tree, 1 element/wave
   K_I64_TGPU_IN = 10,
   K_F32_TGPU_V = 11,  // [N, M>=2], 16-B aligned run: 4 elements per lane, up to 1024
+  K_F32_TGPU_W = 12,  // the same with S = 1: 8 elements per lane (2 x 16 B), up to 2048
 };
 
 __host__ __device__ inline bool kind_is64(int kind) {
@@ -719,6 +720,73 @@ __device__ __forceinline__ f4 tgpu_outer4(KArgs& a, int64_t start, uint32_t v, i
   return val[0];
 }
 
+// S = 1 (no row split: every BASELINE config's tensors) over 2048-element
+// tiles, the default kernel's load shape: U = 2 float4 per lane per row, rows
+// in batches of B (a multiple of 4, so row b of a batch feeds accumulator
+// b & 3 statically), loads through the same pointer accessor as the default
+// reduce.  Row p goes into accumulator p % 4 in increasing row order, then
+// ((a0 + a1) + a2) + a3 — torch's thread order, per component.
+template <int U, int B, bool FULL>
+__device__ __forceinline__ void tgpu_wide(KArgs& a, int64_t start, int count, float fac,
+                                          bool sum_only) {
+  static_assert(B % 4 == 0, "batch must keep the accumulator index static");
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  f4 acc[4][U];
+  uint32_t vi[U];
+  bool ok[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    vi[u] = threadIdx.x + u * kBlock;
+    ok[u] = FULL || (int)(4 * vi[u]) < count;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k][u] = z;
+  }
+  const int n = a.n;
+  int b0 = 0;
+  for (; b0 + B <= n; b0 += B) {
+    f4 x[B][U];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const float* p = cptr32(a, b0 + b) + start;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        x[b][u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[b & 3][u] += x[b][u];
+  }
+  if (b0 < n) {  // b0 % 4 == 0 here
+    const int nb = n - b0;
+    f4 x[B][U];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      if (b < nb) {
+        const float* p = cptr32(a, b0 + b) + start;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          x[b][u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+      if (b < nb)
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[b & 3][u] += x[b][u];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!FULL && !ok[u]) continue;
+    f4 r = ((acc[0][u] + acc[1][u]) + acc[2][u]) + acc[3][u];
+    if (!sum_only)
+      r = f4{__fmul_rn(r.x, fac), __fmul_rn(r.y, fac), __fmul_rn(r.z, fac), __fmul_rn(r.w, fac)};
+    stg4<true>(a.out32 + start, vi[u], r);
+    if (a.flags & FA_F_BCAST)
+      for (int i = 0; i < n; ++i) stg4<true>(const_cast<float*>(cptr32(a, i)) + start, vi[u], r);
+  }
+}
+
 // lane value of the inner order; the wave then runs the shuffle tree
 template <class Src>
 __device__ __forceinline__ float tgpu_inner(const Src& src, int64_t e, int n, int bw, int lane) {
@@ -745,6 +813,13 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   const int base = t.kind & 0xFF, ls = (t.kind >> 8) & 0xFF;
   const bool sum_only = a.flags & FA_F_SUM_ONLY;
   const int n = a.n;
+  if constexpr (LS == 0) {
+    if (base == K_F32_TGPU_W) {
+      if (t.count == 8 * kBlock) tgpu_wide<2, 16, true>(a, t.start, t.count, fac, sum_only);
+      else tgpu_wide<2, 16, false>(a, t.start, t.count, fac, sum_only);
+      return;
+    }
+  }
   if (base == K_F32_TGPU_V) {
     const uint32_t v = threadIdx.x;
     if ((int)(v * 4) >= t.count) return;
@@ -1358,9 +1433,14 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
       const int64_t head = std::min<int64_t>((4 - g.offset % 4) % 4, g.numel);
       const int64_t body = (g.numel - head) / 4 * 4;
       scalar(0, head);
-      for (int64_t c = head; c < head + body; c += 4 * kBlock) {
-        t.push_back(Tile{g.offset + c, (int32_t)std::min<int64_t>(4 * kBlock, head + body - c),
-                         K_F32_TGPU_V | (ls << 8)});
+      // S = 1: 2048-element tiles, the default reduce's load shape (r02:
+      // 151.9 us on cfg2 with the 1024-element form; FA_PLAN_TUNE_TGPU_NARROW
+      // keeps that form for A/B)
+      const bool wide = S == 1 && !(flags & FA_PLAN_TUNE_TGPU_NARROW);
+      const int64_t te = wide ? 8 * kBlock : 4 * kBlock;
+      for (int64_t c = head; c < head + body; c += te) {
+        t.push_back(Tile{g.offset + c, (int32_t)std::min<int64_t>(te, head + body - c),
+                         (wide ? K_F32_TGPU_W : K_F32_TGPU_V) | (ls << 8)});
         fac.push_back(f);
       }
       scalar(head + body, g.numel);

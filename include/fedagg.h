@@ -87,6 +87,8 @@ extern "C" {
 #define FA_PLAN_TUNE_ISSUE_ALL 0x100000u /* tuning: a batch's loads back to back
                                             (n <= FA_INLINE_CLIENTS, 2048-float tiles,
                                             BATCH4 or 8 clients per batch)     */
+#define FA_PLAN_TUNE_TGPU_NARROW 0x200000u /* tuning: torch-GPU order, S = 1 tensors in
+                                              1024-element tiles (r02 form)      */
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
 #define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
 /* tuning: persistent grid of 256*k workgroups striding over the tiles */
