@@ -26,7 +26,7 @@ FA_E_RANGE = -2
 FA_E_ALIGN = -3
 FA_E_HIP = -4
 FA_E_NOMEM = -5
-FA_MAX_CLIENTS = 4096
+FA_MAX_CLIENTS = 65536
 FA_INLINE_CLIENTS = 128
 FA_F_BCAST = 1
 FA_F_SUM_ONLY = 2

@@ -873,10 +873,14 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   }
 }
 
+// fa_broadcast_f32: up to kBcastInline destinations per launch, pointers in
+// the kernel arguments (more destinations: consecutive launches, each
+// re-reading the source)
+constexpr int kBcastInline = 256;
 struct BcastArgs {
   const float* src;
   int n;
-  float* dst[FA_MAX_CLIENTS];
+  float* dst[kBcastInline];
 };
 __global__ __launch_bounds__(kBlock) void bcast_kernel(BcastArgs a,
                                                        int64_t numel) {
@@ -1881,19 +1885,20 @@ int fa_broadcast_f32(const float* src, float* const* dst, int n, int64_t numel, 
   if (numel < 0 || (numel > 0 && (!src || (n > 0 && !dst))))
     return set_err(FA_E_INVAL, "fa_broadcast_f32: bad args");
   if (n == 0 || numel == 0) return FA_OK;
-  BcastArgs a;
-  memset(&a, 0, sizeof a);
-  a.src = src;
-  a.n = n;
   if (!aligned16(src)) return set_err(FA_E_ALIGN, "fa_broadcast_f32: src not 16-B aligned");
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < n; ++i)
     if (!dst[i] || !aligned16(dst[i]))
       return set_err(FA_E_ALIGN, "fa_broadcast_f32: dst %d NULL or unaligned", i);
-    a.dst[i] = dst[i];
+  for (int i0 = 0; i0 < n; i0 += kBcastInline) {
+    BcastArgs a;
+    memset(&a, 0, sizeof a);
+    a.src = src;
+    a.n = std::min(kBcastInline, n - i0);
+    for (int i = 0; i < a.n; ++i) a.dst[i] = dst[i0 + i];
+    hipLaunchKernelGGL(bcast_kernel, dim3(grid_for(numel / 4 + 1, kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, a, numel);
+    HIP_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(bcast_kernel, dim3(grid_for(numel / 4 + 1, kBlock)), dim3(kBlock), 0,
-                     (hipStream_t)stream, a, numel);
-  HIP_TRY(hipGetLastError());
   return FA_OK;
 }
 

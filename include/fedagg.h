@@ -62,9 +62,12 @@ extern "C" {
 #define FA_E_HIP (-4)     /* HIP runtime error (message in fa_last_error)     */
 #define FA_E_NOMEM (-5)
 
-/* Max clients per call.  Up to FA_INLINE_CLIENTS the client pointer tables
- * travel in the kernel arguments; above, in a stream-ordered device table. */
-#define FA_MAX_CLIENTS 4096
+/* Max clients per call (2^16: the cascade's four levels, promotions after
+ * 16, 256 and 4096 rows, all exercised; 65,536 wrn16_8 clients would need
+ * 2.9 TB, so one GPU's HBM, not this limit, bounds N).  Up to
+ * FA_INLINE_CLIENTS the client pointer tables travel in the kernel
+ * arguments; above, in a stream-ordered device table. */
+#define FA_MAX_CLIENTS 65536
 #define FA_INLINE_CLIENTS 128
 
 /* fa_reduce flags */

@@ -42,7 +42,7 @@ def test_version_and_error_paths():
     assert L.fa_reduce(None, None, None, 1, None, None, None, 0, None) == _lib.FA_E_INVAL
     assert L.fa_div_f32(None, 2.0, None, 0, None) == _lib.FA_OK
     assert L.fa_div_f32(None, 2.0, None, 5, None) == _lib.FA_E_INVAL
-    assert L.fa_broadcast_f32(None, None, 5000, 10, None) == _lib.FA_E_RANGE
+    assert L.fa_broadcast_f32(None, None, _lib.FA_MAX_CLIENTS + 1, 10, None) == _lib.FA_E_RANGE
     with pytest.raises(_lib.FedaggError, match="overlap"):
         _lib.build_tiles_host(np.array([[0, 10], [5, 10]]), 20)
 

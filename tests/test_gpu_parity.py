@@ -65,16 +65,18 @@ def test_reduce_matches_oracle(lib, n, mode):
         assert k == k2 and bits_equal(g, want), (n, mode, k)
 
 
-@pytest.mark.parametrize("n", [511, 512, 1000, 4095, 4096])
+@pytest.mark.parametrize("n", [511, 512, 1000, 4095, 4096, 4097, 8193, 65536])
 def test_many_clients_up_to_the_maximum(lib, n):
-    """Up to FA_MAX_CLIENTS: the device pointer table, the cascade's third
-    level (promotion after 16^3 = 4096 rows) and every column rule, against
-    the oracle and torch itself.  torch runs single-threaded here: with
-    N*M >= 32768 its column chunking across threads can move a tensor's last
-    few tail columns to another order; the engine defines the
-    single-thread order, which is what torch produces for the reference's
+    """Up to FA_MAX_CLIENTS = 2^16: the device pointer table, the cascade's
+    third and fourth levels (promotions after 16^2 and 16^3 = 4096 rows; l3
+    accumulates every 4096-row block from there on) and every column rule,
+    against the oracle and torch itself.  torch runs single-threaded here:
+    with N*M >= 32768 its column chunking across threads can move a tensor's
+    last few tail columns to another order; the engine defines
+    the single-thread order, which is what torch produces for the reference's
     layouts."""
-    man = _rand_manifest(np.random.default_rng(n), [0, 1, 5, 33, 100, 1060])
+    sizes = [0, 1, 5, 33, 100, 1060] if n <= 8193 else [0, 1, 5, 33, 260]
+    man = _rand_manifest(np.random.default_rng(n), sizes)
     layout = BucketLayout.from_manifest(man)
     states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
     out32, out64 = _reduce(lib, layout, states_to_buckets(layout, states, DEV))
@@ -104,6 +106,24 @@ def test_weighted_many_clients(lib):
         x = np.stack([s[j][1] for s in states])
         want = O.mean_i64_trunc(x) if x.dtype == np.int64 else O.weighted_sum0(x, w)
         assert bits_equal(got[k], want), k
+
+
+@pytest.mark.parametrize("n", [1, 3, 256, 257, 600])
+def test_broadcast_f32(lib, n):
+    """fa_broadcast_f32 (the stand-alone global -> clients copy): every
+    destination gets every element, ragged tail included; more than 256
+    destinations take consecutive launches."""
+    numel = 1000 * 4 + 3
+    src = torch.randn(numel, device=DEV)
+    dst = [torch.full((numel + 5,), -1.0, device=DEV) for _ in range(n)]
+    ptrs = (ctypes.c_void_p * n)(*[d.data_ptr() for d in dst])
+    stream = torch.cuda.current_stream().cuda_stream
+    lib.check(lib.lib.fa_broadcast_f32(ctypes.c_void_p(src.data_ptr()), ptrs, n, numel,
+                                       ctypes.c_void_p(stream)), "fa_broadcast_f32")
+    torch.cuda.synchronize()
+    for d in dst:
+        assert torch.equal(d[:numel], src)
+        assert bool((d[numel:] == -1.0).all())
 
 
 def test_too_many_clients_is_refused(lib):
@@ -255,7 +275,7 @@ def test_errors(lib):
         bk = states_to_buckets(layout, [synth.gen_state({"keys": [
             {"key": "k0", "shape": [100], "dtype": "float32"},
             {"key": "nbt", "shape": [], "dtype": "int64"}]}, 0)], DEV)
-        _reduce(lib, layout, bk * 4097)
+        _reduce(lib, layout, bk * (lib.FA_MAX_CLIENTS + 1))
     misaligned = torch.zeros(200, device=DEV)[1:]
     plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel)
     rc = lib.lib.fa_reduce(plan.handle, lib.ptr_array([misaligned.data_ptr()]),
