@@ -54,10 +54,10 @@ def _expected(states, weights):
     return out
 
 
-def _run(mode, counts, root, weighted=False, exchange=C.FA_XCHG_REDUCE, nchunks=5):
-    layout = BucketLayout.from_manifest(MAN)
+def _run(mode, counts, root, weighted=False, exchange=C.FA_XCHG_REDUCE, nchunks=5, man=MAN):
+    layout = BucketLayout.from_manifest(man)
     n = sum(counts)
-    states = [synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL) for c in range(n)]
+    states = [synth.gen_state(man, c, synth.MODE_ADVERSARIAL) for c in range(n)]
     c32, c64 = _buckets(layout, states)
     w = O.weights_from_sizes(np.arange(1, n + 1) * 5 + 1) if weighted else None
     _, tiles = layout_tiles(layout)
@@ -269,6 +269,26 @@ def test_blocked_schedule_weighted_is_exact(counts):
             src = bufs[r]["OUT64"] if s.kind == "i64" else bufs[r]["OUT"]
             got = src[s.offset:s.offset + s.numel].reshape(s.shape)
             assert got.tobytes() == np.asarray(want[s.key]).tobytes(), (r, s.key)
+
+
+# N_total > 4096 (FA_MAX_CLIENTS is 65536): the chained state's fourth plane,
+# the fold's level-3 promotion after every 256th block
+SMALL_MAN = {"keys": [{"key": f"k{j}", "shape": [m] if m else [], "dtype": "float32"}
+                      for j, m in enumerate([40, 3, 0, 64 + 5])]
+             + [{"key": "nbt", "shape": [], "dtype": "int64"}]}
+
+
+@pytest.mark.parametrize("mode,counts", [(C.FA_MODE_BLOCKED, [2000, 2500, 700]),
+                                         (C.FA_MODE_BLOCKED, [4100, 0, 1]),
+                                         (C.FA_MODE_CHAINED, [3000, 2200]),
+                                         (C.FA_MODE_CHAINED, [1, 4200, 17])])
+def test_exact_schedules_beyond_4096_clients(mode, counts):
+    layout, states, _, bufs, _ = _run(mode, counts, 0, man=SMALL_MAN)
+    want = _expected(states, None)
+    for s in layout.slots:
+        src = bufs[0]["OUT64"] if s.kind == "i64" else bufs[0]["OUT"]
+        got = src[s.offset:s.offset + s.numel].reshape(s.shape)
+        assert got.tobytes() == np.asarray(want[s.key]).tobytes(), s.key
 
 
 @pytest.mark.parametrize("counts", [[4, 9, 0, 2, 5], [1, 1, 1, 17], [3] * 8])
