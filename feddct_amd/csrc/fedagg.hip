@@ -636,6 +636,96 @@ __global__ __launch_bounds__(kBlock) void bcast_tiles_kernel(ReduceArgs args) {
   }
 }
 
+// The round's broadcast (default since r02): one workgroup per (tile, group
+// of G consecutive clients), groups fastest, so a tile's groups run side by
+// side and its source is fetched once and then served from the caches; the
+// tile's loads (U float4 per lane) go out before the group's G*U stores.
+// G = ceil(n / ceil(n / 8)) (20 clients: 7, 7, 6).  tools/bcastlab.hip
+// (profiles/r02_bcastlab.jsonl), 20 x 43.9 MB: groups of 5-10 clients
+// 134.9-135.2 us, the pure-fill ceiling 130.1 us, one workgroup per tile
+// writing all 20 clients (bcast_tiles_kernel above, the r01 form, kept as
+// FA_PLAN_TUNE_BCAST_TILES) 153-155 us.  One client per workgroup reaches
+// the fill ceiling in the lab (no tile table) but in the product each
+// workgroup's dependent tile-descriptor and source loads then serialise
+// (168-267 us measured): the group amortises them.
+__global__ __launch_bounds__(kBlock) void bcast_group_kernel(ReduceArgs args, uint32_t groups,
+                                                             uint32_t gsize) {
+  (void)args;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const uint32_t total = (uint32_t)a.ntiles * groups;
+  for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
+    const uint32_t ti = v / groups;
+    const int c0 = (int)((v - ti * groups) * gsize);
+    const int c1 = min(a.n, c0 + (int)gsize);
+    const Tile t = a.tiles[ti];
+    const int kb = t.kind & 0xFF;
+    if (kb == K_F32_VEC || kb == K_F32_TGPU_V || kb == K_F32_TGPU_W) {
+      const uint32_t nv = (uint32_t)t.count / 4;
+      // up to 4 vectors per lane (the table's U)
+      f4 r[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t vi = threadIdx.x + u * kBlock;
+        if (vi < nv) r[u] = ldg4<false>(a.out32 + t.start, vi);
+      }
+      for (int c = c0; c < c1; ++c) {
+        float* d = const_cast<float*>(cptr32(a, c)) + t.start;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t vi = threadIdx.x + u * kBlock;
+          if (vi < nv) stg4<true>(d, vi, r[u]);
+        }
+      }
+    } else if ((int)threadIdx.x < t.count) {
+      const int64_t e = t.start + threadIdx.x;
+      if (!kind_is64(t.kind)) {
+        const float r = a.out32[e];
+        for (int c = c0; c < c1; ++c) const_cast<float*>(cptr32(a, c))[e] = r;
+      } else {
+        const int64_t r = a.out64[e];
+        for (int c = c0; c < c1; ++c) const_cast<int64_t*>(cptr64(a, c))[e] = r;
+      }
+    }
+  }
+}
+
+// The flat form of the round's broadcast (tuning, FA_PLAN_TUNE_BCAST_FLAT;
+// plans cut from a segment list with FA_PLAN_GAPS_ARE_PADDING only: their
+// buckets hold tensors and padding, so the whole fp32 bucket may be copied
+// without the tile table) — one workgroup per (1024-float part, client),
+// clients fastest, one 16-B load and one non-temporal 16-B store per lane.
+// In tools/bcastlab.hip this shape runs at the pure-fill ceiling (split_U1_G1
+// / split_rt: 130-134 us for 20 x 43.9 MB against 128-130 us of pure
+// writes; profiles/r02_bcastlab*.jsonl), but in the product, on the same box,
+// it took 168-169 us standalone and 255-265 us after the reduce, against
+// 150-170 us for bcast_group_kernel (exp_bcast, profiles/r02_exp_bcast*.jsonl)
+// — not explained yet, so it is not the default.  The int64 bucket is one
+// extra part per client.
+__global__ __launch_bounds__(kBlock) void bcast_flat_kernel(ReduceArgs args, uint32_t parts,
+                                                            int64_t f32_numel,
+                                                            int64_t i64_numel) {
+  (void)args;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const uint32_t n = (uint32_t)a.n;
+  const uint32_t total = (parts + (i64_numel > 0 ? 1u : 0u)) * n;
+  const int64_t nv = f32_numel / 4;
+  for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
+    const uint32_t p = v / n;
+    const int c = (int)(v - p * n);
+    if (p < parts) {
+      const int64_t base = (int64_t)p * (4 * kBlock);  // floats
+      float* d = const_cast<float*>(cptr32(a, c));
+      if ((int64_t)p * kBlock + threadIdx.x < nv)
+        stg4<true>(d + base, threadIdx.x, ldg4<false>(a.out32 + base, threadIdx.x));
+      if (p == parts - 1 && (int64_t)threadIdx.x < f32_numel - 4 * nv)
+        d[4 * nv + threadIdx.x] = a.out32[4 * nv + threadIdx.x];
+    } else {
+      int64_t* d = const_cast<int64_t*>(cptr64(a, c));
+      for (int64_t e = threadIdx.x; e < i64_numel; e += kBlock) d[e] = a.out64[e];
+    }
+  }
+}
+
 // ---------------------------------------------- torch-ROCm's GPU order ----
 // The reduction torch-ROCm itself performs for stack(list, 0).mean(0) on
 // device tensors (ATen/native/hip/Reduce.cuh as built into this torch:
@@ -882,16 +972,30 @@ struct BcastArgs {
   int n;
   float* dst[kBcastInline];
 };
-__global__ __launch_bounds__(kBlock) void bcast_kernel(BcastArgs a,
-                                                       int64_t numel) {
+// One workgroup per (2048-float part, group of <= 8 destinations), groups
+// fastest (bcast_group_kernel's shape: 157-160 us for 20 x 43.9 MB, against
+// 168-169 us with one destination per workgroup); the last part also copies
+// the numel % 4 tail.
+__global__ __launch_bounds__(kBlock) void bcast_kernel(BcastArgs a, int64_t numel,
+                                                       uint32_t parts, uint32_t groups,
+                                                       uint32_t gsize) {
   const int64_t nv = numel / 4;
-  for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nv;
-       v += (int64_t)gridDim.x * kBlock) {
-    const f4 x = ld4<true>(a.src + 4 * v);
-    for (int i = 0; i < a.n; ++i) st4<true>(a.dst[i] + 4 * v, x);
+  const uint32_t total = parts * groups;
+  for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
+    const uint32_t p = v / groups;
+    const int c0 = (int)((v - p * groups) * gsize);
+    const int c1 = min(a.n, c0 + (int)gsize);
+    const int64_t v0 = (int64_t)p * 2 * kBlock + threadIdx.x, v1 = v0 + kBlock;
+    f4 r0 = {0.f, 0.f, 0.f, 0.f}, r1 = r0;
+    if (v0 < nv) r0 = ld4<false>(a.src + 4 * v0);
+    if (v1 < nv) r1 = ld4<false>(a.src + 4 * v1);
+    for (int c = c0; c < c1; ++c) {
+      if (v0 < nv) st4<true>(a.dst[c] + 4 * v0, r0);
+      if (v1 < nv) st4<true>(a.dst[c] + 4 * v1, r1);
+    }
+    if (p == parts - 1 && threadIdx.x < numel - 4 * nv)
+      for (int c = c0; c < c1; ++c) a.dst[c][4 * nv + threadIdx.x] = a.src[4 * nv + threadIdx.x];
   }
-  if (blockIdx.x == 0 && threadIdx.x < numel - 4 * nv)
-    for (int i = 0; i < a.n; ++i) a.dst[i][4 * nv + threadIdx.x] = a.src[4 * nv + threadIdx.x];
 }
 
 // Streaming copy (the roofline's calibration): one 16-B non-temporal load and
@@ -995,6 +1099,9 @@ struct fa_plan {
   int order_n = 0;        // FA_ORDER_TORCH_GPU: the client count it was cut for
   float* d_fac = nullptr; // ... and its per-tile mean factors
   int tg_lo[6] = {0, 0, 0, 0, 0, 0};  // ... tiles grouped by row split S = 1..16
+  // cut from a segment list with FA_PLAN_GAPS_ARE_PADDING: every byte of
+  // the buckets is a tensor's or padding, so the broadcast may copy them flat
+  bool flat_bcast = false;
 };
 
 namespace {
@@ -1321,6 +1428,7 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   p->info.tile_elems = tile_elems;
   p->vec_u = tile_elems / (4 * kBlock);
   p->flags = flags;
+  p->flat_bcast = (flags & FA_PLAN_GAPS_ARE_PADDING) != 0;
   std::vector<Tile> tiles, alt;
   rc = build_tiles(s32, s64, tile_elems, flags, &tiles, &p->info);
   if (rc) {
@@ -1683,6 +1791,10 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
                      plan->order_n, n);
     }
     hipError_t e = hipSuccess;
+    // the broadcast as its own launch over the whole table, client groups
+    // per tile (as the default order's split broadcast)
+    const bool bc = (flags & FA_F_BCAST) != 0;
+    a.flags &= ~FA_F_BCAST;
     for (int g = 0; g < 5 && e == hipSuccess; ++g) {
       const int lo = plan->tg_lo[g], cnt = plan->tg_lo[g + 1] - lo;
       if (cnt == 0) continue;
@@ -1696,6 +1808,17 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
         case 3: hipLaunchKernelGGL(tgpu_kernel<3>, dim3(cnt), dim3(kBlock), 0, st, a); break;
         default: hipLaunchKernelGGL(tgpu_kernel<4>, dim3(cnt), dim3(kBlock), 0, st, a); break;
       }
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess && bc && plan->tg_lo[5] > 0) {
+      a.flags |= FA_F_BCAST;
+      a.tiles = plan->d_tiles;
+      a.ntiles = plan->tg_lo[5];
+      const uint32_t groups = (uint32_t)((n + 7) / 8);
+      const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
+      const unsigned grid =
+          (unsigned)std::min<int64_t>((int64_t)a.ntiles * groups, 1ll << 30);
+      hipLaunchKernelGGL(bcast_group_kernel, dim3(grid), dim3(kBlock), 0, st, a, groups, gsize);
       e = hipGetLastError();
     }
     if (table) {
@@ -1723,8 +1846,30 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
   hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st);
   if (e == hipSuccess && split_bcast) {
     a.flags |= FA_F_BCAST;
-    hipLaunchKernelGGL(bcast_tiles_kernel, dim3(ntiles), dim3(kBlock), 0, st, a);
-    e = hipGetLastError();
+    if (plan->flags & FA_PLAN_TUNE_BCAST_TILES) {
+      hipLaunchKernelGGL(bcast_tiles_kernel, dim3(ntiles), dim3(kBlock), 0, st, a);
+    } else if ((plan->flags & FA_PLAN_TUNE_BCAST_FLAT) && plan->flat_bcast && n > 0 &&
+               ((plan->has32 ? plan->info.f32_numel : 0) > 0 || plan->has64)) {
+      const int64_t f = plan->has32 ? plan->info.f32_numel : 0;
+      const int64_t i = plan->has64 ? plan->info.i64_numel : 0;
+      const int64_t parts = f > 0 ? std::max<int64_t>(1, (f / 4 + kBlock - 1) / kBlock) : 0;
+      const int64_t total = (parts + (i > 0 ? 1 : 0)) * n;
+      if (total > (int64_t)UINT32_MAX) {
+        e = hipErrorInvalidValue;
+      } else {
+        const unsigned grid = (unsigned)std::min<int64_t>(total, 1ll << 30);
+        hipLaunchKernelGGL(bcast_flat_kernel, dim3(grid), dim3(kBlock), 0, st, a,
+                           (uint32_t)parts, f, i);
+      }
+    } else if (n > 0 && ntiles > 0) {
+      const uint32_t groups = (uint32_t)((n + 7) / 8);
+      const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
+      // ntiles * groups < 2^32: n clients of ntiles 4-16 KB tiles would
+      // outgrow any GPU's memory long before
+      const unsigned grid = (unsigned)std::min<int64_t>((int64_t)ntiles * groups, 1ll << 30);
+      hipLaunchKernelGGL(bcast_group_kernel, dim3(grid), dim3(kBlock), 0, st, a, groups, gsize);
+    }
+    if (e == hipSuccess) e = hipGetLastError();
   }
   if (table) {
     hipError_t e2 = hipFreeAsync(table, st);
@@ -1895,8 +2040,14 @@ int fa_broadcast_f32(const float* src, float* const* dst, int n, int64_t numel, 
     a.src = src;
     a.n = std::min(kBcastInline, n - i0);
     for (int i = 0; i < a.n; ++i) a.dst[i] = dst[i0 + i];
-    hipLaunchKernelGGL(bcast_kernel, dim3(grid_for(numel / 4 + 1, kBlock)), dim3(kBlock), 0,
-                       (hipStream_t)stream, a, numel);
+    const int64_t parts = std::max<int64_t>(1, (numel / 4 + 2 * kBlock - 1) / (2 * kBlock));
+    const uint32_t groups = (uint32_t)((a.n + 7) / 8);
+    const uint32_t gsize = (uint32_t)((a.n + groups - 1) / groups);
+    if (parts * groups > (int64_t)UINT32_MAX)
+      return set_err(FA_E_RANGE, "fa_broadcast_f32: numel=%lld", (long long)numel);
+    const unsigned grid = (unsigned)std::min<int64_t>(parts * groups, 1ll << 30);
+    hipLaunchKernelGGL(bcast_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a, numel,
+                       (uint32_t)parts, groups, gsize);
     HIP_TRY(hipGetLastError());
   }
   return FA_OK;

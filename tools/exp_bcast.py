@@ -1,5 +1,7 @@
 """Experiment: the round's broadcast (train_fedavg.py:148-149) — the default
-FA_F_BCAST (reduce launch + tile-table broadcast launch), the fused form
+FA_F_BCAST (reduce launch + broadcast launch over client groups), one
+workgroup per tile (r01), the flat copy (one workgroup per part and client),
+the fused form
 (FA_PLAN_TUNE_FUSED_BCAST, under several plan tuning flags) and the reduce
 followed by the standalone whole-bucket broadcast kernel (fa_broadcast_f32; the int64
 keys, 128 B, are left out of that variant), cfg2 shape, interleaved rounds
@@ -37,6 +39,10 @@ def main():
     F = _lib.FA_PLAN_TUNE_FUSED_BCAST
     variants = {
         "default": Reducer(lay, clients, o32, o64, flags=B, plan=plan()),
+        "tiles_r01": Reducer(lay, clients, o32, o64, flags=B,
+                             plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_TILES)),
+        "flat": Reducer(lay, clients, o32, o64, flags=B,
+                        plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_FLAT)),
         "fused": Reducer(lay, clients, o32, o64, flags=B, plan=plan(0, F)),
         "fused_tile1024": Reducer(lay, clients, o32, o64, flags=B, plan=plan(1024, F)),
         "fused_tile2048": Reducer(lay, clients, o32, o64, flags=B, plan=plan(2048, F)),
