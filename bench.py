@@ -1130,8 +1130,13 @@ def main():
             # streaming work BEFORE the headline's own W warmups, so the
             # timed steps do not see the clocks ramp: the copy ceiling of this
             # box, the weighted and broadcast variants of the same reduction
+            # non-zero data on both sides: zero-filled buffers stream faster on
+            # this chip than real data (tools/bcastlab.hip: the same broadcast
+            # 130 us on zeros, 169 us on hashed values), which would overstate
+            # the ceiling
             big = torch.empty(256 * 1024 * 1024, dtype=torch.float32, device=dev)  # 1 GiB
-            big2 = torch.empty_like(big)
+            big.uniform_(-1.0, 1.0)
+            big2 = torch.empty_like(big).uniform_(-1.0, 1.0)
 
             def copy_big():
                 _lib.check(_lib.lib.fa_copy_f32(big.data_ptr(), big2.data_ptr(), big.numel(),

@@ -116,6 +116,18 @@ __global__ __launch_bounds__(256) void split_rt_table(const float* s, Dst d, con
   }
 }
 
+// non-zero, non-repeating data (an integer hash per element)
+__global__ void hash_fill(float* p, int64_t n, uint32_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 15;
+    x *= 2246822519u;
+    x ^= x >> 13;
+    p[i] = (float)(x & 0xFFFFFF) * (1.0f / 16777216.0f) - 0.5f;
+  }
+}
+
 // client-major: workgroup b copies tile b % T into client b / T (the source
 // is re-read from the Infinity Cache, 43.9 MB << 256 MiB)
 template <int U>
@@ -194,6 +206,17 @@ int main() {
         time_ms([&] { client_major<1><<<T(1) * kN, 256>>>(s, d, nv, T(1)); }, 20), bytes);
     rep("client_major_U2",
         time_ms([&] { client_major<2><<<T(2) * kN, 256>>>(s, d, nv, T(2)); }, 20), bytes);
+  }
+  // the same variants with non-zero data in the source and every destination
+  hash_fill<<<4096, 256>>>(s, n, 7u);
+  for (int c = 0; c < kN; ++c) hash_fill<<<4096, 256>>>(d.d[c], n, 100u + c);
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < 3; ++r) {
+    rep("rand_split_rt", time_ms([&] { split_rt<<<parts * kN, 256>>>(s, d, nv, kN, parts); }, 20),
+        bytes);
+    rep("rand_split_U2_G5", time_ms([&] { split<2, 5><<<T(2) * 4, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_tile_major_U2", time_ms([&] { tile_major<2><<<T(2), 256>>>(s, d, nv); }, 20),
+        bytes);
   }
   CK(hipFree(s));
   for (int c = 0; c < kN; ++c) CK(hipFree(d.d[c]));

@@ -3,10 +3,14 @@
 // same allocation scheme.  Standalone lab binary (not the product):
 //   hipcc --offload-arch=gfx950 -O3 -o tools/reducelab tools/reducelab.hip
 // One JSON line per (variant, N, round); GB/s counts N inputs + 1 output.
+// `reducelab hashed`: every buffer filled with non-zero hashed values first
+// (zero-filled buffers stream faster on this chip than real data,
+// tools/bcastlab.hip; the r02 numbers before this option were on zeros).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                                  \
@@ -107,6 +111,17 @@ __global__ __launch_bounds__(256) void copy1(const float* s, float* d, int64_t n
   if (v < nv) st(d, v, ld(s, v));
 }
 
+__global__ void hash_fill(float* p, int64_t n, uint32_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 15;
+    x *= 2246822519u;
+    x ^= x >> 13;
+    p[i] = (float)(x & 0xFFFFFF) * (1.0f / 16777216.0f) - 0.5f;
+  }
+}
+
 template <class F>
 float time_us(F f, int reps) {
   hipEvent_t a, b;
@@ -125,7 +140,8 @@ float time_us(F f, int reps) {
   return ms * 1e3f / reps;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool hashed = argc > 1 && strcmp(argv[1], "hashed") == 0;
   const int64_t m = 10971136;  // floats per client: ~ the wrn16_8 bucket, 4096-aligned
   const int64_t nv = m / 4;
   std::vector<float*> bufs(MAXN);
@@ -140,7 +156,8 @@ int main() {
   for (int c = 0; c < MAXN; ++c) p.c[c] = bufs[c];
   auto rep = [&](const char* name, int n, float us, int nw) {
     double bytes = (double)m * 4 * (n + nw);
-    printf("{\"variant\": \"%s\", \"n\": %d, \"us\": %.2f, \"GBps\": %.1f}\n", name, n, us,
+    printf("{\"variant\": \"%s\", \"n\": %d, \"data\": \"%s\", \"us\": %.2f, "
+           "\"GBps\": %.1f}\n", name, n, hashed ? "hashed" : "zeros", us,
            bytes / (us * 1e-6) / 1e9);
     fflush(stdout);
   };
@@ -155,6 +172,14 @@ int main() {
   CK(hipMalloc(&out2, m * 4));
   Ptrs p2;
   for (int c = 0; c < MAXN; ++c) p2.c[c] = bufs2[c];
+  if (hashed) {
+    uint32_t seed = 1;
+    for (auto* q : bufs) hash_fill<<<4096, 256>>>(q, m, seed++);
+    for (auto* q : bufs2) hash_fill<<<4096, 256>>>(q, m, seed++);
+    hash_fill<<<4096, 256>>>(out, m, seed++);
+    hash_fill<<<4096, 256>>>(out2, m, seed++);
+    CK(hipDeviceSynchronize());
+  }
   int flip = 0;
 #define RUN(N)                                                                                   \
   rep("rw_U1", N, time_us([&] { nsum<N, 1, 0><<<t1, 256>>>(p, out, nv, t1, 1); }, 20), 1);       \
@@ -179,8 +204,10 @@ int main() {
   for (int r = 0; r < 2; ++r) {
     rep("copy1", 1, time_us([&] { copy1<<<t1, 256>>>(bufs[0], out, nv); }, 20), 1);
     RUN(5) RUN(20)
-    PARK(20, 1) PARK(20, 2) PARK(20, 4) PARK(20, 8) PARK(20, 16)
-    PARK(5, 1) PARK(5, 4) PARK(5, 16)
+    if (!hashed) {
+      PARK(20, 1) PARK(20, 2) PARK(20, 4) PARK(20, 8) PARK(20, 16)
+      PARK(5, 1) PARK(5, 4) PARK(5, 16)
+    }
   }
   return 0;
 }
