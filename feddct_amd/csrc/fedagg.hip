@@ -640,14 +640,14 @@ __global__ __launch_bounds__(kBlock) void bcast_tiles_kernel(ReduceArgs args) {
 // of G consecutive clients), groups fastest, so a tile's groups run side by
 // side and its source is fetched once and then served from the caches; the
 // tile's loads (U float4 per lane) go out before the group's G*U stores.
-// G = ceil(n / ceil(n / 8)) (20 clients: 7, 7, 6).  tools/bcastlab.hip
-// (profiles/r02_bcastlab.jsonl), 20 x 43.9 MB: groups of 5-10 clients
-// 134.9-135.2 us, the pure-fill ceiling 130.1 us, one workgroup per tile
-// writing all 20 clients (bcast_tiles_kernel above, the r01 form, kept as
-// FA_PLAN_TUNE_BCAST_TILES) 153-155 us.  One client per workgroup reaches
-// the fill ceiling in the lab (no tile table) but in the product each
-// workgroup's dependent tile-descriptor and source loads then serialise
-// (168-267 us measured): the group amortises them.
+// G = ceil(n / ceil(n / kBcastGroup)) (20 clients: 10, 10).  tools/bcastlab.hip
+// on hashed data (profiles/r02_bcastlab_gsweep_hashed.jsonl), 20 x 43.9 MB,
+// U = 2: G = 10 150.7-151.7 us, G = 5/7 158.7-160.5, G = 4 164, G = 2 173,
+// one workgroup per tile writing all 20 (bcast_tiles_kernel above, the r01
+// form, kept as FA_PLAN_TUNE_BCAST_TILES) 173-176, one client per workgroup
+// 169-170 us.  (On zero-filled buffers every form is faster and G = 1 looks
+// best: 130 us — not a real-data ceiling.)
+constexpr int kBcastGroup = 10;
 __global__ __launch_bounds__(kBlock) void bcast_group_kernel(ReduceArgs args, uint32_t groups,
                                                              uint32_t gsize) {
   (void)args;
@@ -972,10 +972,9 @@ struct BcastArgs {
   int n;
   float* dst[kBcastInline];
 };
-// One workgroup per (2048-float part, group of <= 8 destinations), groups
-// fastest (bcast_group_kernel's shape: 157-160 us for 20 x 43.9 MB, against
-// 168-169 us with one destination per workgroup); the last part also copies
-// the numel % 4 tail.
+// One workgroup per (2048-float part, group of <= kBcastGroup destinations),
+// groups fastest (bcast_group_kernel's shape); the last part also copies the
+// numel % 4 tail.
 __global__ __launch_bounds__(kBlock) void bcast_kernel(BcastArgs a, int64_t numel,
                                                        uint32_t parts, uint32_t groups,
                                                        uint32_t gsize) {
@@ -1814,7 +1813,7 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
       a.flags |= FA_F_BCAST;
       a.tiles = plan->d_tiles;
       a.ntiles = plan->tg_lo[5];
-      const uint32_t groups = (uint32_t)((n + 7) / 8);
+      const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
       const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
       const unsigned grid =
           (unsigned)std::min<int64_t>((int64_t)a.ntiles * groups, 1ll << 30);
@@ -1862,7 +1861,7 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
                            (uint32_t)parts, f, i);
       }
     } else if (n > 0 && ntiles > 0) {
-      const uint32_t groups = (uint32_t)((n + 7) / 8);
+      const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
       const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
       // ntiles * groups < 2^32: n clients of ntiles 4-16 KB tiles would
       // outgrow any GPU's memory long before
@@ -2041,7 +2040,7 @@ int fa_broadcast_f32(const float* src, float* const* dst, int n, int64_t numel, 
     a.n = std::min(kBcastInline, n - i0);
     for (int i = 0; i < a.n; ++i) a.dst[i] = dst[i0 + i];
     const int64_t parts = std::max<int64_t>(1, (numel / 4 + 2 * kBlock - 1) / (2 * kBlock));
-    const uint32_t groups = (uint32_t)((a.n + 7) / 8);
+    const uint32_t groups = (uint32_t)((a.n + kBcastGroup - 1) / kBcastGroup);
     const uint32_t gsize = (uint32_t)((a.n + groups - 1) / groups);
     if (parts * groups > (int64_t)UINT32_MAX)
       return set_err(FA_E_RANGE, "fa_broadcast_f32: numel=%lld", (long long)numel);

@@ -211,6 +211,19 @@ int main() {
   hash_fill<<<4096, 256>>>(s, n, 7u);
   for (int c = 0; c < kN; ++c) hash_fill<<<4096, 256>>>(d.d[c], n, 100u + c);
   CK(hipDeviceSynchronize());
+  for (int r = 0; r < 2; ++r) {
+    rep("rand_split_U1_G2", time_ms([&] { split<1, 2><<<T(1) * 10, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_split_U1_G4", time_ms([&] { split<1, 4><<<T(1) * 5, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_split_U1_G7", time_ms([&] { split<1, 7><<<T(1) * 3, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_split_U1_G10", time_ms([&] { split<1, 10><<<T(1) * 2, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_split_U2_G2", time_ms([&] { split<2, 2><<<T(2) * 10, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_split_U2_G4", time_ms([&] { split<2, 4><<<T(2) * 5, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_split_U2_G7", time_ms([&] { split<2, 7><<<T(2) * 3, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_split_U2_G10", time_ms([&] { split<2, 10><<<T(2) * 2, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_split_U4_G4", time_ms([&] { split<4, 4><<<T(4) * 5, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_split_U4_G10", time_ms([&] { split<4, 10><<<T(4) * 2, 256>>>(s, d, nv); }, 20), bytes);
+    rep("rand_fill_U1", time_ms([&] { fill<1><<<T(1) * kN, 256>>>(d, nv, T(1)); }, 20), wbytes);
+  }
   for (int r = 0; r < 3; ++r) {
     rep("rand_split_rt", time_ms([&] { split_rt<<<parts * kN, 256>>>(s, d, nv, kN, parts); }, 20),
         bytes);
