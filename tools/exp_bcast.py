@@ -43,6 +43,12 @@ def main():
                              plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_TILES)),
         "flat": Reducer(lay, clients, o32, o64, flags=B,
                         plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_FLAT)),
+        # the reduce's result stores temporal / sc1, so the broadcast that
+        # follows may find its source in the caches
+        "st_plain": Reducer(lay, clients, o32, o64, flags=B,
+                            plan=plan(0, _lib.FA_PLAN_TUNE_ST_PLAIN)),
+        "st_sc1": Reducer(lay, clients, o32, o64, flags=B,
+                          plan=plan(0, _lib.FA_PLAN_TUNE_ST_SC1)),
         "fused": Reducer(lay, clients, o32, o64, flags=B, plan=plan(0, F)),
         "fused_tile1024": Reducer(lay, clients, o32, o64, flags=B, plan=plan(1024, F)),
         "fused_tile2048": Reducer(lay, clients, o32, o64, flags=B, plan=plan(2048, F)),
