@@ -174,4 +174,4 @@ def test_chain_errors(lib):
     assert call(vec, 2, lib.FaChain(0, 4, None, None, P)) == lib.FA_E_INVAL   # finish too early
     assert call(vec, 3, lib.FaChain(2, 4, b.data_ptr(), None, P)) == lib.FA_E_INVAL  # > n_total
     assert call(vec, 2, lib.FaChain(0, 4, None, b.data_ptr(), 10)) == lib.FA_E_INVAL  # plane
-    assert call(vec, 1, lib.FaChain(0, 5000, None, b.data_ptr(), P)) == lib.FA_E_RANGE
+    assert call(vec, 1, lib.FaChain(0, lib.FA_MAX_CLIENTS + 1, None, b.data_ptr(), P)) == lib.FA_E_RANGE
