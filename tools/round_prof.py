@@ -1,0 +1,43 @@
+"""The cfg2 round's kernels alone, for rocprofv3 (kernel trace and the
+separate FETCH_SIZE / WRITE_SIZE passes of tools/gpu_round_pmc.sh):
+
+    python tools/round_prof.py round K   # reduce + bcast_group_kernel (FA_F_BCAST)
+    python tools/round_prof.py tgpu K    # the torch-GPU-order reduce (tgpu_kernel<0>)
+"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from feddct_amd import _lib  # noqa: E402
+from feddct_amd.layout import BucketLayout  # noqa: E402
+from feddct_amd.workload import Reducer, load_manifest, make_clients  # noqa: E402
+
+
+def main():
+    mode, k = sys.argv[1], int(sys.argv[2])
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    man = load_manifest("wrn16_8_c10")
+    lay = BucketLayout.from_manifest(man)
+    n = 20
+    cl = make_clients(lay, man, range(n), dev)
+    o32, o64 = torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])
+    if mode == "round":
+        red = Reducer(lay, cl, o32, o64, flags=_lib.FA_F_BCAST)
+    elif mode == "tgpu":
+        plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
+                         order=_lib.FA_ORDER_TORCH_GPU, n=n)
+        red = Reducer(lay, cl, o32, o64, plan=plan)
+    else:
+        raise SystemExit(f"unknown mode {mode!r}")
+    for _ in range(k):
+        red()
+    torch.cuda.synchronize()
+    print(f"{mode}: {k} launches, B = {lay.state_bytes()} bytes per client, n = {n}")
+
+
+if __name__ == "__main__":
+    main()
