@@ -689,39 +689,47 @@ __global__ __launch_bounds__(kBlock) void bcast_group_kernel(ReduceArgs args, ui
   }
 }
 
-// The flat form of the round's broadcast (tuning, FA_PLAN_TUNE_BCAST_FLAT;
-// plans cut from a segment list with FA_PLAN_GAPS_ARE_PADDING only: their
+// The flat form of the round's broadcast (the default for plans cut from a
+// segment list with FA_PLAN_GAPS_ARE_PADDING, i.e. every Python plan: their
 // buckets hold tensors and padding, so the whole fp32 bucket may be copied
-// without the tile table) — one workgroup per (1024-float part, client),
-// clients fastest, one 16-B load and one non-temporal 16-B store per lane.
-// In tools/bcastlab.hip this shape runs at the pure-fill ceiling (split_U1_G1
-// / split_rt: 130-134 us for 20 x 43.9 MB against 128-130 us of pure
-// writes; profiles/r02_bcastlab*.jsonl), but in the product, on the same box,
-// it took 168-169 us standalone and 255-265 us after the reduce, against
-// 150-170 us for bcast_group_kernel (exp_bcast, profiles/r02_exp_bcast*.jsonl)
-// — not explained yet, so it is not the default.  The int64 bucket is one
-// extra part per client.
+// without the tile table): bcast_group_kernel's shape — one workgroup per
+// (2048-float part, group of <= kBcastGroup clients), groups fastest — over
+// the flat bucket, so no workgroup waits on a tile-descriptor fetch; the
+// int64 bucket is one extra part.  cfg2 round (tools/exp_bcast.py, same
+// box, profiles/r02_exp_bcast_flatgroups.jsonl): 308.7 us against 312.4 us
+// through the tile table (FA_PLAN_TUNE_BCAST_TABLE) and 331.7 us for r01's
+// form; one client per workgroup instead: 403-407 us.
 __global__ __launch_bounds__(kBlock) void bcast_flat_kernel(ReduceArgs args, uint32_t parts,
+                                                            uint32_t groups, uint32_t gsize,
                                                             int64_t f32_numel,
                                                             int64_t i64_numel) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  const uint32_t n = (uint32_t)a.n;
-  const uint32_t total = (parts + (i64_numel > 0 ? 1u : 0u)) * n;
+  const uint32_t total = (parts + (i64_numel > 0 ? 1u : 0u)) * groups;
   const int64_t nv = f32_numel / 4;
   for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
-    const uint32_t p = v / n;
-    const int c = (int)(v - p * n);
+    const uint32_t p = v / groups;
+    const int c0 = (int)((v - p * groups) * gsize);
+    const int c1 = min(a.n, c0 + (int)gsize);
     if (p < parts) {
-      const int64_t base = (int64_t)p * (4 * kBlock);  // floats
-      float* d = const_cast<float*>(cptr32(a, c));
-      if ((int64_t)p * kBlock + threadIdx.x < nv)
-        stg4<true>(d + base, threadIdx.x, ldg4<false>(a.out32 + base, threadIdx.x));
+      const int64_t base = (int64_t)p * (8 * kBlock);  // floats
+      const int64_t v0 = (int64_t)p * 2 * kBlock + threadIdx.x, v1 = v0 + kBlock;
+      f4 r0 = {0.f, 0.f, 0.f, 0.f}, r1 = r0;
+      if (v0 < nv) r0 = ldg4<false>(a.out32 + base, threadIdx.x);
+      if (v1 < nv) r1 = ldg4<false>(a.out32 + base, threadIdx.x + kBlock);
+      for (int c = c0; c < c1; ++c) {
+        float* d = const_cast<float*>(cptr32(a, c)) + base;
+        if (v0 < nv) stg4<true>(d, threadIdx.x, r0);
+        if (v1 < nv) stg4<true>(d, threadIdx.x + kBlock, r1);
+      }
       if (p == parts - 1 && (int64_t)threadIdx.x < f32_numel - 4 * nv)
-        d[4 * nv + threadIdx.x] = a.out32[4 * nv + threadIdx.x];
+        for (int c = c0; c < c1; ++c)
+          const_cast<float*>(cptr32(a, c))[4 * nv + threadIdx.x] = a.out32[4 * nv + threadIdx.x];
     } else {
-      int64_t* d = const_cast<int64_t*>(cptr64(a, c));
-      for (int64_t e = threadIdx.x; e < i64_numel; e += kBlock) d[e] = a.out64[e];
+      for (int64_t e = threadIdx.x; e < i64_numel; e += kBlock) {
+        const int64_t r = a.out64[e];
+        for (int c = c0; c < c1; ++c) const_cast<int64_t*>(cptr64(a, c))[e] = r;
+      }
     }
   }
 }
@@ -1847,18 +1855,21 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
     a.flags |= FA_F_BCAST;
     if (plan->flags & FA_PLAN_TUNE_BCAST_TILES) {
       hipLaunchKernelGGL(bcast_tiles_kernel, dim3(ntiles), dim3(kBlock), 0, st, a);
-    } else if ((plan->flags & FA_PLAN_TUNE_BCAST_FLAT) && plan->flat_bcast && n > 0 &&
+    } else if (!(plan->flags & FA_PLAN_TUNE_BCAST_TABLE) && plan->flat_bcast && n > 0 &&
                ((plan->has32 ? plan->info.f32_numel : 0) > 0 || plan->has64)) {
       const int64_t f = plan->has32 ? plan->info.f32_numel : 0;
       const int64_t i = plan->has64 ? plan->info.i64_numel : 0;
-      const int64_t parts = f > 0 ? std::max<int64_t>(1, (f / 4 + kBlock - 1) / kBlock) : 0;
-      const int64_t total = (parts + (i > 0 ? 1 : 0)) * n;
+      const int64_t parts =
+          f > 0 ? std::max<int64_t>(1, (f / 4 + 2 * kBlock - 1) / (2 * kBlock)) : 0;
+      const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
+      const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
+      const int64_t total = (parts + (i > 0 ? 1 : 0)) * groups;
       if (total > (int64_t)UINT32_MAX) {
         e = hipErrorInvalidValue;
       } else {
         const unsigned grid = (unsigned)std::min<int64_t>(total, 1ll << 30);
         hipLaunchKernelGGL(bcast_flat_kernel, dim3(grid), dim3(kBlock), 0, st, a,
-                           (uint32_t)parts, f, i);
+                           (uint32_t)parts, groups, gsize, f, i);
       }
     } else if (n > 0 && ntiles > 0) {
       const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);

@@ -90,9 +90,10 @@ extern "C" {
 #define FA_PLAN_TUNE_ISSUE_ALL 0x100000u /* tuning: a batch's loads back to back
                                             (n <= FA_INLINE_CLIENTS, 2048-float tiles,
                                             BATCH4 or 8 clients per batch)     */
-#define FA_PLAN_TUNE_BCAST_FLAT 0x800000u /* tuning: FA_F_BCAST as a flat copy, one
-                                             workgroup per (part, client); needs
-                                             FA_PLAN_GAPS_ARE_PADDING         */
+#define FA_PLAN_TUNE_BCAST_TABLE 0x800000u /* tuning: FA_F_BCAST through the tile
+                                              table (client groups per tile) also
+                                              on gap-padded plans, which copy
+                                              their buckets flat by default    */
 #define FA_PLAN_TUNE_BCAST_TILES 0x400000u /* tuning: FA_F_BCAST as one workgroup per
                                               tile writing every client (r01 form) */
 #define FA_PLAN_TUNE_TGPU_NARROW 0x200000u /* tuning: torch-GPU order, S = 1 tensors in

@@ -1,7 +1,7 @@
 """Experiment: the round's broadcast (train_fedavg.py:148-149) — the default
-FA_F_BCAST (reduce launch + broadcast launch over client groups), one
-workgroup per tile (r01), the flat copy (one workgroup per part and client),
-the fused form
+FA_F_BCAST (reduce launch + a flat broadcast launch over client groups),
+the same groups through the tile table, one workgroup per tile (r01), the
+fused form
 (FA_PLAN_TUNE_FUSED_BCAST, under several plan tuning flags) and the reduce
 followed by the standalone whole-bucket broadcast kernel (fa_broadcast_f32; the int64
 keys, 128 B, are left out of that variant), cfg2 shape, interleaved rounds
@@ -41,8 +41,8 @@ def main():
         "default": Reducer(lay, clients, o32, o64, flags=B, plan=plan()),
         "tiles_r01": Reducer(lay, clients, o32, o64, flags=B,
                              plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_TILES)),
-        "flat": Reducer(lay, clients, o32, o64, flags=B,
-                        plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_FLAT)),
+        "table": Reducer(lay, clients, o32, o64, flags=B,
+                         plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_TABLE)),
         # the reduce's result stores temporal / sc1, so the broadcast that
         # follows may find its source in the caches
         "st_plain": Reducer(lay, clients, o32, o64, flags=B,
