@@ -1062,7 +1062,7 @@ def build_line(args, world, nbytes_rank, bytes_per_client, t_step, t_kernel, ext
                    "algorithmic_bytes_per_step": nbytes_rank * world,
                    "parallelism": (f"client shards x{world}: {extra.get('selected_mode')} "
                                    "(fastest bit-exact round form; all forms in 'modes')"
-                                   if world > 1 else "single GPU")},
+                                   if extra.get("selected_mode") else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_pmc": traffic_src,
@@ -1091,10 +1091,15 @@ def main():
                     help="rehearsal: every rank on cuda:0 (with --dist-backend gloo)")
     ap.add_argument("--kernel-only", action="store_true",
                     help="only the timed reduce launches (for rocprofv3 runs)")
+    ap.add_argument("--multi-rehearsal", action="store_true",
+                    help="run the N>1 path (every round form, native RCCL communicator "
+                         "included) with however many ranks there are, also one: a "
+                         "one-GPU rehearsal of the driver's multi-GPU command")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
+    multi = world > 1 or args.multi_rehearsal
+    if multi:
         # diagnosis only: a multi-rank run that stalls leaves every rank's
         # Python stack on stderr (nothing is interrupted)
         import faulthandler
@@ -1108,7 +1113,7 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     group = None
-    if world > 1:
+    if multi:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -1127,7 +1132,7 @@ def main():
 
     extra = {}
     ncomm = None
-    if world == 1:
+    if not multi:
         per = []
         if not args.kernel_only:
             # streaming work BEFORE the headline's own W warmups, so the
@@ -1216,7 +1221,7 @@ def main():
             line["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if multi:
         if ncomm is not None:
             ncomm.close()  # the library's communicator before torch's teardown
         dist.barrier()
