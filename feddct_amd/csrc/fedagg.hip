@@ -1596,6 +1596,7 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
   p->info.ntiles = (int32_t)t.size();
   p->info.ntiles_tail = (int32_t)t.size();
   p->flags = flags;
+  p->flat_bcast = (flags & FA_PLAN_GAPS_ARE_PADDING) != 0;
   p->order = FA_ORDER_TORCH_GPU;
   p->order_n = n;
   for (const Tile& x : t) (kind_is64(x.kind) ? p->has64 : p->has32) = true;
@@ -1725,6 +1726,41 @@ int fa_plan_get_info(const fa_plan* plan, fa_plan_info* info) {
   return FA_OK;
 }
 
+namespace {
+// The round's broadcast launch (after the reduce, over the arguments the
+// reduce used): the flat copy in client groups on gap-padded plans, client
+// groups per tile through the tile table otherwise (or with
+// FA_PLAN_TUNE_BCAST_TABLE); r01's one-workgroup-per-tile form with
+// FA_PLAN_TUNE_BCAST_TILES (CPU-order tables only: tiles_ok).
+hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, bool tiles_ok,
+                        hipStream_t st) {
+  a.flags |= FA_F_BCAST;
+  if (n <= 0) return hipSuccess;
+  const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
+  const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
+  if (tiles_ok && (plan->flags & FA_PLAN_TUNE_BCAST_TILES)) {
+    hipLaunchKernelGGL(bcast_tiles_kernel, dim3(ntiles), dim3(kBlock), 0, st, a);
+  } else if (!(plan->flags & FA_PLAN_TUNE_BCAST_TABLE) && plan->flat_bcast &&
+             ((plan->has32 ? plan->info.f32_numel : 0) > 0 || plan->has64)) {
+    const int64_t f = plan->has32 ? plan->info.f32_numel : 0;
+    const int64_t i = plan->has64 ? plan->info.i64_numel : 0;
+    const int64_t parts =
+        f > 0 ? std::max<int64_t>(1, (f / 4 + 2 * kBlock - 1) / (2 * kBlock)) : 0;
+    const int64_t total = (parts + (i > 0 ? 1 : 0)) * groups;
+    if (total > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)std::min<int64_t>(total, 1ll << 30);
+    hipLaunchKernelGGL(bcast_flat_kernel, dim3(grid), dim3(kBlock), 0, st, a, (uint32_t)parts,
+                       groups, gsize, f, i);
+  } else if (ntiles > 0) {
+    // ntiles * groups < 2^32: n clients of ntiles 4-16 KB tiles would
+    // outgrow any GPU's memory long before
+    const unsigned grid = (unsigned)std::min<int64_t>((int64_t)ntiles * groups, 1ll << 30);
+    hipLaunchKernelGGL(bcast_group_kernel, dim3(grid), dim3(kBlock), 0, st, a, groups, gsize);
+  }
+  return hipGetLastError();
+}
+}  // namespace
+
 int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const* c64, int n,
               const float* weights, float* out32, int64_t* out64, unsigned flags,
               void* stream) {
@@ -1818,15 +1854,9 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
       e = hipGetLastError();
     }
     if (e == hipSuccess && bc && plan->tg_lo[5] > 0) {
-      a.flags |= FA_F_BCAST;
       a.tiles = plan->d_tiles;
       a.ntiles = plan->tg_lo[5];
-      const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
-      const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
-      const unsigned grid =
-          (unsigned)std::min<int64_t>((int64_t)a.ntiles * groups, 1ll << 30);
-      hipLaunchKernelGGL(bcast_group_kernel, dim3(grid), dim3(kBlock), 0, st, a, groups, gsize);
-      e = hipGetLastError();
+      e = launch_bcast(plan, a, n, a.ntiles, false, st);
     }
     if (table) {
       hipError_t e2 = hipFreeAsync(table, st);
@@ -1851,36 +1881,7 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
   const bool split_bcast = (flags & FA_F_BCAST) && !(plan->flags & FA_PLAN_TUNE_FUSED_BCAST);
   if (split_bcast) a.flags &= ~FA_F_BCAST;
   hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st);
-  if (e == hipSuccess && split_bcast) {
-    a.flags |= FA_F_BCAST;
-    if (plan->flags & FA_PLAN_TUNE_BCAST_TILES) {
-      hipLaunchKernelGGL(bcast_tiles_kernel, dim3(ntiles), dim3(kBlock), 0, st, a);
-    } else if (!(plan->flags & FA_PLAN_TUNE_BCAST_TABLE) && plan->flat_bcast && n > 0 &&
-               ((plan->has32 ? plan->info.f32_numel : 0) > 0 || plan->has64)) {
-      const int64_t f = plan->has32 ? plan->info.f32_numel : 0;
-      const int64_t i = plan->has64 ? plan->info.i64_numel : 0;
-      const int64_t parts =
-          f > 0 ? std::max<int64_t>(1, (f / 4 + 2 * kBlock - 1) / (2 * kBlock)) : 0;
-      const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
-      const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
-      const int64_t total = (parts + (i > 0 ? 1 : 0)) * groups;
-      if (total > (int64_t)UINT32_MAX) {
-        e = hipErrorInvalidValue;
-      } else {
-        const unsigned grid = (unsigned)std::min<int64_t>(total, 1ll << 30);
-        hipLaunchKernelGGL(bcast_flat_kernel, dim3(grid), dim3(kBlock), 0, st, a,
-                           (uint32_t)parts, groups, gsize, f, i);
-      }
-    } else if (n > 0 && ntiles > 0) {
-      const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
-      const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
-      // ntiles * groups < 2^32: n clients of ntiles 4-16 KB tiles would
-      // outgrow any GPU's memory long before
-      const unsigned grid = (unsigned)std::min<int64_t>((int64_t)ntiles * groups, 1ll << 30);
-      hipLaunchKernelGGL(bcast_group_kernel, dim3(grid), dim3(kBlock), 0, st, a, groups, gsize);
-    }
-    if (e == hipSuccess) e = hipGetLastError();
-  }
+  if (e == hipSuccess && split_bcast) e = launch_bcast(plan, a, n, ntiles, true, st);
   if (table) {
     hipError_t e2 = hipFreeAsync(table, st);
     if (e == hipSuccess) e = e2;
