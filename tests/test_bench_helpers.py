@@ -29,3 +29,27 @@ def test_ulp_across_signed_zero():
     b = torch.tensor([-0.0, 0.0, -1.0e-45])
     h = bench.ulp_hist(a, b)
     assert h["0"] == 2 and h["2"] == 1
+
+
+def test_build_line_keeps_the_bench_contract():
+    """The one JSON line: every field the driver and the judge read, with
+    value = world x per-rank bytes / step time and the roofline from the
+    kernel time (bench contract, task ④)."""
+    import argparse
+    args = argparse.Namespace(steps=20, warmup=5)
+    nb, t_step, t_kernel = 921663624, 150e-6, 141e-6
+    line = bench.build_line(args, 2, nb, 43888744, t_step, t_kernel,
+                            {"selected_mode": "blocked/native", "cpu_baseline": None})
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["metric"] == bench.METRIC and line["unit"] == "GB/s"
+    assert line["n_gpus"] == 2 and line["steps"] == 20 and line["warmup"] == 5
+    assert abs(line["value"] - 2 * nb / t_step / 1e9) < 0.01
+    assert line["scaling"] == "weak" and line["higher_is_better"] is True
+    r = line["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == bench.HBM_PEAK_GBS
+    assert abs(r["frac"] - nb / t_kernel / 1e9 / bench.HBM_PEAK_GBS) < 1e-3
+    assert "blocked/native" in line["config"]["parallelism"]
+    assert line["config"]["algorithmic_bytes_per_step"] == 2 * nb
