@@ -702,14 +702,17 @@ __global__ __launch_bounds__(kBlock) void bcast_group_kernel(ReduceArgs args, ui
 __global__ __launch_bounds__(kBlock) void bcast_flat_kernel(ReduceArgs args, uint32_t parts,
                                                             uint32_t groups, uint32_t gsize,
                                                             int64_t f32_numel,
-                                                            int64_t i64_numel) {
+                                                            int64_t i64_numel, int reverse) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const uint32_t total = (parts + (i64_numel > 0 ? 1u : 0u)) * groups;
   const int64_t nv = f32_numel / 4;
   for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
-    const uint32_t p = v / groups;
-    const int c0 = (int)((v - p * groups) * gsize);
+    uint32_t p = v / groups;
+    // tuning (FA_PLAN_TUNE_BCAST_REVERSE): the parts in reverse order, the
+    // reduce's last-written results first
+    if (reverse && p < parts) p = parts - 1 - p;
+    const int c0 = (int)((v % groups) * gsize);
     const int c1 = min(a.n, c0 + (int)gsize);
     if (p < parts) {
       const int64_t base = (int64_t)p * (8 * kBlock);  // floats
@@ -1750,7 +1753,7 @@ hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, b
     if (total > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<int64_t>(total, 1ll << 30);
     hipLaunchKernelGGL(bcast_flat_kernel, dim3(grid), dim3(kBlock), 0, st, a, (uint32_t)parts,
-                       groups, gsize, f, i);
+                       groups, gsize, f, i, (plan->flags & FA_PLAN_TUNE_BCAST_REVERSE) ? 1 : 0);
   } else if (ntiles > 0) {
     // ntiles * groups < 2^32: n clients of ntiles 4-16 KB tiles would
     // outgrow any GPU's memory long before

@@ -94,6 +94,8 @@ extern "C" {
                                               table (client groups per tile) also
                                               on gap-padded plans, which copy
                                               their buckets flat by default    */
+#define FA_PLAN_TUNE_BCAST_REVERSE 0x1000000u /* tuning: the flat broadcast walks the
+                                                 bucket from its end            */
 #define FA_PLAN_TUNE_BCAST_TILES 0x400000u /* tuning: FA_F_BCAST as one workgroup per
                                               tile writing every client (r01 form) */
 #define FA_PLAN_TUNE_TGPU_NARROW 0x200000u /* tuning: torch-GPU order, S = 1 tensors in

@@ -43,6 +43,8 @@ def main():
                              plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_TILES)),
         "table": Reducer(lay, clients, o32, o64, flags=B,
                          plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_TABLE)),
+        "flat_reverse": Reducer(lay, clients, o32, o64, flags=B,
+                                plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_REVERSE)),
         # the reduce's result stores temporal / sc1, so the broadcast that
         # follows may find its source in the caches
         "st_plain": Reducer(lay, clients, o32, o64, flags=B,
