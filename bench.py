@@ -93,6 +93,39 @@ def launch_stats(ts):
             "last_us": round(ts[-1] * 1e6, 2), "n": len(ts)}
 
 
+ABORT_RC = 3   # exit status of a run ended by a phase deadline (never 0)
+
+
+class PhaseDeadline:
+    """``with PhaseDeadline(name, seconds, on_abort):`` — if the block is
+    still running after ``seconds`` (a collective that never completes),
+    ``on_abort(name)`` runs on a timer thread (it prints the flagged line) and
+    the process then exits with ABORT_RC, so the driver sees a failed run and
+    not a number from a hung job."""
+
+    def __init__(self, name, seconds, on_abort):
+        self.name, self.seconds, self.on_abort = name, seconds, on_abort
+
+    def _fire(self):
+        try:
+            self.on_abort(self.name)
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(ABORT_RC)
+
+    def __enter__(self):
+        import threading
+        self.timer = threading.Timer(self.seconds, self._fire)
+        self.timer.daemon = True
+        self.timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.timer.cancel()
+        return False
+
+
 def digest_of(layout, out32, out64, prefix=""):
     """SHA-256 of the keys under ``prefix`` (stripped), as tests/golden does."""
     import hashlib
@@ -871,7 +904,8 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
         completes) ends the run on every rank — each rank's own timer, same
         deadline — instead of leaving the job hung until the launcher's limit.
         Rank 0 first prints the line from the forms that finished, flagged
-        (parity unchecked, the phase named)."""
+        (parity unchecked, the phase named); PhaseDeadline then exits with
+        ABORT_RC."""
         import faulthandler
         log(f"[rank {rank}] phase '{phase}' exceeded {deadline_s:.0f} s; stacks follow")
         faulthandler.dump_traceback(all_threads=True)
@@ -890,22 +924,9 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
                 extra["selected_mode"] = best
                 print(json.dumps(build_line(args, world, nbytes_rank, layout.state_bytes(),
                                             done[best]["t"], t_kernel, extra)), flush=True)
-        sys.stderr.flush()
-        os._exit(0)
 
-    class phase:
-        def __init__(self, name):
-            self.name = name
-
-        def __enter__(self):
-            import threading
-            self.timer = threading.Timer(deadline_s, abort_run, args=(self.name,))
-            self.timer.daemon = True
-            self.timer.start()
-
-        def __exit__(self, *exc):
-            self.timer.cancel()
-            return False
+    def phase(name):
+        return PhaseDeadline(name, deadline_s, abort_run)
 
     def run_mode(name, make, root, exact_class, steps=None, warm=None):
         log(f"[rank {rank}] {name}")

@@ -27,7 +27,9 @@ are bound to pinned host buckets and staged through device buckets
 from __future__ import annotations
 
 import ctypes
+import warnings
 import weakref
+from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -57,23 +59,45 @@ class Engine:
         # order (default), or torch-ROCm's GPU one (set_summation_order)
         self.order = "torch_cpu"
         self._plans: Dict[tuple, _lib.Plan] = {}
+        # torch-GPU-order plans are cut per client count: a small LRU, so a
+        # loop whose participation varies does not grow device plans forever
+        self._gpu_plans: "OrderedDict[tuple, Optional[_lib.Plan]]" = OrderedDict()
+        self._warned_gpu_order = False
         self._layouts: Dict[tuple, BucketLayout] = {}
         self._pipes: Dict[tuple, object] = {}
 
     # ------------------------------------------------------------ caches --
+    GPU_PLAN_CACHE = 8
+
     def plan(self, layout: BucketLayout, device: torch.device, n: int = 0,
-             order: str = "torch_cpu") -> _lib.Plan:
-        gpu = order == "torch_gpu"
-        key = (layout.signature, device.index) + ((n, order) if gpu else ())
+             order: str = "torch_cpu") -> Optional[_lib.Plan]:
+        """The layout's plan on ``device``.  For the torch-GPU order, the
+        plan cut for ``n`` clients, or None when torch itself would split
+        some key across blocks there (outside the restated configurations,
+        fa_torch_gpu_config)."""
+        if order == "torch_gpu":
+            key = (layout.signature, device.index, n)
+            if key in self._gpu_plans:
+                self._gpu_plans.move_to_end(key)
+                return self._gpu_plans[key]
+            try:
+                with torch.cuda.device(device):
+                    p = _lib.Plan(layout.segs32, layout.f32_numel, layout.segs64,
+                                  layout.i64_numel, order=_lib.FA_ORDER_TORCH_GPU, n=n)
+            except _lib.FedaggError as e:
+                if "outside the restated" not in str(e):
+                    raise
+                p = None
+            self._gpu_plans[key] = p
+            while len(self._gpu_plans) > self.GPU_PLAN_CACHE:
+                self._gpu_plans.popitem(last=False)
+            return p
+        key = (layout.signature, device.index)
         p = self._plans.get(key)
         if p is None:
             with torch.cuda.device(device):
-                if gpu:   # cut for this client count (the GPU order depends on N)
-                    p = _lib.Plan(layout.segs32, layout.f32_numel, layout.segs64,
-                                  layout.i64_numel, order=_lib.FA_ORDER_TORCH_GPU, n=n)
-                else:
-                    p = _lib.Plan(layout.segs32, layout.f32_numel, layout.segs64,
-                                  layout.i64_numel)
+                p = _lib.Plan(layout.segs32, layout.f32_numel, layout.segs64,
+                              layout.i64_numel)
             self._plans[key] = p
         return p
 
@@ -189,6 +213,14 @@ class Engine:
         if order == "torch_gpu" and (weights is not None or n < 2):
             order = "torch_cpu"   # (the GPU order is torch's unweighted mean, N >= 2)
         plan = self.plan(layout, dev, n, order)
+        if plan is None:   # torch would split a key across blocks at this N
+            if not self._warned_gpu_order:
+                warnings.warn(f"feddct_amd: torch-GPU summation order is not restated for "
+                              f"N={n} on this layout (torch splits a key across blocks); "
+                              "this round uses torch's CPU order", RuntimeWarning,
+                              stacklevel=3)
+                self._warned_gpu_order = True
+            plan = self.plan(layout, dev, n, "torch_cpu")
         flags = _lib.FA_F_BCAST if fuse else 0
         a32, a64 = self._ptr_arrays(cas)
         self._launch(plan, a32, a64, n, self._weights_arg(weights, n), out32.data_ptr(),
@@ -309,7 +341,9 @@ def set_summation_order(order: str) -> None:
     BASELINE config 1 and its device-independent definition) or
     ``"torch_gpu"`` (torch-ROCm's own GPU reduction — what the reference's
     training runs computed, their models being on the GPU,
-    train_fedavg.py:244-250; unweighted rounds of N >= 2 clients).
+    train_fedavg.py:244-250; unweighted rounds of N >= 2 clients; a round
+    torch would split across thread blocks warns once and takes the CPU
+    order).
     Host-resident modules always take the CPU order, which is what the
     reference computes for them."""
     if order not in ORDERS:

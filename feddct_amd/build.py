@@ -11,6 +11,8 @@ DEPS = SRCS + [os.path.join(HERE, "csrc", "common.h"),
                os.path.join(HERE, "..", "include", "fedagg.h")]
 OUT = os.path.join(HERE, "libfedagg.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# test infrastructure (build_loopback, below)
+LOOP_DIR = os.path.join(HERE, "..", "tests", "loopback")
 
 # -ffp-contract=off: no FMA contraction anywhere (the weighted path's x*w must
 # round before the add); no -ffast-math / denormal flushing: the sum must be
@@ -76,7 +78,8 @@ def build(force: bool = False, extra=()) -> str:
         os.replace(COMM_OUT + ".tmp", COMM_OUT)
     build_shim(force)
     build_example(force)
-    build_loopback(force)
+    if os.path.isdir(LOOP_DIR):   # test infrastructure; absent when tests/ is not shipped
+        build_loopback(force, extra)
     return OUT
 
 
@@ -97,19 +100,14 @@ def build_example(force: bool = False) -> str:
     return EXAMPLE_OUT
 
 
-if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
-
-
 # Test infrastructure: the native multi-rank rounds on one GPU.  fedcomm.hip
 # compiled unchanged, linked against an in-process loopback of the RCCL
 # subset it calls (tests/loopback/loopccl.hip) instead of librccl, and a C++
 # driver (tests/loopback/loop_round.cpp) run by tests/test_gpu_loopback.py.
 # Nothing in the package links or loads these.
-LOOP_DIR = os.path.join(HERE, "..", "tests", "loopback")
 
 
-def build_loopback(force: bool = False) -> str:
+def build_loopback(force: bool = False, extra=()) -> str:
     inc = "-I" + os.path.join(HERE, "..", "include")
     ccl_src = os.path.join(LOOP_DIR, "loopccl.hip")
     ccl = os.path.join(LOOP_DIR, "libloopccl.so")
@@ -122,7 +120,7 @@ def build_loopback(force: bool = False) -> str:
                        check=True)
         os.replace(ccl + ".tmp", ccl)
     if force or _stale(comm, COMM_DEPS + [OUT, ccl]):
-        subprocess.run([HIPCC, *FLAGS, "-Wl,-soname,libfedagg_comm_loop.so", "-o", comm + ".tmp",
+        subprocess.run([HIPCC, *FLAGS, *extra, "-Wl,-soname,libfedagg_comm_loop.so", "-o", comm + ".tmp",
                         COMM_SRC, "-L" + HERE, "-lfedagg", "-L" + LOOP_DIR, "-lloopccl",
                         "-Wl,-rpath,$ORIGIN:$ORIGIN/../../feddct_amd"], check=True)
         os.replace(comm + ".tmp", comm)
@@ -133,3 +131,7 @@ def build_loopback(force: bool = False) -> str:
                         "-Wl,-rpath,$ORIGIN:$ORIGIN/../../feddct_amd"], check=True)
         os.replace(drv + ".tmp", drv)
     return drv
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

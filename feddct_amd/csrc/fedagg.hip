@@ -84,7 +84,13 @@ struct Tile {
 static_assert(sizeof(Tile) == 16, "tile is 16 B");
 
 constexpr int kBlock = 256;
-constexpr int kDefaultU = 2;  // float4 vectors per thread per client (tools/tune.py)
+constexpr int kDefaultU = 2;
+// MI355X's device properties as torch-ROCm's setReduceConfig reads them
+// (multiProcessorCount, maxThreadsPerMultiProcessor): they decide where torch
+// splits a reduction across blocks (fa_torch_gpu_config); a GPU test checks
+// them against torch.cuda.get_device_properties.
+constexpr int64_t kTorchNumCU = 256;
+constexpr int64_t kTorchMaxThreadsPerCU = 2048;  // float4 vectors per thread per client (tools/tune.py)
 
 constexpr int kInline = FA_INLINE_CLIENTS;
 
@@ -636,6 +642,30 @@ __global__ __launch_bounds__(kBlock) void bcast_tiles_kernel(ReduceArgs args) {
   }
 }
 
+// (part, client group) of broadcast block v.  xcd: the groups of one part
+// are blocks b, b + 8, b + 16, ... — one XCD under the round-robin dispatch
+// (MI355X_MICROARCH.md, workgroup dispatch; speed only, never correctness),
+// so the part is fetched into that XCD's L2 once and the other groups read
+// it there; the grid covers ceil(nparts / 8) * 8 * groups blocks (false:
+// padding).  Plain form: groups fastest on consecutive blocks, which land on
+// different XCDs — every group fetched its own copy (FETCH_SIZE 2 B at
+// N = 20 with two groups, r02).
+__device__ __forceinline__ bool bcast_part(uint32_t v, uint32_t nparts, uint32_t groups, bool xcd,
+                                           uint32_t* p, uint32_t* g) {
+  if (xcd) {
+    const uint32_t q = v / 8;
+    *g = q % groups;
+    *p = (q / groups) * 8 + v % 8;
+    return *p < nparts;
+  }
+  *p = v / groups;
+  *g = v % groups;
+  return true;
+}
+__host__ __device__ inline uint32_t bcast_blocks(uint32_t nparts, uint32_t groups, bool xcd) {
+  return (xcd ? (nparts + 7) / 8 * 8 : nparts) * groups;
+}
+
 // The round's broadcast (default since r02): one workgroup per (tile, group
 // of G consecutive clients), groups fastest, so a tile's groups run side by
 // side and its source is fetched once and then served from the caches; the
@@ -649,13 +679,14 @@ __global__ __launch_bounds__(kBlock) void bcast_tiles_kernel(ReduceArgs args) {
 // best: 130 us — not a real-data ceiling.)
 constexpr int kBcastGroup = 10;
 __global__ __launch_bounds__(kBlock) void bcast_group_kernel(ReduceArgs args, uint32_t groups,
-                                                             uint32_t gsize) {
+                                                             uint32_t gsize, int xcd) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  const uint32_t total = (uint32_t)a.ntiles * groups;
+  const uint32_t total = bcast_blocks((uint32_t)a.ntiles, groups, xcd);
   for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
-    const uint32_t ti = v / groups;
-    const int c0 = (int)((v - ti * groups) * gsize);
+    uint32_t ti, g;
+    if (!bcast_part(v, (uint32_t)a.ntiles, groups, xcd, &ti, &g)) continue;
+    const int c0 = (int)(g * gsize);
     const int c1 = min(a.n, c0 + (int)gsize);
     const Tile t = a.tiles[ti];
     const int kb = t.kind & 0xFF;
@@ -702,17 +733,20 @@ __global__ __launch_bounds__(kBlock) void bcast_group_kernel(ReduceArgs args, ui
 __global__ __launch_bounds__(kBlock) void bcast_flat_kernel(ReduceArgs args, uint32_t parts,
                                                             uint32_t groups, uint32_t gsize,
                                                             int64_t f32_numel,
-                                                            int64_t i64_numel, int reverse) {
+                                                            int64_t i64_numel, int reverse,
+                                                            int xcd) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  const uint32_t total = (parts + (i64_numel > 0 ? 1u : 0u)) * groups;
+  const uint32_t nparts = parts + (i64_numel > 0 ? 1u : 0u);
+  const uint32_t total = bcast_blocks(nparts, groups, xcd);
   const int64_t nv = f32_numel / 4;
   for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
-    uint32_t p = v / groups;
+    uint32_t p, g;
+    if (!bcast_part(v, nparts, groups, xcd, &p, &g)) continue;
     // tuning (FA_PLAN_TUNE_BCAST_REVERSE): the parts in reverse order, the
     // reduce's last-written results first
     if (reverse && p < parts) p = parts - 1 - p;
-    const int c0 = (int)((v % groups) * gsize);
+    const int c0 = (int)(g * gsize);
     const int c1 = min(a.n, c0 + (int)gsize);
     if (p < parts) {
       const int64_t base = (int64_t)p * (8 * kBlock);  // floats
@@ -899,6 +933,52 @@ __device__ __forceinline__ float tgpu_inner(const Src& src, int64_t e, int n, in
   return v;
 }
 
+// M == 1 with N >= 128: torch vectorises along the input (setReduceConfig's
+// "vectorize along input": dim0 = N / 4 >= 32), so the block is bw =
+// last_pow2(N / 4) (at most 512) threads; thread x sums the 4-element
+// vectors x, x+bw, ... into 4 accumulators, one per vector component, then
+// the <= 3 trailing rows N - N%4 + x into accumulator 0, and combines
+// ((v0 + v1) + v2) + v3 (input_vectorized_thread_reduce_impl).  The threads
+// meet in block_x_reduce: the shared-memory halving tree for offsets bw/2
+// down to 64, then the intra-wave tree with increasing offsets.  One wave per
+// element here: lane l plays threads l + 64 j (j < bw / 64), and the halving
+// over j is the shared-memory tree.
+template <class Src>
+__device__ __forceinline__ float tgpu_inner_vec(const Src& src, int64_t e, int n, int bw,
+                                                int lane) {
+  const int J = bw >= 64 ? bw / 64 : 1;
+  const int tail = n - n % 4;
+  float t[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    t[j] = 0.f;
+    const int x = lane + 64 * j;
+    if (j >= J || x >= bw) continue;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    for (int q = x; 4 * q + 3 < n; q += bw) {
+      v0 = __fadd_rn(v0, src(4 * q, e));
+      v1 = __fadd_rn(v1, src(4 * q + 1, e));
+      v2 = __fadd_rn(v2, src(4 * q + 2, e));
+      v3 = __fadd_rn(v3, src(4 * q + 3, e));
+    }
+    if (tail + x < n) v0 = __fadd_rn(v0, src(tail + x, e));
+    t[j] = __fadd_rn(__fadd_rn(__fadd_rn(v0, v1), v2), v3);
+  }
+  if (J >= 8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t[j] = __fadd_rn(t[j], t[j + 4]);
+  }
+  if (J >= 4) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) t[j] = __fadd_rn(t[j], t[j + 2]);
+  }
+  if (J >= 2) t[0] = __fadd_rn(t[0], t[1]);
+  float v = t[0];
+  const int dx = bw >= 64 ? 64 : bw;
+  for (int off = 1; off < dx; off <<= 1) v = __fadd_rn(v, __shfl_down(v, off, 64));
+  return v;
+}
+
 // One instantiation per row split S = 1 << LS (the plan groups its tiles by
 // S and launches each group): a single S per kernel keeps the register
 // budget of the parts' values to that S (a runtime switch over S = 1..16 in
@@ -955,8 +1035,10 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   if (w >= t.count) return;
   const int64_t e = t.start + w;
   const int bw = 1 << ls;
+  const bool vec = (t.kind >> 16) & 1;   // N >= 128: input-vectorised form
   if (base == K_F32_TGPU_IN) {
-    const float s = tgpu_inner(SrcF32{a, false}, e, n, bw, lane);
+    const float s = vec ? tgpu_inner_vec(SrcF32{a, false}, e, n, bw, lane)
+                        : tgpu_inner(SrcF32{a, false}, e, n, bw, lane);
     if (lane == 0) {
       const float r = sum_only ? s : __fmul_rn(s, fac);
       a.out32[e] = r;
@@ -964,7 +1046,8 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
         for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
     }
   } else {
-    const float s = tgpu_inner(SrcI64{a}, e, n, bw, lane);
+    const float s = vec ? tgpu_inner_vec(SrcI64{a}, e, n, bw, lane)
+                        : tgpu_inner(SrcI64{a}, e, n, bw, lane);
     if (lane == 0) {
       const int64_t r = (int64_t)__fmul_rn(s, fac);
       a.out64[e] = r;
@@ -990,10 +1073,11 @@ __global__ __launch_bounds__(kBlock) void bcast_kernel(BcastArgs a, int64_t nume
                                                        uint32_t parts, uint32_t groups,
                                                        uint32_t gsize) {
   const int64_t nv = numel / 4;
-  const uint32_t total = parts * groups;
+  const uint32_t total = bcast_blocks(parts, groups, true);
   for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
-    const uint32_t p = v / groups;
-    const int c0 = (int)((v - p * groups) * gsize);
+    uint32_t p, g;
+    if (!bcast_part(v, parts, groups, true, &p, &g)) continue;
+    const int c0 = (int)(g * gsize);
     const int c1 = min(a.n, c0 + (int)gsize);
     const int64_t v0 = (int64_t)p * 2 * kBlock + threadIdx.x, v1 = v0 + kBlock;
     f4 r0 = {0.f, 0.f, 0.f, 0.f}, r1 = r0;
@@ -1147,6 +1231,28 @@ int check_segs(const fa_seg* s, int ns, int64_t numel, const char* what,
     if (g.numel > 0) end = g.offset + g.numel;
   }
   return FA_OK;
+}
+
+// May the broadcast copy the buckets flat?  Only when the caller declared the
+// gaps padding (FA_PLAN_GAPS_ARE_PADDING) AND the segments, with that
+// padding, cover the whole bucket: no gap (leading, between, trailing) of
+// `pad` elements or more, i.e. no room for a key the plan does not own.  A
+// plan over some of a layout's keys (a column chunk) keeps the tile-table
+// broadcast, which writes its own tiles only.
+bool covers_with_padding(const std::vector<fa_seg>& s, int64_t numel, int64_t pad) {
+  int64_t pos = 0;
+  for (const fa_seg& g : s) {
+    if (g.numel == 0) continue;
+    if (g.offset - pos >= pad) return false;
+    pos = g.offset + g.numel;
+  }
+  return numel - pos < pad;
+}
+
+bool flat_bcast_ok(unsigned flags, const std::vector<fa_seg>& s32, int64_t f32_numel,
+                   const std::vector<fa_seg>& s64, int64_t i64_numel) {
+  return (flags & FA_PLAN_GAPS_ARE_PADDING) && covers_with_padding(s32, f32_numel, 64) &&
+         covers_with_padding(s64, i64_numel, 1);
 }
 
 // Every element belongs to at most one tile: two tiles over one element would
@@ -1438,7 +1544,7 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   p->info.tile_elems = tile_elems;
   p->vec_u = tile_elems / (4 * kBlock);
   p->flags = flags;
-  p->flat_bcast = (flags & FA_PLAN_GAPS_ARE_PADDING) != 0;
+  p->flat_bcast = flat_bcast_ok(flags, s32, f32_numel, s64, i64_numel);
   std::vector<Tile> tiles, alt;
   rc = build_tiles(s32, s64, tile_elems, flags, &tiles, &p->info);
   if (rc) {
@@ -1484,20 +1590,44 @@ int fa_torch_gpu_config(int n, int64_t m, int* stride) {
     while (p * 2 <= v) p *= 2;
     return p;
   };
+  auto div_up = [](int64_t a, int64_t b) { return (a + b - 1) / b; };
   int64_t S;
   if (m == 1) {
-    if (n >= 128) return 0;  // (torch vectorises the input there)
-    S = last_pow2(n);
+    // a 0-dim key stacked to [N]: lanes over the N values; from N >= 128 on
+    // torch vectorises the input (tgpu_inner_vec), and N <= FA_MAX_CLIENTS
+    // keeps values per thread below the cross-block threshold (N / 512 <
+    // 256).  `stride` is the block width.
+    S = n < 128 ? last_pow2(n) : std::min<int64_t>(last_pow2(n / 4), 512);
   } else {
+    // setReduceConfig, "vectorize along output" ([N, M] reduced over dim 0,
+    // iter.ndim() == 2), set_block_dimension with MAX_NUM_THREADS 512
     const int64_t ovs = m % 4 == 0 ? 4 : (m % 2 == 0 ? 2 : 1);
     const int64_t mnt = 512 / ovs, dim0 = m / ovs;
     const int64_t d0 = dim0 < mnt ? last_pow2(dim0) : mnt;
     const int64_t d1 = n < mnt ? last_pow2(n) : mnt;
-    int64_t bw = std::min<int64_t>(d0, 64);
-    const int64_t bh = std::min<int64_t>(d1, mnt / bw);
+    const int64_t bw0 = std::min<int64_t>(d0, 64);
+    const int64_t bh = std::min<int64_t>(d1, mnt / bw0);
+    const int64_t bw = std::min<int64_t>(d0, mnt / bh);
     const bool split = n >= std::min<int64_t>(bh * 16, 256);
     S = split ? bh : 1;
-    if ((n + S - 1) / S >= 256 || S > 16) return 0;  // cross-block split / kernel limit
+    if (S > 16) return 0;  // kernel limit (tgpu_kernel<LS>, LS <= 4)
+    const int64_t vpt = div_up(n, S);
+    if (split && vpt >= 256) {
+      // the cross-block ("global") split: only when the output grid is
+      // small against the target grid (kTorchNumCU CUs; max threads per CU
+      // 256 for a 2-D iterator, the device's own for a single block —
+      // ROCm's `uses_a_single_block` reads grid.x == 1)
+      const int64_t grid = div_up(dim0, bw);
+      const int64_t tpm = grid == 1 ? kTorchMaxThreadsPerCU : 256;
+      const int64_t target = kTorchNumCU * (tpm / (bw * bh));
+      if (grid <= target) {
+        int64_t c = std::max(std::min(div_up(target, grid), div_up(vpt, 16)), div_up(vpt, 256));
+        if (c > kTorchNumCU) c = kTorchNumCU;
+        else if (c > div_up(kTorchNumCU, 2)) c = div_up(kTorchNumCU, 2);
+        else if (c < 16) c = 1;
+        if (c > 1) return 0;  // global_reduce: not restated
+      }
+    }
   }
   if (stride) *stride = (int)S;
   return 1;
@@ -1535,7 +1665,8 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
       // torch's factor: float(num_outputs) / numel, in float
       const float f = (float)g.numel / (float)((int64_t)n * g.numel);
       if (g.numel == 1) {
-        t.push_back(Tile{g.offset, 1, (pass ? K_I64_TGPU_IN : K_F32_TGPU_IN) | (ls << 8)});
+        const int vec = n >= 128 ? 1 << 16 : 0;  // input-vectorised (tgpu_inner_vec)
+        t.push_back(Tile{g.offset, 1, (pass ? K_I64_TGPU_IN : K_F32_TGPU_IN) | (ls << 8) | vec});
         fac.push_back(f);
         continue;
       }
@@ -1599,7 +1730,7 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
   p->info.ntiles = (int32_t)t.size();
   p->info.ntiles_tail = (int32_t)t.size();
   p->flags = flags;
-  p->flat_bcast = (flags & FA_PLAN_GAPS_ARE_PADDING) != 0;
+  p->flat_bcast = flat_bcast_ok(flags, s32, f32_numel, s64, i64_numel);
   p->order = FA_ORDER_TORCH_GPU;
   p->order_n = n;
   for (const Tile& x : t) (kind_is64(x.kind) ? p->has64 : p->has32) = true;
@@ -1749,16 +1880,22 @@ hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, b
     const int64_t i = plan->has64 ? plan->info.i64_numel : 0;
     const int64_t parts =
         f > 0 ? std::max<int64_t>(1, (f / 4 + 2 * kBlock - 1) / (2 * kBlock)) : 0;
-    const int64_t total = (parts + (i > 0 ? 1 : 0)) * groups;
-    if (total > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
+    const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_NOXCD) ? 0 : 1;
+    const int64_t np = parts + (i > 0 ? 1 : 0);
+    if ((np + 8) * groups > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
+    const int64_t total = bcast_blocks((uint32_t)np, groups, xcd);
     const unsigned grid = (unsigned)std::min<int64_t>(total, 1ll << 30);
     hipLaunchKernelGGL(bcast_flat_kernel, dim3(grid), dim3(kBlock), 0, st, a, (uint32_t)parts,
-                       groups, gsize, f, i, (plan->flags & FA_PLAN_TUNE_BCAST_REVERSE) ? 1 : 0);
+                       groups, gsize, f, i, (plan->flags & FA_PLAN_TUNE_BCAST_REVERSE) ? 1 : 0,
+                       xcd);
   } else if (ntiles > 0) {
     // ntiles * groups < 2^32: n clients of ntiles 4-16 KB tiles would
     // outgrow any GPU's memory long before
-    const unsigned grid = (unsigned)std::min<int64_t>((int64_t)ntiles * groups, 1ll << 30);
-    hipLaunchKernelGGL(bcast_group_kernel, dim3(grid), dim3(kBlock), 0, st, a, groups, gsize);
+    const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_NOXCD) ? 0 : 1;
+    const unsigned grid =
+        (unsigned)std::min<int64_t>(bcast_blocks((uint32_t)ntiles, groups, xcd), 1ll << 30);
+    hipLaunchKernelGGL(bcast_group_kernel, dim3(grid), dim3(kBlock), 0, st, a, groups, gsize,
+                       xcd);
   }
   return hipGetLastError();
 }
@@ -2057,9 +2194,10 @@ int fa_broadcast_f32(const float* src, float* const* dst, int n, int64_t numel, 
     const int64_t parts = std::max<int64_t>(1, (numel / 4 + 2 * kBlock - 1) / (2 * kBlock));
     const uint32_t groups = (uint32_t)((a.n + kBcastGroup - 1) / kBcastGroup);
     const uint32_t gsize = (uint32_t)((a.n + groups - 1) / groups);
-    if (parts * groups > (int64_t)UINT32_MAX)
+    if ((parts + 8) * groups > (int64_t)UINT32_MAX)
       return set_err(FA_E_RANGE, "fa_broadcast_f32: numel=%lld", (long long)numel);
-    const unsigned grid = (unsigned)std::min<int64_t>(parts * groups, 1ll << 30);
+    const unsigned grid =
+        (unsigned)std::min<int64_t>(bcast_blocks((uint32_t)parts, groups, true), 1ll << 30);
     hipLaunchKernelGGL(bcast_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a, numel,
                        (uint32_t)parts, groups, gsize);
     HIP_TRY(hipGetLastError());

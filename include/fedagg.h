@@ -71,11 +71,18 @@ extern "C" {
 #define FA_INLINE_CLIENTS 128
 
 /* fa_reduce flags */
-#define FA_F_BCAST 1u    /* also write the result into every client bucket  */
+#define FA_F_BCAST 1u    /* also write the result into every client bucket:
+                            the plan's tiles (a second launch); a plan whose
+                            segments cover the whole bucket up to padding
+                            (FA_PLAN_GAPS_ARE_PADDING, no gap of >= 64 fp32 /
+                            >= 1 int64 elements) copies [0, f32_numel) and
+                            [0, i64_numel) flat instead                    */
 #define FA_F_SUM_ONLY 2u /* fp32 keys: write the ordered sum, skip the /N   */
 
 /* Plan-build flags */
-#define FA_PLAN_GAPS_ARE_PADDING 1u /* bytes between segments may be written */
+#define FA_PLAN_GAPS_ARE_PADDING 1u /* bytes between segments may be written
+                                       (vector runs span them); with full
+                                       coverage also FA_F_BCAST's flat copy */
 #define FA_PLAN_TUNE_NO_NT 2u       /* tuning: plain (temporal) loads/stores   */
 #define FA_PLAN_TUNE_BATCH8 4u     /* tuning: force 8 clients per load batch  */
 #define FA_PLAN_TUNE_BATCH16 8u    /* tuning: force 16 clients per load batch */
@@ -96,6 +103,9 @@ extern "C" {
                                               their buckets flat by default    */
 #define FA_PLAN_TUNE_BCAST_REVERSE 0x1000000u /* tuning: the flat broadcast walks the
                                                  bucket from its end            */
+#define FA_PLAN_TUNE_BCAST_NOXCD 0x2000000u /* tuning: the flat broadcast's client
+                                                groups of a part on consecutive
+                                                blocks (r02 form) instead of one XCD */
 #define FA_PLAN_TUNE_BCAST_TILES 0x400000u /* tuning: FA_F_BCAST as one workgroup per
                                               tile writing every client (r01 form) */
 #define FA_PLAN_TUNE_TGPU_NARROW 0x200000u /* tuning: torch-GPU order, S = 1 tensors in
@@ -180,7 +190,8 @@ int fa_plan_create_order(const fa_seg *seg32, int nseg32, int64_t f32_numel,
                          int n, int order, unsigned flags, fa_plan **out);
 
 /* The hot path: every key of N client buckets -> global bucket, one launch
- * (FA_F_BCAST: plus one broadcast launch over the same tiles).
+ * (FA_F_BCAST: plus one broadcast launch — over the same tiles, or the flat
+ * bucket copy when the plan covers the whole bucket, see FA_F_BCAST).
  *   c32[i] / c64[i]  : client i's fp32 / int64 bucket (slot order 0..n-1)
  *   weights          : NULL -> mean (sum / n);  else fp32 w[i], result =
  *                      ordered sum of fp32(x_i * w_i) (no division)

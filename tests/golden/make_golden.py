@@ -117,6 +117,72 @@ def build_models(ref):
     return out
 
 
+# The reference's other FedDCT sweep layouts (r03; VERDICT r02 missing 1):
+# (arch, split_factor, num_selected) from the launch scripts, all CIFAR-100:
+#   script/feddct_wrn168_split{2,8,16,32}_cifar100_96clients_96choose_650rounds.sh:27
+#   script/feddct_resnet110_split4_cifar100_100clients_100choose_650rounds.sh:27  (N=25)
+#   script/feddct_resnet110_split4_cifar100_80clients_80choose_650rounds.sh       (N=20)
+SWEEP = [("wide_resnetsl16_8", "wrnsl16_8", 2, 48), ("wide_resnetsl16_8", "wrnsl16_8", 8, 12),
+         ("wide_resnetsl16_8", "wrnsl16_8", 16, 6), ("wide_resnetsl16_8", "wrnsl16_8", 32, 3),
+         ("resnet110sl", "resnet110sl", 4, 25), ("resnet110sl", "resnet110sl", 4, 20)]
+
+
+def sweep_name(tag, sf):
+    return f"{tag}_sf{sf}_c100"
+
+
+def build_sweep_models(ref):
+    norm = ref["norm"]
+    out = {}
+    for arch, tag, sf, _ in SWEEP:
+        b = ref_args(ref, ["--arch", arch, "--split_factor", str(sf), "--dataset", "cifar100",
+                           "--num_classes", "100"])
+        name = sweep_name(tag, sf)
+        out[name + "_main"] = lambda b=b: ref["splitnetsl"].SplitNetMainClient(
+            b, norm_layer=norm.norm(b.norm_mode), criterion=None)
+        out[name + "_proxy"] = lambda b=b: ref["splitnetsl"].SplitNetProxyClient(
+            b, norm_layer=norm.norm(b.norm_mode), criterion=None)
+    return out
+
+
+def sweep_digests():
+    """Manifests + reference FedDCT digests for SWEEP (merged into
+    digests.json; the existing entries are left as they are)."""
+    ref = import_reference()
+    torch.set_num_threads(8)
+    torch.manual_seed(0)
+    builders = build_sweep_models(ref)
+    man_dir = os.path.join(REPO, "feddct_amd", "manifests")
+    manifests = {}
+    for name, mk in builders.items():
+        m = manifest_of(name, mk())
+        manifests[name] = m
+        with open(os.path.join(man_dir, name + ".json"), "w") as f:
+            json.dump(m, f, indent=0)
+        print(name, len(m["keys"]), "keys", flush=True)
+    path = os.path.join(REPO, "tests", "golden", "digests.json")
+    with open(path) as f:
+        digests = json.load(f)
+    for _, tag, sf, n in SWEEP:
+        lm, lp = sweep_name(tag, sf) + "_main", sweep_name(tag, sf) + "_proxy"
+        if f"feddct/{lp}/n{n}" in digests:
+            continue
+        gm, gp = builders[lm](), builders[lp]()
+        ms = [builders[lm]() for _ in range(n)]
+        ps = [builders[lp]() for _ in range(n)]
+        for i in range(n):
+            fill_module(ms[i], manifests[lm], i, synth.MODE_REALISTIC)
+            fill_module(ps[i], manifests[lp], i, synth.MODE_REALISTIC)
+        ref["feddct"].server_aggregate(gm, gp, ms, ps)
+        digests[f"feddct/{lm}/n{n}"] = state_digest(gm)
+        digests[f"feddct/{lp}/n{n}"] = state_digest(gp)
+        print("feddct", lm, n, digests[f"feddct/{lm}/n{n}"], digests[f"feddct/{lp}/n{n}"],
+              flush=True)
+        del gm, gp, ms, ps
+        with open(path, "w") as f:   # after every case: a long run keeps what it has
+            json.dump(digests, f, indent=1)
+
+
 def manifest_of(name, module):
     keys = []
     for k, v in module.state_dict().items():
@@ -261,4 +327,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--sweep"]:
+        sweep_digests()
+    else:
+        main()

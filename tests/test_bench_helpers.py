@@ -31,6 +31,25 @@ def test_ulp_across_signed_zero():
     assert h["0"] == 2 and h["2"] == 1
 
 
+def test_phase_deadline_exits_nonzero_with_the_flagged_line():
+    """A phase that outlives its deadline prints the flagged line and ends
+    the process with a non-zero status (it used to exit 0)."""
+    import subprocess
+    code = ("import sys, time; sys.path.insert(0, %r); import bench\n"
+            "with bench.PhaseDeadline('xchg', 1.0, lambda p: print('{\"aborted\": \"%%s\"}' %% p)):\n"
+            "    time.sleep(30)\n" % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == bench.ABORT_RC != 0
+    assert '{"aborted": "xchg"}' in r.stdout
+
+
+def test_phase_deadline_cancelled_when_the_phase_finishes():
+    with bench.PhaseDeadline("ok", 0.5, lambda p: None):
+        pass
+    import time
+    time.sleep(0.8)   # the timer would have fired (and exited) by now
+
+
 def test_build_line_keeps_the_bench_contract():
     """The one JSON line: every field the driver and the judge read, with
     value = world x per-rank bytes / step time and the roofline from the

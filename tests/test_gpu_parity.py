@@ -207,6 +207,42 @@ def test_sum_only_and_bcast_flags(lib):
             assert bits_equal(a, b), k
 
 
+@pytest.mark.parametrize("which", ["middle", "head", "tail", "i64_subset"])
+def test_bcast_of_a_partial_plan_leaves_other_keys_alone(lib, which):
+    """FA_F_BCAST on a gap-padded plan over SOME of a layout's
+    keys (a column chunk) must write only that plan's keys into the clients;
+    the flat bucket copy is for plans that cover the whole bucket."""
+    from feddct_amd._lib import FA_F_BCAST
+    n = 5
+    man = _rand_manifest(None, [100, 4096, 7, 3000, 1, 64])
+    man["keys"].append({"key": "nbt2", "shape": [], "dtype": "int64"})
+    layout = BucketLayout.from_manifest(man)
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    bk = states_to_buckets(layout, states, DEV)
+    before = [(f.clone(), i.clone()) for f, i in bk]
+    s32, s64 = layout.segs32, layout.segs64
+    own = {"middle": [0, 2, 4, 5], "head": [0, 1, 2], "tail": [3, 4, 5]}.get(which)
+    segs32 = s32 if own is None else s32[own]
+    segs64 = s64[:1] if which == "i64_subset" else s64
+    plan = lib.Plan(segs32, layout.f32_numel, segs64, layout.i64_numel)
+    out32 = torch.zeros_like(bk[0][0])
+    out64 = torch.zeros_like(bk[0][1])
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    lib.check(lib.lib.fa_reduce(plan.handle, lib.ptr_array([b[0].data_ptr() for b in bk]),
+                                lib.ptr_array([b[1].data_ptr() for b in bk]), n, None,
+                                out32.data_ptr(), out64.data_ptr(), FA_F_BCAST, s))
+    torch.cuda.synchronize()
+    mine32 = {(int(o), int(m)) for o, m in segs32}
+    mine64 = {(int(o), int(m)) for o, m in segs64}
+    for (f, i), (f0, i0) in zip(bk, before):
+        for o, m in s32:
+            want = out32 if (int(o), int(m)) in mine32 else f0
+            assert torch.equal(f[o:o + m], want[o:o + m]), (which, o)
+        for o, m in s64:
+            want = out64 if (int(o), int(m)) in mine64 else i0
+            assert torch.equal(i[o:o + m], want[o:o + m]), (which, o)
+
+
 def test_int64_adversarial(lib):
     man = {"keys": [{"key": f"i{j}", "shape": s, "dtype": "int64"}
                     for j, s in enumerate([[], [1], [3], [9], [40], [300]])]}

@@ -37,6 +37,21 @@ def _torch_gpu_mean(rows):
 
 SHAPES = [(n, m) for n in (2, 3, 5, 8, 9, 16, 17, 20, 24, 31, 32, 33, 64, 100, 127, 200)
           for m in (1, 2, 3, 5, 10, 16, 17, 100, 432, 1000, 4096, 2 ** 16 + 4)]
+# r03: 0-dim keys past N = 128 (torch vectorises the input), and many rows
+# per thread without a cross-block split (large outputs: N = 512 ... 1000)
+SHAPES += [(n, 1) for n in (128, 129, 130, 131, 255, 256, 257, 511, 512, 1000, 2047, 2048,
+                            2051, 5000, 8192, 20001)]
+SHAPES += [(n, m) for n in (300, 512, 600) for m in (2 ** 16, 2 ** 18 + 4, 2 ** 18 + 2)]
+SHAPES += [(1000, 2 ** 16), (1100, 2 ** 18 + 2)]
+
+
+def test_device_properties_are_the_restated_ones():
+    """setReduceConfig's cross-block decision reads the CU count and the
+    threads per CU; the restatement (oracle) and fa_torch_gpu_config assume
+    MI355X's."""
+    p = torch.cuda.get_device_properties(DEV)
+    assert p.multi_processor_count == G.NUM_CU
+    assert p.max_threads_per_multi_processor == G.MAX_THREADS_PER_CU
 
 
 @pytest.mark.parametrize("n,m", [s for s in SHAPES if G.supported(*s)])
@@ -78,6 +93,52 @@ def _vs_torch(layout, buckets, out32, out64):
         if not ok:
             bad.append(s.key)
     return bad
+
+
+# Row-split layouts: every M here reaches a row split S
+# = 2, 4, 8 or 16 at some of the client counts below (S = bh, torch's block
+# height, once N >= min(16 bh, 256)); 0-dim keys run the lane tree, from
+# N = 128 on in the input-vectorised form.
+SPLIT_MS = [1, 2, 3, 6, 16, 36, 64, 100, 128, 160, 200, 256, 1024, 4097, 65536, 300000]
+SPLIT_NS = [32, 48, 64, 100, 127, 128, 200, 256, 300]
+
+
+def _split_manifest():
+    keys = [{"key": f"t{j}", "shape": [m] if m > 1 else [], "dtype": "float32"}
+            for j, m in enumerate(SPLIT_MS)]
+    keys.append({"key": "nbt", "shape": [], "dtype": "int64"})
+    return {"keys": keys}
+
+
+def test_row_split_layout_reaches_every_split():
+    """The parametrised kernel test below covers S = 1, 2, 4, 8 and 16."""
+    from feddct_amd import _lib
+    seen = set()
+    for n in SPLIT_NS:
+        for m in SPLIT_MS:
+            st = ctypes.c_int(0)
+            if m > 1 and _lib.lib.fa_torch_gpu_config(n, m, ctypes.byref(st)):
+                seen.add(st.value)
+    assert {1, 2, 4, 8, 16} <= seen, seen
+
+
+@pytest.mark.parametrize("n", SPLIT_NS)
+def test_row_split_kernels_match_torch_gpu_mean(lib, n):
+    """tgpu_kernel<LS> for every row split the layout reaches at this N, bit
+    for bit against torch-ROCm's own cuda mean of every key (keys torch
+    would split across blocks, or S > 16, are skipped — see the config)."""
+    man = _split_manifest()
+    keep = []
+    for e in man["keys"]:
+        m = int(np.prod(e["shape"])) if e["shape"] else 1
+        if lib.lib.fa_torch_gpu_config(n, m, None):
+            keep.append(e)
+    man = {"keys": keep}
+    layout = BucketLayout.from_manifest(man)
+    from feddct_amd.workload import make_clients
+    cl = make_clients(layout, man, range(n), DEV, mode=synth.MODE_ADVERSARIAL)
+    out32, out64 = _gpu_order_reduce(lib, layout, cl)
+    assert _vs_torch(layout, cl, out32, out64) == []
 
 
 @pytest.mark.parametrize("case", ["cfg2", "cfg3", "cfg5", "small_adversarial"])
@@ -129,7 +190,107 @@ def test_gpu_order_broadcast_and_errors(lib):
             assert torch.equal(src[sl.offset:sl.offset + sl.numel],
                                res[sl.offset:sl.offset + sl.numel])
     with pytest.raises(lib.FedaggError, match="outside the restated"):
-        lib.Plan(np.array([[0, 64]]), 64, order=lib.FA_ORDER_TORCH_GPU, n=4000)
+        lib.Plan(np.array([[0, 4096]]), 4096, order=lib.FA_ORDER_TORCH_GPU, n=4000)
+
+
+def _dropin_vs_reference_loop(man, n, mode=synth.MODE_ADVERSARIAL, expect_warning=False):
+    import copy
+    import warnings
+    import feddct_amd
+    from feddct_amd.fedavg import server_aggregate
+    from helpers import StateModule
+    from oracle.torch_mirror import reference_loop
+    states = [synth.gen_state(man, i, mode) for i in range(n)]
+    mods = [StateModule(man).load_numpy(s).to(DEV) for s in states]
+    ref_g, ref_c = StateModule(man).to(DEV), [copy.deepcopy(m) for m in mods]
+    reference_loop(ref_g, ref_c)
+    feddct_amd.set_summation_order("torch_gpu")
+    try:
+        g = StateModule(man).to(DEV)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            server_aggregate(g, mods)
+        torch.cuda.synchronize()
+    finally:
+        feddct_amd.set_summation_order("torch_cpu")
+    warned = any("not restated" in str(x.message) for x in w)
+    assert warned == expect_warning
+    return g, mods, ref_g, ref_c, states
+
+
+@pytest.mark.parametrize("n", [48, 128, 200])
+def test_dropin_gpu_order_many_clients(n):
+    """a BN model (0-dim num_batches_tracked keys) at N >= 128 in
+    the torch-GPU order used to raise inside the training loop; now it is
+    restated (input-vectorised lane order) and bit-exact vs the reference
+    loop on GPU modules.  N = 48 is the sf2 script's slot count."""
+    man = {"keys": [{"key": "conv.weight", "shape": [64, 16, 3, 3], "dtype": "float32"},
+                    {"key": "bn.weight", "shape": [64], "dtype": "float32"},
+                    {"key": "bn.running_mean", "shape": [64], "dtype": "float32"},
+                    {"key": "bn.num_batches_tracked", "shape": [], "dtype": "int64"},
+                    {"key": "fc.weight", "shape": [100, 256], "dtype": "float32"},
+                    {"key": "fc.bias", "shape": [100], "dtype": "float32"}]}
+    g, mods, ref_g, ref_c, _ = _dropin_vs_reference_loop(man, n)
+    for k, v in ref_g.state_dict().items():
+        a, b = g.state_dict()[k], v
+        if v.dtype == torch.float32:
+            a, b = a.view(torch.int32), b.view(torch.int32)
+        assert torch.equal(a, b), k
+        assert torch.equal(mods[-1].state_dict()[k], ref_c[-1].state_dict()[k]), k
+
+
+def test_dropin_gpu_order_outside_restatement_warns_and_uses_cpu_order():
+    """A 4096-element key at N = 600: torch splits it across blocks
+    (global_reduce, not restated) -> one RuntimeWarning, and the round is
+    torch's CPU order, bit for bit (oracle)."""
+    man = {"keys": [{"key": "w", "shape": [4096], "dtype": "float32"},
+                    {"key": "nbt", "shape": [], "dtype": "int64"}]}
+    g, mods, _, _, states = _dropin_vs_reference_loop(man, 600, expect_warning=True)
+    from oracle.torch_order import aggregate_state
+    for k, want in aggregate_state(states):
+        assert g.state_dict()[k].cpu().numpy().tobytes() == np.asarray(want).tobytes(), k
+
+
+def test_dropin_gpu_order_sf2_proxy_layout_n48():
+    """the drop-in at N = 48 on the wrnsl16_8 sf2 proxy
+    layout (script/feddct_wrn168_split2_cifar100_96clients_96choose_650rounds
+    .sh:27) — its large tensors take the S = 2 row split — against the
+    reference loop run on GPU modules, global and clients bit for bit."""
+    import copy
+    import feddct_amd
+    from feddct_amd.fedavg import server_aggregate
+    from helpers import StateModule
+    from oracle.torch_mirror import reference_loop
+    from test_gpu_sweep import _fill_module
+    from feddct_amd import _lib
+    man = load_manifest("wrnsl16_8_sf2_c100_proxy")
+    n = 48
+    splits = set()
+    for e in man["keys"]:
+        st = ctypes.c_int(0)
+        m = int(np.prod(e["shape"])) if e["shape"] else 1
+        assert _lib.lib.fa_torch_gpu_config(n, m, ctypes.byref(st)), e["key"]
+        if m > 1:
+            splits.add(st.value)
+    assert 2 in splits, splits
+    mods = [StateModule(man).to(DEV) for _ in range(n)]
+    for i, mo in enumerate(mods):
+        _fill_module(_lib, mo, man, i)
+    ref_g, ref_c = StateModule(man).to(DEV), [copy.deepcopy(m) for m in mods]
+    reference_loop(ref_g, ref_c)
+    feddct_amd.set_summation_order("torch_gpu")
+    try:
+        g = StateModule(man).to(DEV)
+        server_aggregate(g, mods)
+        torch.cuda.synchronize()
+    finally:
+        feddct_amd.set_summation_order("torch_cpu")
+    for k, v in ref_g.state_dict().items():
+        a, b = g.state_dict()[k], v
+        if v.dtype == torch.float32:
+            a, b = a.view(torch.int32), b.view(torch.int32)
+        assert torch.equal(a, b), k
+        assert torch.equal(mods[7].state_dict()[k], ref_c[7].state_dict()[k]), k
 
 
 @pytest.mark.parametrize("n", [2, 5, 20, 24])
