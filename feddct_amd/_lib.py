@@ -30,6 +30,7 @@ FA_MAX_CLIENTS = 65536
 FA_INLINE_CLIENTS = 128
 FA_F_BCAST = 1
 FA_F_SUM_ONLY = 2
+FA_F_BCAST_ONLY = 4
 FA_PLAN_GAPS_ARE_PADDING = 1
 FA_PLAN_TUNE_NO_NT = 2
 FA_PLAN_TUNE_BATCH8 = 4

@@ -6,9 +6,14 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRCS = [os.path.join(HERE, "csrc", f) for f in ("fedagg.hip", "prox.hip")]
-DEPS = SRCS + [os.path.join(HERE, "csrc", "common.h"),
-               os.path.join(HERE, "..", "include", "fedagg.h")]
+# fedagg_k*.hip: the reduce kernel variants, split over units that compile
+# in parallel (one unit held them all: 5 minutes of device compilation)
+SRCS = [os.path.join(HERE, "csrc", f) for f in
+        ("fedagg.hip", "fedagg_k1a.hip", "fedagg_k1b.hip", "fedagg_k2a.hip", "fedagg_k2b.hip",
+         "fedagg_k2c.hip", "fedagg_k2d.hip", "fedagg_k4a.hip", "fedagg_k4b.hip", "prox.hip")]
+HEADERS = [os.path.join(HERE, "csrc", "common.h"), os.path.join(HERE, "csrc", "reduce_impl.h"),
+           os.path.join(HERE, "..", "include", "fedagg.h")]
+DEPS = SRCS + HEADERS
 OUT = os.path.join(HERE, "libfedagg.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # test infrastructure (build_loopback, below)
@@ -66,9 +71,32 @@ def _stale(out, deps):
                                                                    for d in deps)
 
 
+def _compile_units(srcs, flags, jobs=None, force=False):
+    """hipcc -c of every stale unit (older than its source or a shared
+    header), several at once; returns the object paths."""
+    objdir = os.path.join(HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
+    jobs = jobs or min(len(srcs), int(os.environ.get("MAX_JOBS", "0")) or os.cpu_count() or 4, 16)
+    cflags = [f for f in flags if f not in ("-shared",)]
+    objs, procs = [], []
+    for src in srcs:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if not force and not _stale(obj, [src] + HEADERS):
+            continue
+        while len([p for p in procs if p.poll() is None]) >= jobs:
+            procs[[p.poll() is None for p in procs].index(True)].wait()
+        procs.append(subprocess.Popen([HIPCC, *cflags, "-c", "-o", obj, src]))
+    bad = [p.args[-1] for p in procs if p.wait() != 0]
+    if bad:
+        raise subprocess.CalledProcessError(1, f"hipcc -c {bad}")
+    return objs
+
+
 def build(force: bool = False, extra=()) -> str:
     if force or _stale(OUT, DEPS):
-        cmd = [HIPCC, *FLAGS, *extra, "-Wl,-soname,libfedagg.so", "-o", OUT + ".tmp", *SRCS]
+        objs = _compile_units(SRCS, [*FLAGS, *extra], force=force or bool(extra))
+        cmd = [HIPCC, *FLAGS, *extra, "-Wl,-soname,libfedagg.so", "-o", OUT + ".tmp", *objs]
         subprocess.run(cmd, check=True)
         os.replace(OUT + ".tmp", OUT)
     if force or _stale(COMM_OUT, COMM_DEPS + [OUT]):

@@ -1,0 +1,8 @@
+// fedagg_k1b.hip — reduce_kernel instantiations of libfedagg.so (see
+// reduce_impl.h): one share of the (U, B) launcher set, compiled in
+// parallel with the other units.
+#include "reduce_impl.h"
+
+FA_K_LAUNCH_U(, 1, 8)
+FA_K_LAUNCH_U(, 1, 16)
+FA_K_LAUNCH_CHAIN(, 1, 8)

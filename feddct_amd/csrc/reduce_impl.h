@@ -1,0 +1,614 @@
+// reduce_impl.h — the reduce kernel family of libfedagg.so (torch's CPU
+// summation order over flat client buckets, fedagg.hip's header comment) and
+// its launchers.  Shared by fedagg.hip (plans, C ABI, every other kernel)
+// and the fedagg_k*.hip translation units, which instantiate the launcher
+// templates for disjoint (tile width U, client batch B) sets so hipcc builds
+// the ~100 reduce_kernel variants in parallel; fedagg.hip declares those
+// instantiations extern.  Every kernel instance is compiled in exactly one
+// translation unit (its launches are made from there).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.h"
+
+namespace fa_k {
+
+// ----------------------------------------------------------------- tiles --
+enum TileKind : int32_t {
+  K_F32_VEC = 0,      // cascade order, 16-B vectors, count % 4 == 0
+  K_F32_CASC_S = 1,   // cascade order, one element per thread (unaligned)
+  K_F32_ILP4 = 2,     // tail columns: ILP-4 order
+  K_F32_INNER = 3,    // M == 1: ILP-4 (n < 8) or 8-lane inner (n >= 8)
+  K_I64_CASC = 4,
+  K_I64_ILP4 = 5,
+  K_I64_INNER = 6,
+  // torch-ROCm's GPU order (fa_plan_create_order, FA_ORDER_TORCH_GPU); the
+  // tile's kind carries log2 of its stride in bits 8-15
+  K_F32_TGPU = 7,     // [N, M>=2]: S-way row split, 4 round-robin accumulators
+  K_I64_TGPU = 8,
+  K_F32_TGPU_IN = 9,  // M == 1: lane split + intra-wave shuffle tree, 1 element/wave
+  K_I64_TGPU_IN = 10,
+  K_F32_TGPU_V = 11,  // [N, M>=2], 16-B aligned run: 4 elements per lane, up to 1024
+  K_F32_TGPU_W = 12,  // the same with S = 1: 8 elements per lane (2 x 16 B), up to 2048
+};
+
+__host__ __device__ inline bool kind_is64(int kind) {
+  const int b = kind & 0xFF;
+  return b == K_I64_CASC || b == K_I64_ILP4 || b == K_I64_INNER || b == K_I64_TGPU ||
+         b == K_I64_TGPU_IN;
+}
+
+struct Tile {
+  int64_t start;  // first element (bucket index)
+  int32_t count;  // elements
+  int32_t kind;
+};
+static_assert(sizeof(Tile) == 16, "tile is 16 B");
+
+constexpr int kBlock = 256;
+constexpr int kDefaultU = 2;
+// MI355X's device properties as torch-ROCm's setReduceConfig reads them
+// (multiProcessorCount, maxThreadsPerMultiProcessor): they decide where torch
+// splits a reduction across blocks (fa_torch_gpu_config); a GPU test checks
+// them against torch.cuda.get_device_properties.
+constexpr int64_t kTorchNumCU = 256;
+constexpr int64_t kTorchMaxThreadsPerCU = 2048;  // float4 vectors per thread per client (tools/tune.py)
+
+constexpr int kInline = FA_INLINE_CLIENTS;
+
+// Client pointer tables travel inline in the kernel arguments for
+// n <= kInline (the common case: no setup copy at all); beyond that they sit
+// in a stream-ordered device allocation (tab32/tab64/tabw).
+struct ReduceArgs {
+  const Tile* tiles;
+  float* out32;
+  int64_t* out64;
+  int n;
+  unsigned flags;
+  int ntiles;   // tiles in the table (== grid)
+  int nscalar;  // leading scalar tiles
+  int xcd_swz;  // tuning: give each XCD a contiguous range of vector tiles
+  // The cascade's position (fa_reduce_chain; a plain reduction is row0 = 0,
+  // n_total = n): these clients are rows row0 .. row0+n-1 of an n_total-row
+  // reduction.  The level accumulators start from st_in's planes (bit l of
+  // lev_in: plane l at st_in + l*plane; others +0) and, with st_out, end
+  // there (bit l of lev_out) instead of being finished into out32.
+  int n_total;
+  int row0;
+  int lev_in;
+  int lev_out;
+  const float* st_in;
+  float* st_out;
+  int64_t plane;
+  const float* tfac;  // torch-GPU order: per-tile mean factor fl(M)/fl(N*M)
+  const float* const* tab32;
+  const int64_t* const* tab64;
+  const float* tabw;
+  const float* c32[kInline];
+  const int64_t* c64[kInline];
+  float w[kInline];
+};
+
+// The kernel reads its arguments through this constant-address-space view of
+// the kernarg segment.  Binding a by-value struct parameter to a reference
+// instead makes the compiler copy the whole 2.6 KB struct into per-lane
+// scratch (measured: 7x slower); the kernarg view keeps every pointer fetch a
+// scalar load.
+typedef __attribute__((address_space(4))) const ReduceArgs KArgs;
+
+__device__ __forceinline__ const float* cptr32(KArgs& a, int i) {
+  return a.n <= kInline ? a.c32[i] : a.tab32[i];
+}
+__device__ __forceinline__ const int64_t* cptr64(KArgs& a, int i) {
+  return a.n <= kInline ? a.c64[i] : a.tab64[i];
+}
+__device__ __forceinline__ float cw(KArgs& a, int i) {
+  return a.n <= kInline ? a.w[i] : a.tabw[i];
+}
+
+// Pointer source of the vector path.  TAB (the DEEP kernels, n >= 256): the
+// device table through a constant-address-space view (read-only for the
+// launch), so a uniform index is one scalar load: 2-10 % faster at 300
+// clients than generic loads (2 % slower at 200, hence only from 256 on).
+// Otherwise the runtime-selecting accessor above.  Measured
+// (tools/exp_ab.py, same box, one process): compiled this way the inline
+// kernel issues each client's U loads behind a vmcnt(0) wait and runs
+// 141-146 us on the cfg2 workload; reading a.c32[i] directly lets the
+// compiler issue the whole batch's loads back to back, which is 4-6 %
+// SLOWER (148-156 us) at every batch size tried (1, 4, 8, 16 clients).
+typedef const float* f32p;
+#define FA_CONST __attribute__((address_space(4)))
+template <bool TAB>
+__device__ __forceinline__ const float* vptr32(KArgs& a, int i) {
+  if constexpr (TAB) return ((const FA_CONST f32p*)a.tab32)[i];
+  else return cptr32(a, i);
+}
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// The weights of clients b0..b0+nb-1, read once per batch BEFORE its data
+// loads are issued, through scalar loads only (kernarg array, or the device
+// table through the constant address space: read-only for the launch).
+// Reading each weight in the add phase instead put a load round trip and a
+// vmcnt/lgkmcnt(0) wait between consecutive clients' adds (the weighted
+// kernel ran 4-6 % behind the mean, r02 profiles).
+template <int NB>
+__device__ __forceinline__ void load_weights(KArgs& a, int b0, int nb, float (&wb)[NB]) {
+  if (a.n <= kInline) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) wb[b] = b < nb ? a.w[b0 + b] : 0.f;
+  } else {
+    const FA_CONST float* t = (const FA_CONST float*)a.tabw;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) wb[b] = b < nb ? t[b0 + b] : 0.f;
+  }
+}
+
+constexpr unsigned kWaveContig = 0x200u;  // internal a.flags bit (FA_PLAN_TUNE_WAVE_CONTIG)
+
+// c10::utils::CeilLog2 / ATen multi_row_sum level power
+__host__ __device__ inline int ceil_log2_i(int64_t n) {
+  if (n <= 1) return 0;
+  int r = 0;
+  uint64_t v = (uint64_t)(n - 1);
+  while (v) { ++r; v >>= 1; }
+  return r;
+}
+__host__ __device__ inline int level_power(int64_t n) {
+  int c = ceil_log2_i(n) / 4;
+  return c > 4 ? c : 4;
+}
+
+__device__ __forceinline__ f4 add4(f4 a, f4 b) {
+  return f4{__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y), __fadd_rn(a.z, b.z),
+            __fadd_rn(a.w, b.w)};
+}
+__device__ __forceinline__ f4 mul4s(f4 a, float s) {
+  return f4{__fmul_rn(a.x, s), __fmul_rn(a.y, s), __fmul_rn(a.z, s),
+            __fmul_rn(a.w, s)};
+}
+__device__ __forceinline__ f4 div4s(f4 a, float s) {
+  return f4{__fdiv_rn(a.x, s), __fdiv_rn(a.y, s), __fdiv_rn(a.z, s),
+            __fdiv_rn(a.w, s)};
+}
+
+// Global-address-space views: loads/stores compile to global_* (not flat_*)
+// instructions; with a uniform base and a 32-bit vector index they take the
+// SGPR-base + one-VGPR-offset form, so a batch of B clients costs no 64-bit
+// per-lane address arithmetic and no address VGPRs.
+typedef __attribute__((address_space(1))) const f4 gcf4;
+typedef __attribute__((address_space(1))) f4 gf4;
+
+template <bool NT>
+__device__ __forceinline__ f4 ldg4(const float* base, uint32_t vidx) {
+  gcf4* g = (gcf4*)base;
+  if constexpr (NT) return __builtin_nontemporal_load(g + vidx);
+  else return g[vidx];
+}
+template <bool NT>
+__device__ __forceinline__ void stg4(float* base, uint32_t vidx, f4 v) {
+  gf4* g = (gf4*)base;
+  if constexpr (NT) __builtin_nontemporal_store(v, g + vidx);
+  else g[vidx] = v;
+}
+template <bool NT>
+__device__ __forceinline__ f4 ld4(const float* p) {
+  return ldg4<NT>(p, 0);
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, f4 v) {
+  stg4<NT>(p, 0, v);
+}
+
+// Result store of a vector tile.  POL bit 2: through a buffer op with the
+// sc1 cache-policy bit (explicit aux bits: 2 = nt, 16 = sc1) instead of the
+// global nt store; the descriptor is based at the tile start (uniform).
+template <int POL>
+__device__ __forceinline__ void st_out(float* out, int64_t start, uint32_t vidx, f4 v) {
+  if constexpr ((POL & 4) != 0) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(out + start, (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(16 * vidx), 0, (POL & 2) ? 18 : 16);
+  } else {
+    stg4<(POL & 2) != 0>(out + start, vidx, v);
+  }
+}
+
+// -------------------------------------------------- vectorised cascade ----
+// ATen multi_row_sum over the n clients for 4*U columns per thread.  The
+// loop over clients is uniform (scalar control).  Clients go in batches of B:
+// the batch's B pointers come in as one scalar load, all B*U 16-B loads are
+// issued, then the adds run in client order with the block promotion after
+// every full block of 2^lp rows (lp = 4 for n < 2^20).
+template <int U, bool DEEP>
+struct Acc {
+  f4 l0[U], l1[U], l2[U], l3[U];
+};
+
+template <int U, bool DEEP>
+__device__ __forceinline__ void promote(Acc<U, DEEP>& A, int ii, int lp, int mask) {
+  if ((ii & mask) != 0) return;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    A.l1[u] = add4(A.l1[u], A.l0[u]);
+    A.l0[u] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  if constexpr (DEEP) {
+    if ((ii & (mask << lp)) != 0) return;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      A.l2[u] = add4(A.l2[u], A.l1[u]);
+      A.l1[u] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    if ((ii & (mask << (2 * lp))) != 0) return;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      A.l3[u] = add4(A.l3[u], A.l2[u]);
+      A.l2[u] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// One batch of NB clients starting at b0.  FULL: every lane's U vectors are
+// inside the tile (no per-lane predicate).
+template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool TAB>
+__device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t start,
+                                      const uint32_t (&vi)[U], const bool (&ok)[U],
+                                      int lp, int mask, int r0) {
+  f4 x[NB][U];
+  float wb[NB];
+  if constexpr (WEIGHTED) load_weights<NB>(a, b0, NB, wb);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const float* p = bptr<TAB, POL>(a, b0 + b) + start;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
+      else x[b][u] = ok[u] ? ldg4<(POL & 1) != 0>(p, vi[u]) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f4 v = x[b][u];
+      if constexpr (WEIGHTED) v = mul4s(v, wb[b]);
+      A.l0[u] = add4(A.l0[u], v);
+    }
+    promote<U, DEEP>(A, r0 + b0 + b + 1, lp, mask);
+  }
+}
+
+// Pointer source of a batch's loads.  POL bit 3 (tuning, n <= the inline
+// count only): the kernarg pointer array read directly, which lets the
+// compiler issue the whole batch's loads back to back instead of one
+// client's loads behind a vmcnt(0) wait (slower at N = 20, r01; swept for
+// small N, r02).
+template <bool TAB, int POL>
+__device__ __forceinline__ const float* bptr(KArgs& a, int i) {
+  if constexpr ((POL & 8) != 0) return a.c32[i];
+  else return vptr32<TAB>(a, i);
+}
+
+// The last, partial batch (nb < NB clients): same issue-all-then-add shape,
+// every step guarded by a uniform (scalar) branch.
+template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool TAB>
+__device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, int nb,
+                                           int64_t start, const uint32_t (&vi)[U],
+                                           const bool (&ok)[U], int lp, int mask, int r0) {
+  f4 x[NB][U];
+  float wb[NB];
+  if constexpr (WEIGHTED) load_weights<NB>(a, b0, nb, wb);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b < nb) {
+      const float* p = bptr<TAB, POL>(a, b0 + b) + start;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
+        else x[b][u] = ok[u] ? ldg4<(POL & 1) != 0>(p, vi[u]) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b < nb) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        f4 v = x[b][u];
+        if constexpr (WEIGHTED) v = mul4s(v, wb[b]);
+        A.l0[u] = add4(A.l0[u], v);
+      }
+      promote<U, DEEP>(A, r0 + b0 + b + 1, lp, mask);
+    }
+  }
+}
+
+template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool CHAIN>
+__device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
+                                         int count) {
+  // TAB: the DEEP kernels' constant-space pointer table; a chain segment may
+  // be DEEP (n_total >= 256) with few local clients, so it takes the
+  // runtime-selected pointer source instead
+  constexpr bool TAB = DEEP && !CHAIN;
+  const int n = a.n;
+  const int nt = CHAIN ? a.n_total : n;
+  const int r0 = CHAIN ? a.row0 : 0;
+  const int lp = level_power(nt);
+  const int mask = (1 << lp) - 1;
+  Acc<U, DEEP> A;
+  uint32_t vi[U];
+  bool ok[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    // block-strided (default): lane t takes vectors t, t+256, ...; wave-
+    // contiguous (tuning flag): each wave owns U*1 KiB of adjacent bytes
+    const int v = (a.flags & kWaveContig)
+                      ? (int)(threadIdx.x & ~63u) * U + u * 64 + (int)(threadIdx.x & 63u)
+                      : (int)threadIdx.x + u * kBlock;
+    vi[u] = (uint32_t)v;
+    ok[u] = FULL || 4 * v < count;
+    A.l0[u] = A.l1[u] = A.l2[u] = A.l3[u] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  if constexpr (CHAIN) {
+    // the state after rows 0..row0-1 (levels outside lev_in are +0, exactly
+    // what the cascade holds there after its promotions)
+    if (a.st_in) {
+      const int li = a.lev_in;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        if (li & 1) A.l0[u] = ldg4<true>(a.st_in + start, vi[u]);
+        if (li & 2) A.l1[u] = ldg4<true>(a.st_in + a.plane + start, vi[u]);
+        if constexpr (DEEP) {
+          if (li & 4) A.l2[u] = ldg4<true>(a.st_in + 2 * a.plane + start, vi[u]);
+          if (li & 8) A.l3[u] = ldg4<true>(a.st_in + 3 * a.plane + start, vi[u]);
+        }
+      }
+    }
+  }
+  int b0 = 0;
+  for (; b0 + B <= n; b0 += B)
+    batch<U, B, FULL, DEEP, WEIGHTED, POL, TAB>(a, A, b0, start, vi, ok, lp, mask, r0);
+  if (b0 < n)
+    batch_tail<U, B, FULL, DEEP, WEIGHTED, POL, TAB>(a, A, b0, n - b0, start, vi, ok, lp, mask,
+                                                     r0);
+  if constexpr (CHAIN) {
+    if (a.st_out) {
+      const int lo = a.lev_out;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        if (lo & 1) stg4<true>(a.st_out + start, vi[u], A.l0[u]);
+        if (lo & 2) stg4<true>(a.st_out + a.plane + start, vi[u], A.l1[u]);
+        if constexpr (DEEP) {
+          if (lo & 4) stg4<true>(a.st_out + 2 * a.plane + start, vi[u], A.l2[u]);
+          if (lo & 8) stg4<true>(a.st_out + 3 * a.plane + start, vi[u], A.l3[u]);
+        }
+      }
+      return;
+    }
+  }
+
+  const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
+  const float fn = (float)nt;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!ok[u]) continue;
+    // acc2/acc3 stay +0 unless DEEP; x + (+0) == x for every x a +0-seeded
+    // round-to-nearest sum can produce (never -0), so skipping them is exact.
+    f4 s = add4(A.l0[u], A.l1[u]);
+    if constexpr (DEEP) {
+      s = add4(s, A.l2[u]);
+      s = add4(s, A.l3[u]);
+    }
+    const f4 r = sum_only ? s : div4s(s, fn);
+    st_out<POL>(a.out32, start, vi[u], r);
+    if (!CHAIN && (a.flags & FA_F_BCAST)) {
+      for (int i = 0; i < n; ++i)
+        stg4<(POL & 2) != 0>(const_cast<float*>(vptr32<TAB>(a, i)) + start, vi[u], r);
+    }
+  }
+}
+
+// ------------------------------------------------------- scalar orders ----
+struct SrcF32 {
+  KArgs& a;
+  bool weighted;
+  __device__ float operator()(int i, int64_t e) const {
+    float x = cptr32(a, i)[e];
+    return weighted ? __fmul_rn(x, cw(a, i)) : x;
+  }
+};
+struct SrcI64 {
+  KArgs& a;
+  __device__ float operator()(int i, int64_t e) const {
+    return (float)cptr64(a, i)[e];  // .float(): int64 -> fp32, round to nearest
+  }
+};
+
+// multi_row_sum over rows first, first+stride, ... (count rows), 1 column.
+// The four level accumulators are named variables (a runtime-indexed array
+// would live in scratch).
+template <class Src>
+__device__ float cascade_seq(const Src& src, int64_t e, int first, int stride,
+                             int count) {
+  const int lp = level_power(count);
+  const int step = 1 << lp, mask = step - 1;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int i = 0;
+  for (; i + step <= count;) {
+    for (int j = 0; j < step; ++j, ++i) a0 = __fadd_rn(a0, src(first + i * stride, e));
+    a1 = __fadd_rn(a1, a0);
+    a0 = 0.f;
+    if (i & (mask << lp)) continue;
+    a2 = __fadd_rn(a2, a1);
+    a1 = 0.f;
+    if (i & (mask << (2 * lp))) continue;
+    a3 = __fadd_rn(a3, a2);
+    a2 = 0.f;
+  }
+  for (; i < count; ++i) a0 = __fadd_rn(a0, src(first + i * stride, e));
+  a0 = __fadd_rn(a0, a1);
+  a0 = __fadd_rn(a0, a2);
+  return __fadd_rn(a0, a3);
+}
+
+// ATen row_sum: ILP-4 over rows first + k*stride (count rows).
+template <class Src>
+__device__ float ilp4_seq(const Src& src, int64_t e, int first, int stride,
+                          int count) {
+  const int q = count / 4;
+  float p0 = cascade_seq(src, e, first, 4 * stride, q);
+  const float p1 = cascade_seq(src, e, first + stride, 4 * stride, q);
+  const float p2 = cascade_seq(src, e, first + 2 * stride, 4 * stride, q);
+  const float p3 = cascade_seq(src, e, first + 3 * stride, 4 * stride, q);
+  for (int i = 4 * q; i < count; ++i) p0 = __fadd_rn(p0, src(first + i * stride, e));
+  p0 = __fadd_rn(p0, p1);
+  p0 = __fadd_rn(p0, p2);
+  return __fadd_rn(p0, p3);
+}
+
+// ATen vectorized_inner_sum (M == 1, n >= 8): 8 lanes, each an ILP-4 over
+// the n/8 vectors; scalar tail into a fresh +0; then lanes 0..7 in order.
+template <class Src>
+__device__ float inner_seq(const Src& src, int64_t e, int n) {
+  if (n < 8) return ilp4_seq(src, e, 0, 1, n);
+  const int nv = n / 8;
+  float fin = 0.f;
+  for (int k = 8 * nv; k < n; ++k) fin = __fadd_rn(fin, src(k, e));
+  for (int l = 0; l < 8; ++l) fin = __fadd_rn(fin, ilp4_seq(src, e, l, 8, nv));
+  return fin;
+}
+
+template <bool WEIGHTED>
+__device__ void tile_scalar(KArgs& a, Tile t) {
+  const int j = threadIdx.x;
+  if (j >= t.count) return;
+  const int64_t e = t.start + j;
+  const int n = a.n;
+  const float fn = (float)n;
+  if (t.kind <= K_F32_INNER) {
+    SrcF32 src{a, WEIGHTED};
+    float s;
+    if (t.kind == K_F32_CASC_S) s = cascade_seq(src, e, 0, 1, n);
+    else if (t.kind == K_F32_ILP4) s = ilp4_seq(src, e, 0, 1, n);
+    else s = inner_seq(src, e, n);
+    s = __fadd_rn(0.f, s);  // sum_out: out (=+0) += value
+    const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
+    const float r = sum_only ? s : __fdiv_rn(s, fn);
+    a.out32[e] = r;
+    if (a.flags & FA_F_BCAST)
+      for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
+  } else {
+    SrcI64 src{a};
+    float s;
+    if (t.kind == K_I64_CASC) s = cascade_seq(src, e, 0, 1, n);
+    else if (t.kind == K_I64_ILP4) s = ilp4_seq(src, e, 0, 1, n);
+    else s = inner_seq(src, e, n);
+    s = __fadd_rn(0.f, s);
+    // load_state_dict copy_: fp32 -> int64 truncates toward zero
+    const int64_t r = (int64_t)__fdiv_rn(s, fn);
+    a.out64[e] = r;
+    if (a.flags & FA_F_BCAST)
+      for (int i = 0; i < n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
+  }
+}
+
+template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN>
+__device__ __forceinline__ void run_tile(KArgs& a, int ti) {
+  if (a.xcd_swz && ti >= a.nscalar) {
+    // bijective: blocks i and i+8 share an XCD (round-robin dispatch); XCD x
+    // gets the contiguous tile range [x*q + min(x,r), ...) of the vector tiles
+    const int i = ti - a.nscalar, nv = a.ntiles - a.nscalar;
+    const int q = nv / 8, r = nv % 8, x = i % 8, j = i / 8;
+    ti = a.nscalar + x * q + min(x, r) + j;
+  }
+  const Tile t = a.tiles[ti];
+  if (t.kind == K_F32_VEC) {
+    if (t.count == 4 * U * kBlock)
+      tile_vec<U, B, true, DEEP, WEIGHTED, POL, CHAIN>(a, t.start, t.count);
+    else
+      tile_vec<U, B, false, DEEP, WEIGHTED, POL, CHAIN>(a, t.start, t.count);
+  } else if (!CHAIN) {
+    tile_scalar<WEIGHTED>(a, t);
+  }
+}
+
+// One workgroup per tile (default), or a persistent grid walking the table
+// with stride gridDim.x (tuning: FA_PLAN_TUNE_PERSIST).
+template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN = false>
+__global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs args) {
+  (void)args;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  if ((int)gridDim.x >= a.ntiles) {
+    run_tile<U, B, DEEP, WEIGHTED, POL, CHAIN>(a, blockIdx.x);
+  } else {
+    for (int ti = blockIdx.x; ti < a.ntiles; ti += gridDim.x) {
+      run_tile<U, B, DEEP, WEIGHTED, POL, CHAIN>(a, ti);
+      __syncthreads();  // scalar tiles exit threads early; keep the block in step
+    }
+  }
+}
+
+// --------------------------------------------------------------- launches --
+// tuning state of the calling thread (defined in fedagg.hip): occupancy cap
+// through dynamic LDS, persistent grid size
+extern thread_local size_t t_dyn_lds;
+extern thread_local int t_grid_cap;
+
+template <int U, int B, bool DEEP, bool W, int POL, bool CHAIN = false>
+hipError_t launch_one(const ReduceArgs& a, int ntiles, hipStream_t st) {
+  const int grid = (t_grid_cap > 0 && t_grid_cap < ntiles) ? t_grid_cap : ntiles;
+  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, POL, CHAIN>), dim3(grid), dim3(kBlock),
+                     t_dyn_lds, st, a);
+  return hipGetLastError();
+}
+
+// Chain segments (fa_reduce_chain): default cache policy, the plan's tile
+// width, 16-client batches for unweighted segments of >= 16 clients.
+template <int U, int B>
+hipError_t launch_chain_ub(const ReduceArgs& a, int ntiles, bool deep, bool w, hipStream_t st) {
+  if (deep) return w ? launch_one<U, B, true, true, 3, true>(a, ntiles, st)
+                     : launch_one<U, B, true, false, 3, true>(a, ntiles, st);
+  return w ? launch_one<U, B, false, true, 3, true>(a, ntiles, st)
+           : launch_one<U, B, false, false, 3, true>(a, ntiles, st);
+}
+template <int U, int B>
+hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, int pol, hipStream_t st) {
+  // pol: bit 0 = non-temporal loads, bit 1 = non-temporal stores (default 3),
+  // bit 2 = result stores with sc1 (buffer op)
+  if (deep) return w ? launch_one<U, B, true, true, 3>(a, ntiles, st)
+                     : launch_one<U, B, true, false, 3>(a, ntiles, st);
+  if (w) return pol == 3 ? launch_one<U, B, false, true, 3>(a, ntiles, st)
+                         : launch_one<U, B, false, true, 0>(a, ntiles, st);
+  switch (pol) {
+    case 5: return launch_one<U, B, false, false, 5>(a, ntiles, st);
+    case 7: return launch_one<U, B, false, false, 7>(a, ntiles, st);
+    case 0: return launch_one<U, B, false, false, 0>(a, ntiles, st);
+    case 1: return launch_one<U, B, false, false, 1>(a, ntiles, st);
+    case 2: return launch_one<U, B, false, false, 2>(a, ntiles, st);
+    default: return launch_one<U, B, false, false, 3>(a, ntiles, st);
+  }
+}
+
+
+}  // namespace fa_k
+
+// The (U, B) launcher instantiations, each in one fedagg_k*.hip unit.
+#define FA_K_LAUNCH_U(EXT, U, B)                                                      \
+  EXT template hipError_t fa_k::launch_u<U, B>(const fa_k::ReduceArgs&, int, bool, bool, int, \
+                                                hipStream_t);
+#define FA_K_LAUNCH_CHAIN(EXT, U, B)                                                          \
+  EXT template hipError_t fa_k::launch_chain_ub<U, B>(const fa_k::ReduceArgs&, int, bool, bool, \
+                                                       hipStream_t);
+#define FA_K_UNITS(EXT)                                                                  \
+  FA_K_LAUNCH_U(EXT, 1, 1) FA_K_LAUNCH_U(EXT, 1, 4) FA_K_LAUNCH_U(EXT, 1, 8)            \
+  FA_K_LAUNCH_U(EXT, 1, 16) FA_K_LAUNCH_CHAIN(EXT, 1, 8)                                 \
+  FA_K_LAUNCH_U(EXT, 2, 1) FA_K_LAUNCH_U(EXT, 2, 4)                                      \
+  FA_K_LAUNCH_U(EXT, 2, 8) FA_K_LAUNCH_CHAIN(EXT, 2, 8)                                  \
+  FA_K_LAUNCH_U(EXT, 2, 16) FA_K_LAUNCH_CHAIN(EXT, 2, 16)                                \
+  FA_K_LAUNCH_U(EXT, 4, 1) FA_K_LAUNCH_U(EXT, 4, 4) FA_K_LAUNCH_U(EXT, 4, 8)             \
+  FA_K_LAUNCH_CHAIN(EXT, 4, 8)

@@ -78,6 +78,9 @@ extern "C" {
                             >= 1 int64 elements) copies [0, f32_numel) and
                             [0, i64_numel) flat instead                    */
 #define FA_F_SUM_ONLY 2u /* fp32 keys: write the ordered sum, skip the /N   */
+#define FA_F_BCAST_ONLY 4u /* no reduction: out32 / out64 (the global state)
+                              written into every client bucket, as
+                              FA_F_BCAST's launch (weights ignored)       */
 
 /* Plan-build flags */
 #define FA_PLAN_GAPS_ARE_PADDING 1u /* bytes between segments may be written
@@ -196,7 +199,7 @@ int fa_plan_create_order(const fa_seg *seg32, int nseg32, int64_t f32_numel,
  *   weights          : NULL -> mean (sum / n);  else fp32 w[i], result =
  *                      ordered sum of fp32(x_i * w_i) (no division)
  *   out32 / out64    : global buckets (may alias a client bucket)
- *   flags            : FA_F_BCAST | FA_F_SUM_ONLY
+ *   flags            : FA_F_BCAST | FA_F_SUM_ONLY, or FA_F_BCAST_ONLY
  * int64 keys always take the mean + truncation path (weights ignored). */
 int fa_reduce(const fa_plan *plan, const float *const *c32,
               const int64_t *const *c64, int n, const float *weights,

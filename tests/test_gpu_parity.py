@@ -243,6 +243,44 @@ def test_bcast_of_a_partial_plan_leaves_other_keys_alone(lib, which):
             assert torch.equal(i[o:o + m], want[o:o + m]), (which, o)
 
 
+@pytest.mark.parametrize("n", [1, 7, 20, 21, 300])
+@pytest.mark.parametrize("form", ["flat", "flat_noxcd", "table", "table_noxcd", "tgpu"])
+def test_broadcast_forms_and_bcast_only(lib, n, form):
+    """Every broadcast form writes the global state into every client —
+    FA_F_BCAST after the reduce and FA_F_BCAST_ONLY alone (the reference's
+    initial sync, train_fedavg.py:244-250) — with XCD-paired client groups
+    (default, r03) and r02's consecutive groups, client counts that leave a
+    short last group, and part counts that are not a multiple of 8."""
+    from feddct_amd._lib import FA_F_BCAST, FA_F_BCAST_ONLY
+    man = _rand_manifest(None, [100, 4096, 7, 3000, 1, 64, 20000])
+    layout = BucketLayout.from_manifest(man)
+    states = [synth.gen_state(man, i % 9, synth.MODE_ADVERSARIAL) for i in range(n)]
+    fl = lib.FA_PLAN_GAPS_ARE_PADDING
+    if form.startswith("table"):
+        fl |= lib.FA_PLAN_TUNE_BCAST_TABLE
+    if form.endswith("noxcd"):
+        fl |= lib.FA_PLAN_TUNE_BCAST_NOXCD
+    kw = dict(order=lib.FA_ORDER_TORCH_GPU, n=n) if form == "tgpu" else {}
+    if form == "tgpu" and n < 2:
+        pytest.skip("the torch-GPU order needs N >= 2")
+    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
+                    flags=fl, **kw)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for flag in (FA_F_BCAST, FA_F_BCAST_ONLY):
+        bk = states_to_buckets(layout, states, DEV)
+        g32 = torch.randn_like(bk[0][0])
+        g64 = torch.randint_like(bk[0][1], -1000, 1000)
+        lib.check(lib.lib.fa_reduce(plan.handle, lib.ptr_array([b[0].data_ptr() for b in bk]),
+                                    lib.ptr_array([b[1].data_ptr() for b in bk]), n, None,
+                                    g32.data_ptr(), g64.data_ptr(), flag, s))
+        torch.cuda.synchronize()
+        for f, i in bk:
+            for o, m in layout.segs32:
+                assert torch.equal(f[o:o + m].view(torch.int32),
+                                   g32[o:o + m].view(torch.int32)), (form, flag, o)
+            assert torch.equal(i[:layout.i64_numel], g64[:layout.i64_numel]), (form, flag)
+
+
 def test_int64_adversarial(lib):
     man = {"keys": [{"key": f"i{j}", "shape": s, "dtype": "int64"}
                     for j, s in enumerate([[], [1], [3], [9], [40], [300]])]}

@@ -13,7 +13,7 @@ from conftest import ROOT
 LLVM = "/opt/rocm/lib/llvm/bin"
 LIBS = [os.path.join(ROOT, "feddct_amd", "libfedagg.so"),
         os.path.join(ROOT, "feddct_amd", "libfedagg_comm.so")]
-HOT = "_ZN12_GLOBAL__N_113reduce_kernelILi2ELi16ELb0ELb0ELi3ELb0EEEvNS_10ReduceArgsE"
+HOT = "_ZN4fa_k13reduce_kernelILi2ELi16ELb0ELb0ELi3ELb0EEEvNS_10ReduceArgsE"
 
 
 def _have_tools():
@@ -22,19 +22,33 @@ def _have_tools():
         shutil.which("objcopy")
 
 
-def _code_object(lib, tmp_path):
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _code_objects(lib, tmp_path):
+    """The gfx950 code object of every translation unit: the .hip_fatbin
+    section holds one offload bundle per unit (libfedagg.so is built from
+    several, feddct_amd/build.py), each starting with the bundle magic."""
     fb = tmp_path / (os.path.basename(lib) + ".fatbin")
-    co = tmp_path / (os.path.basename(lib) + ".co")
     subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, str(fb)],
                    check=True)
-    targets = subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--list", "--type=o",
-                              f"--input={fb}"], check=True, capture_output=True,
-                             text=True).stdout.split()
-    assert "hipv4-amdgcn-amd-amdhsa--gfx950" in targets, targets
-    subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o",
-                    f"--input={fb}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
-                    f"--output={co}"], check=True)
-    return str(co)
+    data = fb.read_bytes()
+    starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
+    assert starts, "no offload bundle in " + lib
+    cos = []
+    for k, (a, b) in enumerate(zip(starts, starts[1:] + [len(data)])):
+        part = tmp_path / f"{os.path.basename(lib)}.{k}.bundle"
+        part.write_bytes(data[a:b])
+        co = tmp_path / f"{os.path.basename(lib)}.{k}.co"
+        targets = subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--list",
+                                  "--type=o", f"--input={part}"], check=True,
+                                 capture_output=True, text=True).stdout.split()
+        assert "hipv4-amdgcn-amd-amdhsa--gfx950" in targets, targets
+        subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o",
+                        f"--input={part}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                        f"--output={co}"], check=True)
+        cos.append(str(co))
+    return cos
 
 
 def _kernels(co):
@@ -54,20 +68,36 @@ def _kernels(co):
 @pytest.mark.skipif(not _have_tools(), reason="ROCm llvm tools / objcopy not available")
 @pytest.mark.parametrize("lib", LIBS)
 def test_code_object_has_gfx950_and_no_scratch(lib, tmp_path):
-    co = _code_object(lib, tmp_path)
-    kernels = _kernels(co)
-    assert kernels, "no kernels found in the code object"
+    kernels = {}
+    for co in _code_objects(lib, tmp_path):
+        kernels.update(_kernels(co))
+    assert kernels, "no kernels found in the code objects"
     assert {k: v for k, v in kernels.items() if v} == {}, "kernels using scratch"
 
 
 @pytest.mark.skipif(not _have_tools(), reason="ROCm llvm tools / objcopy not available")
+def test_every_reduce_variant_is_compiled_once(tmp_path):
+    """The reduce kernel family is split over several units (build.py); no
+    instance may be compiled in two of them (each unit registers its own
+    code object for the kernels it launches)."""
+    seen = {}
+    for k, co in enumerate(_code_objects(LIBS[0], tmp_path)):
+        for name in _kernels(co):
+            assert name not in seen, (name, seen.get(name), k)
+            seen[name] = k
+    assert HOT in seen
+
+
+@pytest.mark.skipif(not _have_tools(), reason="ROCm llvm tools / objcopy not available")
 def test_hot_kernel_uses_global_nt_loads(tmp_path):
-    co = _code_object(LIBS[0], tmp_path)
-    dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", co], check=True,
-                         capture_output=True, text=True).stdout
-    m = re.search(re.escape(HOT) + r">:\n(.*?)\n\n", dis, flags=re.S)
-    assert m, "default reduce kernel not found"
-    body = m.group(1)
+    body = None
+    for co in _code_objects(LIBS[0], tmp_path):
+        dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", co], check=True,
+                             capture_output=True, text=True).stdout
+        m = re.search(re.escape(HOT) + r">:\n(.*?)(?:\n\n|\Z)", dis, flags=re.S)
+        if m:
+            body = m.group(1)
+    assert body, "default reduce kernel not found"
     loads = re.findall(r"\b(global|flat|buffer)_load_dwordx4\b[^\n]*", body)
     assert loads and not re.search(r"\bflat_load_dwordx4\b", body), "hot loads are flat"
     nt = re.findall(r"global_load_dwordx4[^\n]*\bnt\b", body)

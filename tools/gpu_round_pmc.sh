@@ -1,11 +1,12 @@
 #!/bin/bash
 # Kernel trace + FETCH_SIZE / WRITE_SIZE passes (separate runs) of the cfg2
-# round (reduce + broadcast) and of the torch-GPU-order reduce.
+# round (reduce + broadcast) and of the torch-GPU-order reduce (MODES: any
+# tools/round_prof.py modes).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for m in round tgpu; do
+for m in ${MODES:-round tgpu}; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/rp_${m}_trace -o run -- python3 tools/round_prof.py $m 50 > gpurun_out/rp_${m}.log 2>&1 \
   && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d gpurun_out/rp_${m}_fetch -o run -- python3 tools/round_prof.py $m 10 >> gpurun_out/rp_${m}.log 2>&1 \
   && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d gpurun_out/rp_${m}_write -o run -- python3 tools/round_prof.py $m 10 >> gpurun_out/rp_${m}.log 2>&1 \

@@ -1,8 +1,11 @@
 """The cfg2 round's kernels alone, for rocprofv3 (kernel trace and the
 separate FETCH_SIZE / WRITE_SIZE passes of tools/gpu_round_pmc.sh):
 
-    python tools/round_prof.py round K   # reduce + bcast_group_kernel (FA_F_BCAST)
-    python tools/round_prof.py tgpu K    # the torch-GPU-order reduce (tgpu_kernel<0>)
+    python tools/round_prof.py round K        # reduce + broadcast launch (FA_F_BCAST)
+    python tools/round_prof.py round_noxcd K  # ... r02's consecutive client groups
+    python tools/round_prof.py bcast K        # the broadcast launch alone (FA_F_BCAST_ONLY)
+    python tools/round_prof.py bcast_noxcd K
+    python tools/round_prof.py tgpu K         # the torch-GPU-order reduce (tgpu_kernel<0>)
 """
 import os
 import sys
@@ -25,8 +28,12 @@ def main():
     n = 20
     cl = make_clients(lay, man, range(n), dev)
     o32, o64 = torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])
-    if mode == "round":
-        red = Reducer(lay, cl, o32, o64, flags=_lib.FA_F_BCAST)
+    nx = _lib.FA_PLAN_GAPS_ARE_PADDING | _lib.FA_PLAN_TUNE_BCAST_NOXCD
+    if mode in ("round", "bcast", "round_noxcd", "bcast_noxcd"):
+        plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
+                         flags=nx if mode.endswith("noxcd") else _lib.FA_PLAN_GAPS_ARE_PADDING)
+        red = Reducer(lay, cl, o32, o64, plan=plan,
+                      flags=_lib.FA_F_BCAST if mode.startswith("round") else _lib.FA_F_BCAST_ONLY)
     elif mode == "tgpu":
         plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
                          order=_lib.FA_ORDER_TORCH_GPU, n=n)
