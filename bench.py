@@ -186,6 +186,10 @@ def pmc_traffic(n_gpus):
                 "source": "profiles/reduce_pmc.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                           "passes (separate runs) of bench.py --kernel-only",
                 "profile_kernel_avg_us": round(d["avg_ns"] / 1e3, 2) if "avg_ns" in d else None,
+                "profile_date_utc": d.get("date_utc"), "profile_host": d.get("host"),
+                "profile_gpu": d.get("gpu"),
+                "note": "measured in a separate profiler run (counters cannot be read from "
+                        "inside the timed process), not in this run",
                 "traffic_over_algorithmic": round(d["hbm_bytes_per_launch"]
                                                   / d["algorithmic_bytes_per_launch"], 4)
                 if d.get("algorithmic_bytes_per_launch") else None}
@@ -413,7 +417,37 @@ def other_configs(dev, steps=100, warmup=20):
                                           24, None)], 1,
         {"wrnsl16_8_sf4_c100_main": "feddct/wrnsl16_8_sf4_c100_main/n24",
          "wrnsl16_8_sf4_c100_proxy": "feddct/wrnsl16_8_sf4_c100_proxy/n24"})
+    # r03: the reference's other FedDCT sweep layouts,
+    # rotated over enough sets that every step misses the 256 MiB MALL
+    for tag, sf, n, rot in (("resnet110sl", 4, 25, 4), ("wrnsl16_8", 32, 3, 6)):
+        nm = f"{tag}_sf{sf}_c100"
+        run(f"sweep_{nm}_n{n}", [((nm + "_main", nm + "_proxy"), n, None)], rot,
+            {nm + "_main": f"feddct/{nm}_main/n{n}", nm + "_proxy": f"feddct/{nm}_proxy/n{n}"})
+        res[f"sweep_{nm}_n{n}"].update(scalar_share(dev, nm, n, steps, warmup))
+    for v in res.values():
+        v["roofline_frac"] = round(v["GBps"] / HBM_PEAK_GBS, 4)
     return res
+
+
+def scalar_share(dev, name, n, steps, warmup):
+    """Where a layout's time goes: its scalar tiles (ILP-4 tails, M == 1 and
+    int64 keys: one thread per element walking the clients) and its vector
+    tiles, each launched alone over the same clients."""
+    from feddct_amd.workload import joint_manifest
+    mans = [load_manifest(name + "_main"), load_manifest(name + "_proxy")]
+    lay = BucketLayout.from_manifest(joint_manifest(mans))
+    cl = make_clients(lay, list(zip(mans, ("0.", "1."))), range(n), dev)
+    o32, o64 = torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])
+    info, tiles = _lib.build_tiles_host(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel)
+    out = {"scalar_tiles": int(info["ntiles_tail"]), "vector_tiles": int(info["ntiles_cascade"]),
+           "scalar_elems_frac": round(info["tail_elems"] / max(1, info["tail_elems"]
+                                                                + info["cascade_elems"]), 5)}
+    for part, sel in (("scalar_tiles_alone_us", tiles[:, 2] != 0),
+                      ("vector_tiles_alone_us", tiles[:, 2] == 0)):
+        plan = _lib.Plan(None, lay.f32_numel, None, lay.i64_numel, 0, tiles=tiles[sel])
+        t, _ = timed_launches(Reducer(lay, cl, o32, o64, plan=plan), steps, warmup)
+        out[part] = round(t * 1e6, 2)
+    return out
 
 
 def cfg5_sharded(dev, world, rank, group, steps, ncomm=None, chain_chunks=16):
@@ -1089,7 +1123,12 @@ def build_line(args, world, nbytes_rank, bytes_per_client, t_step, t_kernel, ext
                      "traffic": traffic, "traffic_pmc": traffic_src,
                      "kernel_us": round(t_kernel * 1e6, 2)},
         "cpu_baseline": None,
+        "host": os.uname().nodename,
     }
+    try:
+        line["gpu"] = torch.cuda.get_device_name(0)
+    except Exception:  # noqa: BLE001  (CPU-only helper tests)
+        line["gpu"] = None
     line.update(extra)
     return line
 

@@ -31,6 +31,7 @@ FA_INLINE_CLIENTS = 128
 FA_F_BCAST = 1
 FA_F_SUM_ONLY = 2
 FA_F_BCAST_ONLY = 4
+FA_PROX_ACCUMULATE = 1
 FA_PLAN_GAPS_ARE_PADDING = 1
 FA_PLAN_TUNE_NO_NT = 2
 FA_PLAN_TUNE_BATCH8 = 4
@@ -68,8 +69,9 @@ EXPORTS = [
     "fa_mean_i64_trunc", "fa_div_f32", "fa_div_trunc_i64", "fa_broadcast_f32",
     "fa_synth_fill_f32", "fa_synth_fill_i64", "fa_copy_f32",
     "fa_norm_plan_create", "fa_norm_plan_destroy", "fa_prox_norms", "fa_prox_grad",
+    "fa_prox_grad_ex",
     "fa_read_probe_f32", "fa_chain_levels", "fa_reduce_chain", "fa_torch_gpu_config",
-    "fa_plan_create_order",
+    "fa_plan_create_order", "fa_table_bytes", "fa_reduce_tab",
 ]
 
 
@@ -120,6 +122,8 @@ def _load():
         "fa_plan_create_from_tiles": (_I, [_P, _I, _I64, _I64, _I, ctypes.c_uint,
                                            ctypes.POINTER(_P)]),
         "fa_reduce": (_I, [_P, _P, _P, _I, _P, _P, _P, ctypes.c_uint, _P]),
+        "fa_table_bytes": (ctypes.c_size_t, [_I]),
+        "fa_reduce_tab": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, ctypes.c_uint, _P]),
         "fa_mean_f32": (_I, [_P, _I, _I64, _P, _P, _I, _P]),
         "fa_weighted_f32": (_I, [_P, _P, _I, _I64, _P, _P, _I, _P]),
         "fa_mean_i64_trunc": (_I, [_P, _I, _I64, _P, _P, _I, _P]),
@@ -139,6 +143,7 @@ def _load():
         "fa_norm_plan_destroy": (_I, [_P]),
         "fa_prox_norms": (_I, [_P, _P, _P, _P, _P, _P]),
         "fa_prox_grad": (_I, [_P, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P]),
+        "fa_prox_grad_ex": (_I, [_P, _P, _P, _P, _P, ctypes.c_float, _P, _P, ctypes.c_uint, _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)  # AttributeError = missing export: loud

@@ -29,7 +29,7 @@ FA_E_COMM = -6
 FA_COMM_UID_BYTES = 128
 
 COMM_EXPORTS = ["fa_comm_unique_id", "fa_comm_init_rank", "fa_comm_init", "fa_comm_destroy",
-                "fa_comm_info", "fa_shard_plan_create", "fa_shard_plan_create_ex",
+                "fa_comm_info", "fa_comm_set_graphs", "fa_shard_plan_create", "fa_shard_plan_create_ex",
                 "fa_shard_plan_destroy", "fa_reduce_sharded", "fa_mean_f32_multi",
                 "fa_stripe_plan_create", "fa_stripe_plan_destroy", "fa_reduce_striped",
                 "fa_chain_plan_create", "fa_chain_plan_destroy", "fa_reduce_chained",
@@ -72,6 +72,7 @@ def _load():
         "fa_comm_init": [_I, ctypes.POINTER(_I), ctypes.POINTER(_P)],
         "fa_comm_destroy": [_P],
         "fa_comm_info": [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I)],
+        "fa_comm_set_graphs": [_P, _I],
         "fa_shard_plan_create": [_P, _P, _I, _I64, _P, _I, _I64, ctypes.POINTER(_I), _I,
                                  ctypes.c_uint, ctypes.POINTER(_P)],
         "fa_shard_plan_destroy": [_P],
@@ -182,6 +183,12 @@ class Comm:
     def single(cls) -> "Comm":
         """A one-rank communicator (no process group needed)."""
         return cls(1, 0, unique_id())
+
+    def set_graphs(self, enable: bool) -> None:
+        """Captured rounds on / off (fedagg_comm.h fa_comm_set_graphs; on by
+        default): each round's schedule replayed from a HIP graph."""
+        _lib.check(lib().fa_comm_set_graphs(self.handle, int(bool(enable))),
+                   "fa_comm_set_graphs")
 
     def info(self):
         n, r, d = _I(), _I(), _I()

@@ -951,6 +951,34 @@ hipError_t table_alloc(void** p, size_t bytes, hipStream_t st) {
   }
   return hipMallocFromPoolAsync(p, bytes, pool, st);
 }
+
+// A caller-owned pointer table (fa_reduce_tab) is written by kernels whose
+// arguments carry the words by value: no host memcpy, no allocation, so the
+// call can be captured into a graph and replayed (the table's contents are
+// the kernel arguments, frozen at capture).
+constexpr int kFillWords = 400;
+struct FillArgs {
+  uint64_t* dst;
+  int count;
+  uint64_t w[kFillWords];
+};
+__global__ void table_fill_kernel(FillArgs a) {
+  for (int i = threadIdx.x; i < a.count; i += blockDim.x) a.dst[i] = a.w[i];
+}
+hipError_t table_fill(void* dst, const std::vector<char>& host, hipStream_t st) {
+  const size_t words = (host.size() + 7) / 8;
+  for (size_t w0 = 0; w0 < words; w0 += kFillWords) {
+    FillArgs f;
+    memset(&f, 0, sizeof f);
+    f.dst = (uint64_t*)dst + w0;
+    f.count = (int)std::min<size_t>(kFillWords, words - w0);
+    memcpy(f.w, host.data() + w0 * 8, std::min<size_t>(f.count * 8, host.size() - w0 * 8));
+    hipLaunchKernelGGL(table_fill_kernel, dim3(1), dim3(256), 0, st, f);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
 }  // namespace
 
 extern "C" {
@@ -1336,9 +1364,17 @@ hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, b
 }
 }  // namespace
 
+size_t fa_table_bytes(int n) { return n > kInline ? ((size_t)n * 20 + 7) / 8 * 8 : 0; }
+
 int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const* c64, int n,
               const float* weights, float* out32, int64_t* out64, unsigned flags,
               void* stream) {
+  return fa_reduce_tab(plan, c32, c64, n, weights, nullptr, out32, out64, flags, stream);
+}
+
+int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* const* c64, int n,
+                  const float* weights, void* ctable, float* out32, int64_t* out64,
+                  unsigned flags, void* stream) {
   if (!plan) return set_err(FA_E_INVAL, "fa_reduce: plan is NULL");
   if (n < 1) return set_err(FA_E_INVAL, "fa_reduce: need at least one client (n=%d)", n);
   if (n > FA_MAX_CLIENTS)
@@ -1397,15 +1433,23 @@ int fa_reduce(const fa_plan* plan, const float* const* c32, const int64_t* const
       h64[i] = need64 ? (const void*)c64[i] : nullptr;
       hw[i] = weights ? weights[i] : 0.f;
     }
-    HIP_TRY(table_alloc(&table, host.size(), st));
-    HIP_TRY(hipMemcpyAsync(table, host.data(), host.size(), hipMemcpyHostToDevice, st));
-    a.tab32 = (const float* const*)table;
-    a.tab64 = (const int64_t* const*)((const void**)table + n);
-    a.tabw = (const float*)((const void**)table + 2 * n);
+    if (ctable) {   // caller-owned (fa_reduce_tab): written by kernels, no memcpy
+      a.tab32 = (const float* const*)ctable;
+      a.tab64 = (const int64_t* const*)((const void**)ctable + n);
+      a.tabw = (const float*)((const void**)ctable + 2 * n);
+      HIP_TRY(table_fill(ctable, host, st));
+    } else {
+      HIP_TRY(table_alloc(&table, host.size(), st));
+      HIP_TRY(hipMemcpyAsync(table, host.data(), host.size(), hipMemcpyHostToDevice, st));
+      a.tab32 = (const float* const*)table;
+      a.tab64 = (const int64_t* const*)((const void**)table + n);
+      a.tabw = (const float*)((const void**)table + 2 * n);
+    }
   }
   if (flags & FA_F_BCAST_ONLY) {
     // the broadcast alone (the reference's initial sync, train_fedavg.py:
     // 244-250, and :148-149 without the reduce): out32/out64 -> every client
+    a.ntiles = in.ntiles;
     hipError_t e = launch_bcast(plan, a, n, in.ntiles, plan->order != FA_ORDER_TORCH_GPU, st);
     if (table) {
       hipError_t e2 = hipFreeAsync(table, st);

@@ -36,7 +36,10 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <list>
 #include <map>
 #include <mutex>
 #include <string>
@@ -62,6 +65,7 @@ struct fa_comm {
   ncclComm_t nc = nullptr;
   int nranks = 0, rank = 0, device = 0;
   hipStream_t cs = nullptr;  // communication stream
+  bool graphs = true;        // replay rounds from captured HIP graphs (fa_comm_set_graphs)
 };
 
 namespace {
@@ -115,6 +119,13 @@ __global__ void scatter_f32_kernel(const float* __restrict__ src, const int64_t*
 // promotes exactly as reduce_kernel's `promote` does at row i), then the
 // finish ((rem + l1) + l2) + l3 and the division.  blk: nblk + has_rem rows
 // of `row` floats (the remainder block's partial last).
+// Up to kFoldPtrs pieces each piece's stripe is read where it lies (r03):
+// src[k] is the stripe's first element — the owner's receive row for a
+// remote piece, or this rank's own block-sum / continuation plane, which the
+// schedule's K_COPY into the receive row would have duplicated (the executor
+// binds the row to the copy's source instead, FA_X_K_COPY below).  More
+// pieces: rows of blk, copies made.
+constexpr int kFoldPtrs = 256;
 struct FoldArgs {
   const float* blk;
   int64_t row;
@@ -125,7 +136,12 @@ struct FoldArgs {
   int lp;
   int n_total;
   int divide;
+  int bound;  // src[] holds every piece's stripe
+  const float* src[kFoldPtrs];
 };
+__device__ __forceinline__ float fold_at(const FoldArgs& a, int k, int64_t e) {
+  return a.bound ? a.src[k][e] : a.blk[(size_t)k * a.row + e];
+}
 __global__ void fold_kernel(FoldArgs a) {
   const int mask = (1 << a.lp) - 1;
   const float fn = (float)a.n_total;
@@ -133,7 +149,7 @@ __global__ void fold_kernel(FoldArgs a) {
        e += (int64_t)gridDim.x * blockDim.x) {
     float l1 = 0.f, l2 = 0.f, l3 = 0.f;
     for (int k = 0; k < a.nblk; ++k) {
-      l1 = __fadd_rn(l1, a.blk[(size_t)k * a.row + e]);
+      l1 = __fadd_rn(l1, fold_at(a, k, e));
       const int i = (k + 1) << a.lp;
       if ((i & (mask << a.lp)) != 0) continue;
       l2 = __fadd_rn(l2, l1);
@@ -142,7 +158,7 @@ __global__ void fold_kernel(FoldArgs a) {
       l3 = __fadd_rn(l3, l2);
       l2 = 0.f;
     }
-    const float l0 = a.has_rem ? a.blk[(size_t)a.nblk * a.row + e] : 0.f;
+    const float l0 = a.has_rem ? fold_at(a, a.nblk, e) : 0.f;
     const float s = __fadd_rn(__fadd_rn(__fadd_rn(l0, l1), l2), l3);
     a.out[e] = a.divide ? __fdiv_rn(s, fn) : s;
   }
@@ -767,7 +783,8 @@ int make_comm(ncclComm_t nc, int device, fa_comm** out) {
 struct fa_round_plan {
   int mode = 0;  // FA_MODE_*
   int xchg = 0;
-  fa_comm* comm = nullptr;
+  fa_comm* comm = nullptr;  // (may be destroyed before the plan: never read in free_round)
+  int device = -1;          // the comm's device, for free_round
   Geo g;
   // e1: chunk plans + their ranges; chained: vector-tile chunk plans + ranges
   std::vector<fa_plan*> chunk;
@@ -805,6 +822,18 @@ struct fa_round_plan {
   std::vector<const int64_t*> i64_rows;
   std::vector<hipEvent_t> ev;  // start, compute-joins (ring), done
   std::map<std::pair<int, int>, std::vector<fa_xfer>> sched;  // (root, weighted) -> ops
+  // captured rounds (one process per GPU): the whole schedule of one
+  // (root, weights, buffers) call as a HIP graph, replayed by one launch;
+  // most recently used first, at most kGraphCache
+  struct Graph {
+    std::string key;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    std::vector<void*> tables;  // device pointer tables the graph's kernels read
+  };
+  std::list<Graph> graphs;
+  hipStream_t gs = nullptr;     // capture stream
+  bool graph_failed = false;    // capture refused once: this plan runs uncaptured
 };
 
 namespace {
@@ -812,7 +841,7 @@ namespace {
 void free_round(fa_round_plan* p) {
   if (!p) return;
   DeviceGuard dg;
-  if (p->comm) (void)hipSetDevice(p->comm->device);
+  if (p->device >= 0) (void)hipSetDevice(p->device);
   for (fa_plan* c : p->chunk) fa_plan_destroy(c);
   fa_plan_destroy(p->stripe);
   fa_plan_destroy(p->plan64);
@@ -824,6 +853,12 @@ void free_round(fa_round_plan* p) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+  for (auto& gr : p->graphs) {
+    if (gr.exec) (void)hipGraphExecDestroy(gr.exec);
+    if (gr.graph) (void)hipGraphDestroy(gr.graph);
+    for (void* t : gr.tables) (void)hipFree(t);
+  }
+  if (p->gs) (void)hipStreamDestroy(p->gs);
   delete p;
 }
 
@@ -872,6 +907,7 @@ int make_round(fa_comm* comm, int mode, const fa_seg* seg32, int nseg32, int64_t
   p->mode = mode;
   p->xchg = xchg;
   p->comm = comm;
+  p->device = comm->device;
   int rc = make_geo(comm->nranks, comm->rank, counts, seg32, nseg32, f32_numel, seg64, nseg64,
                     i64_numel, flags, who, &p->g);
   if (rc) {
@@ -1007,7 +1043,20 @@ struct Local {
   hipStream_t user;  // the caller's stream (compute)
   bool comp_dirty;   // compute-stream work the comm stream has not joined yet
   std::vector<const float*> src;  // e2 stripe sources
+  // while capturing: the graph's own pointer tables for the kernels over
+  // more than FA_INLINE_CLIENTS rows (fa_reduce_tab), taken in order
+  const std::vector<void*>* tables = nullptr;
+  size_t next_table = 0;
+  // blocked fold: piece k's stripe where it lies (NULL: its receive row)
+  std::vector<const float*> blk_src;
 };
+
+// The table of the next >FA_INLINE_CLIENTS-row kernel of a captured round
+// (NULL when not capturing: fa_reduce's own pool).
+void* take_table(Local& L) {
+  if (!L.tables || L.next_table >= L.tables->size()) return nullptr;
+  return (*L.tables)[L.next_table++];
+}
 
 ncclDataType_t dtype_of(int buf, int index) {
   return ((buf == FA_B_STACK || buf == FA_B_GATHER) && index == 1) ? ncclInt64 : ncclFloat32;
@@ -1142,17 +1191,30 @@ int issue_local(Local& L, const fa_xfer& x, hipStream_t s) {
       return fa_div_f32(io->out32 + x.offset, (float)g.n_total, io->out32 + x.offset, x.count,
                         s);
     case FA_X_K_COPY:
-      FA_HIP_TRY(hipMemcpyAsync(addr(L, x.dst, x.dst_index, x.offset),
-                                addr(L, x.src, x.src_index, x.offset), (size_t)x.count * 4,
-                                hipMemcpyDeviceToDevice, s));
+      // the blocked fold reads an own piece in its plane: bind, do not copy
+      if (x.dst == FA_B_BLK && p->bg.P <= kFoldPtrs) {
+        if (L.blk_src.size() < (size_t)p->bg.P) L.blk_src.assign(p->bg.P, nullptr);
+        L.blk_src[x.dst_index] = (const float*)addr(L, x.src, x.src_index, x.offset);
+        return FA_OK;
+      }
+      {
+        // a copy kernel (capture-safe: a D2D hipMemcpyAsync inside a captured
+        // round broke the capture, hipErrorStreamCaptureImplicit, r03)
+        const float* src = (const float*)addr(L, x.src, x.src_index, x.offset);
+        float* dst = (float*)addr(L, x.dst, x.dst_index, x.offset);
+        if ((((uintptr_t)src | (uintptr_t)dst) & 15u) == 0)
+          return fa_copy_f32(src, dst, x.count, s);
+        FA_HIP_TRY(hipMemcpyAsync(dst, src, (size_t)x.count * 4, hipMemcpyDeviceToDevice, s));
+      }
       return FA_OK;
     case FA_X_K_STRIPE: {
       L.src.assign(p->g.n_total, nullptr);
       for (int k = 0; k < g.n_total; ++k)
         L.src[k] = p->recv + (size_t)k * p->row - p->lo[g.rank];  // element e at [e - lo]
       for (int j = 0; j < g.n_local; ++j) L.src[g.lo_slot + j] = io->c32[j];
-      return fa_reduce(p->stripe, L.src.data(), nullptr, g.n_total, nullptr,
-                       p->sbuf - p->lo[g.rank], nullptr, 0, s);
+      void* tab = g.n_total > FA_INLINE_CLIENTS ? take_table(L) : nullptr;
+      return fa_reduce_tab(p->stripe, L.src.data(), nullptr, g.n_total, nullptr, tab,
+                           p->sbuf - p->lo[g.rank], nullptr, 0, s);
     }
     case FA_X_K_CHAIN: {
       fa_chain ch;
@@ -1176,15 +1238,17 @@ int issue_local(Local& L, const fa_xfer& x, hipStream_t s) {
       return FA_OK;
     }
     case FA_X_K_TAILS: {
+      const bool big = g.n_total > FA_INLINE_CLIENTS;
       if (p->plan64) {
-        const int rc = fa_reduce(p->plan64, nullptr, p->i64_rows.data(), g.n_total, nullptr,
-                                 nullptr, io->out64, 0, s);
+        const int rc = fa_reduce_tab(p->plan64, nullptr, p->i64_rows.data(), g.n_total, nullptr,
+                                     big ? take_table(L) : nullptr, nullptr, io->out64, 0, s);
         if (rc) return rc;
       }
       if (p->plan_t32) {
         // pre-multiplied rows when weighted: their plain sum is the weighted order
-        const int rc = fa_reduce(p->plan_t32, p->t32_rows.data(), nullptr, g.n_total, nullptr,
-                                 p->t32_out, nullptr, io->weights ? FA_F_SUM_ONLY : 0, s);
+        const int rc = fa_reduce_tab(p->plan_t32, p->t32_rows.data(), nullptr, g.n_total,
+                                     nullptr, big ? take_table(L) : nullptr, p->t32_out,
+                                     nullptr, io->weights ? FA_F_SUM_ONLY : 0, s);
         if (rc) return rc;
         const int64_t T = p->cg.t32_width;
         hipLaunchKernelGGL(scatter_f32_kernel, dim3((unsigned)std::min<int64_t>(64, (T + 255) / 256)),
@@ -1226,6 +1290,14 @@ int issue_local(Local& L, const fa_xfer& x, hipStream_t s) {
       f.lp = bg.lp;
       f.n_total = g.n_total;
       f.divide = io->weights == nullptr;
+      f.bound = bg.P <= kFoldPtrs;
+      if (f.bound) {
+        for (int k = 0; k < bg.P; ++k) {
+          const float* own = k < (int)L.blk_src.size() ? L.blk_src[k] : nullptr;
+          f.src[k] = own ? own : p->blk + (size_t)k * bg.row;
+        }
+        L.blk_src.assign(L.blk_src.size(), nullptr);
+      }
       const unsigned grid = (unsigned)std::min<int64_t>(2048, (x.count + 255) / 256);
       hipLaunchKernelGGL(fold_kernel, dim3(std::max(1u, grid)), dim3(256), 0, s, f);
       FA_HIP_TRY(hipGetLastError());
@@ -1320,6 +1392,134 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
   return FA_OK;
 }
 
+// ------------------------------------------------------ captured rounds ----
+// One process per GPU: a round's whole schedule (its RCCL groups on the
+// communication stream, its kernels on both streams, the event joins) is
+// captured into a HIP graph once per (root, weights, buffers) and replayed by
+// one hipGraphLaunch on the caller's stream — the executor issued ~12 µs of
+// host calls per step (chained at 16 chunks: 190 µs of host issue per round,
+// profiles/r02_native_round_cost.jsonl).  The capture runs on the plan's own
+// stream (the caller's may be the legacy null stream, which cannot be
+// captured); kernels over more than FA_INLINE_CLIENTS rows take pointer
+// tables the graph owns (fa_reduce_tab).  A round whose other kernels exceed
+// that row count, or a capture the runtime or RCCL refuses, runs uncaptured.
+constexpr size_t kGraphCache = 4;
+
+std::string graph_key(const Local& L, int root, bool weighted) {
+  const Geo& g = L.p->g;
+  const fa_shard_io* io = L.io;
+  std::string k;
+  auto put = [&](const void* p, size_t n) { k.append((const char*)p, n); };
+  put(&root, sizeof root);
+  put(&weighted, sizeof weighted);
+  put(&io->out32, sizeof io->out32);
+  put(&io->out64, sizeof io->out64);
+  if (g.n_local > 0) {
+    put(io->c32, sizeof(void*) * g.n_local);
+    if (io->c64) put(io->c64, sizeof(void*) * g.n_local);
+    if (io->weights) put(io->weights, sizeof(float) * g.n_local);
+  }
+  return k;
+}
+
+// Kernel ops other than the stripe / tails reductions take inline pointer
+// lists only up to FA_INLINE_CLIENTS rows; count the tables those two need.
+bool capturable(const fa_round_plan* p, const std::vector<fa_xfer>& ops, size_t* ntables) {
+  *ntables = 0;
+  const bool big = p->g.n_total > FA_INLINE_CLIENTS;
+  for (const fa_xfer& x : ops) {
+    // RCCL's ncclReduceScatter / ncclGather crash under stream capture (a
+    // segfault in the capturing call, one-rank communicator, ROCm 7.2): the
+    // reduce-scatter + gather exchange runs uncaptured
+    if (x.op == FA_X_REDUCE_SCATTER || x.op == FA_X_GATHER) return false;
+    if (is_comm(x.op)) continue;
+    if (x.op == FA_X_K_STRIPE) {
+      *ntables += big ? 1 : 0;
+    } else if (x.op == FA_X_K_TAILS) {
+      *ntables += big ? (p->plan64 ? 1 : 0) + (p->plan_t32 ? 1 : 0) : 0;
+    } else if (x.nrows > FA_INLINE_CLIENTS ||
+               (x.op == FA_X_K_SUM && p->g.n_local > FA_INLINE_CLIENTS)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+// true: the round ran from a graph (rc = its status); false: run it uncaptured.
+bool replay_graph(Local& L, const std::vector<fa_xfer>& ops, int root, bool weighted, int* rc) {
+  fa_round_plan* p = L.p;
+  size_t ntables = 0;
+  if (!capturable(p, ops, &ntables)) return false;
+  if (hipSetDevice(p->comm->device) != hipSuccess) return false;
+  const std::string key = graph_key(L, root, weighted);
+  for (auto it = p->graphs.begin(); it != p->graphs.end(); ++it) {
+    if (it->key != key) continue;
+    p->graphs.splice(p->graphs.begin(), p->graphs, it);
+    const hipError_t e = hipGraphLaunch(p->graphs.front().exec, L.user);
+    *rc = e == hipSuccess ? FA_OK
+                          : set_err(FA_E_HIP, "hipGraphLaunch: %s", hipGetErrorString(e));
+    return true;
+  }
+  if (!p->gs && hipStreamCreateWithFlags(&p->gs, hipStreamNonBlocking) != hipSuccess) {
+    p->graph_failed = true;
+    return false;
+  }
+  fa_round_plan::Graph gr;
+  gr.key = key;
+  const size_t tb = fa_table_bytes(p->g.n_total);
+  for (size_t i = 0; i < ntables; ++i) {
+    void* t = nullptr;
+    if (hipMalloc(&t, std::max<size_t>(tb, 16)) != hipSuccess) {
+      for (void* x : gr.tables) (void)hipFree(x);
+      return false;
+    }
+    gr.tables.push_back(t);
+  }
+  auto drop = [&](fa_round_plan::Graph& x) {
+    if (x.exec) (void)hipGraphExecDestroy(x.exec);
+    if (x.graph) (void)hipGraphDestroy(x.graph);
+    for (void* t : x.tables) (void)hipFree(t);
+  };
+  // capture on the plan's stream: the executor's "caller stream" is gs
+  Local C = L;
+  C.user = p->gs;
+  C.tables = &gr.tables;
+  C.next_table = 0;
+  hipError_t e = hipStreamBeginCapture(p->gs, hipStreamCaptureModeRelaxed);
+  if (e != hipSuccess) {
+    drop(gr);
+    p->graph_failed = true;
+    return false;
+  }
+  std::vector<Local> one{C};
+  std::vector<const std::vector<fa_xfer>*> sc{&ops};
+  const int erc = execute(one, sc);
+  e = hipStreamEndCapture(p->gs, &gr.graph);
+  if (getenv("FA_GRAPH_DEBUG"))
+    fprintf(stderr, "fedcomm capture: execute rc=%d (%s) end=%s graph=%p\n", erc,
+            erc ? fa_last_error() : "", hipGetErrorString(e), (void*)gr.graph);
+  if (erc != FA_OK || e != hipSuccess || !gr.graph) {
+    drop(gr);
+    (void)hipGetLastError();
+    p->graph_failed = true;   // the runtime or RCCL refused: uncaptured from now on
+    return false;
+  }
+  e = hipGraphInstantiate(&gr.exec, gr.graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    drop(gr);
+    p->graph_failed = true;
+    return false;
+  }
+  p->graphs.push_front(std::move(gr));
+  while (p->graphs.size() > kGraphCache) {
+    drop(p->graphs.back());
+    p->graphs.pop_back();
+  }
+  e = hipGraphLaunch(p->graphs.front().exec, L.user);
+  *rc = e == hipSuccess ? FA_OK : set_err(FA_E_HIP, "hipGraphLaunch: %s", hipGetErrorString(e));
+  return true;
+}
+
 int run_round(fa_round_plan* const* plans, int nlocal, const fa_shard_io* io, int root, int mode,
               const char* who) {
   if (nlocal < 1 || !plans || !io) return set_err(FA_E_INVAL, "%s: bad arguments", who);
@@ -1354,6 +1554,10 @@ int run_round(fa_round_plan* const* plans, int nlocal, const fa_shard_io* io, in
     scheds.push_back(&schedule(p, root, weighted));
   }
   DeviceGuard dg;
+  if (nlocal == 1 && plans[0]->comm->graphs && !plans[0]->graph_failed) {
+    int rc = FA_OK;
+    if (replay_graph(locals[0], *scheds[0], root, weighted, &rc)) return rc;
+  }
   return execute(locals, scheds);
 }
 
@@ -1430,6 +1634,12 @@ int fa_comm_destroy(fa_comm* c) {
   ncclResult_t r = c->nc ? ncclCommDestroy(c->nc) : ncclSuccess;
   delete c;
   if (r != ncclSuccess) return set_err(FA_E_COMM, "ncclCommDestroy: %s", ncclGetErrorString(r));
+  return FA_OK;
+}
+
+int fa_comm_set_graphs(fa_comm* c, int enable) {
+  if (!c) return set_err(FA_E_INVAL, "fa_comm_set_graphs: NULL comm");
+  c->graphs = enable != 0;
   return FA_OK;
 }
 

@@ -73,7 +73,66 @@ PyObject* bump_versions(PyObject*, PyObject* args) {
   Py_RETURN_NONE;
 }
 
+// grad_state(params, views) -> 0: every params[i].grad is views[i] (the flat
+// gradient bucket is bound); 1: every .grad is None; 2: anything else.
+PyObject* grad_state(PyObject*, PyObject* args) {
+  PyObject *params, *views;
+  if (!PyArg_ParseTuple(args, "O!O!", &PyTuple_Type, &params, &PyTuple_Type, &views))
+    return nullptr;
+  const Py_ssize_t n = PyTuple_GET_SIZE(params);
+  if (PyTuple_GET_SIZE(views) != n) {
+    PyErr_SetString(PyExc_ValueError, "grad_state: length mismatch");
+    return nullptr;
+  }
+  bool bound = true, none = true;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* t = PyTuple_GET_ITEM(params, i);
+    PyObject* v = PyTuple_GET_ITEM(views, i);
+    if (!THPVariable_Check(t) || !THPVariable_Check(v)) {
+      PyErr_SetString(PyExc_TypeError, "grad_state: expected tensors");
+      return nullptr;
+    }
+    const at::Tensor& g = THPVariable_Unpack(t).grad();
+    if (g.defined()) none = false;
+    if (!g.defined() || g.unsafeGetTensorImpl() != THPVariable_Unpack(v).unsafeGetTensorImpl())
+      bound = false;
+  }
+  return PyLong_FromLong(bound ? 0 : (none ? 1 : 2));
+}
+
+// bind_grads(params, views) -> None: params[i].grad = views[i] (leaf
+// parameters; the views are slices of one flat gradient bucket).
+PyObject* bind_grads(PyObject*, PyObject* args) {
+  PyObject *params, *views;
+  if (!PyArg_ParseTuple(args, "O!O!", &PyTuple_Type, &params, &PyTuple_Type, &views))
+    return nullptr;
+  const Py_ssize_t n = PyTuple_GET_SIZE(params);
+  if (PyTuple_GET_SIZE(views) != n) {
+    PyErr_SetString(PyExc_ValueError, "bind_grads: length mismatch");
+    return nullptr;
+  }
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* t = PyTuple_GET_ITEM(params, i);
+    PyObject* v = PyTuple_GET_ITEM(views, i);
+    if (!THPVariable_Check(t) || !THPVariable_Check(v)) {
+      PyErr_SetString(PyExc_TypeError, "bind_grads: expected tensors");
+      return nullptr;
+    }
+    const at::Tensor& x = THPVariable_Unpack(t);
+    const at::Tensor& g = THPVariable_Unpack(v);
+    if (g.sizes() != x.sizes() || g.scalar_type() != x.scalar_type() ||
+        g.device() != x.device()) {
+      PyErr_SetString(PyExc_ValueError, "bind_grads: gradient view does not match its parameter");
+      return nullptr;
+    }
+    x.mutable_grad() = g;
+  }
+  Py_RETURN_NONE;
+}
+
 PyMethodDef kMethods[] = {
+    {"grad_state", grad_state, METH_VARARGS, "is every .grad its bucket view / None"},
+    {"bind_grads", bind_grads, METH_VARARGS, ".grad = bucket view for every parameter"},
     {"valid_views", valid_views, METH_VARARGS, "arena validity check (see shim.cpp)"},
     {"bump_versions", bump_versions, METH_VARARGS, "autograd version bump of every tensor"},
     {nullptr, nullptr, 0, nullptr}};

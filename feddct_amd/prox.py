@@ -75,6 +75,29 @@ class _Prox(torch.autograd.Function):
         return (None, *grads_a, *grads_b)
 
 
+class _ProxFlat(torch.autograd.Function):
+    """The one-node form (r03): the parameters are not inputs of the graph
+    node, so a backward is ONE node instead of this node plus an
+    AccumulateGrad per parameter (200 for wrn16_8's client + global: ~0.6 ms
+    of autograd bookkeeping per training step).  Its backward accumulates the
+    gradients straight into flat gradient buckets whose slices are the
+    parameters' ``.grad`` — what AccumulateGrad does, in one launch."""
+
+    @staticmethod
+    def forward(ctx, term, anchor):
+        total = term.norms_forward()
+        ctx.term = term
+        return total
+
+    @staticmethod
+    def backward(ctx, gout):
+        if torch.is_grad_enabled():
+            raise RuntimeError("feddct_amd.prox: the one-node proximal term has no double "
+                               "backward; use proximal_term(..., flat_grads=False)")
+        ctx.term.accumulate_grads(gout)
+        return None, None
+
+
 class ProximalTerm:
     """Bound (client, global) pair: plan built once, reused every step."""
 
@@ -106,21 +129,109 @@ class ProximalTerm:
         segs = np.array([(o, m) for o, m, _ in slots], np.int64).reshape(-1, 2)
         with torch.cuda.device(self.ca.device):
             self.plan = _NormPlan(segs, layout.f32_numel)
+        self._flat = None   # gradient buckets of the one-node form, made on first use
+
+    # ------------------------------------------------- the one-node form --
+    def _flat_state(self):
+        if self._flat is None:
+            dev = self.ca.device
+            sides = []
+            for params, arena in ((list(self.client_model.parameters()), self.ca),
+                                  (list(self.global_model.parameters()), self.ga)):
+                keep = [(p, sl) for p, sl in zip(params, self.slots) if p.requires_grad]
+                buf = torch.zeros_like(arena.f32) if keep else None
+                views = tuple(buf[o:o + m].view(shape) for _, (o, m, shape) in keep)
+                sides.append((tuple(p for p, _ in keep), views, buf))
+            self._flat = (sides, torch.zeros((), device=dev, requires_grad=True),
+                          torch.empty(max(1, self.plan.nseg), dtype=torch.float32, device=dev))
+        return self._flat
+
+    def norms_forward(self) -> torch.Tensor:
+        _, _, norms = self._flat_state()
+        dev = self.ca.device
+        total = torch.empty((), dtype=torch.float32, device=dev)
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _lib.check(_lib.lib.fa_prox_norms(self.plan.handle, self.ca.ptr32, self.ga.ptr32,
+                                          norms.data_ptr(), total.data_ptr(), s),
+                   "fa_prox_norms")
+        return total
+
+    def accumulate_grads(self, gout: torch.Tensor) -> None:
+        """.grad += d term / d w for both models' parameters, through their
+        bound flat gradient buckets (one kernel)."""
+        from . import _fa_shim
+        sides, _, norms = self._flat_state()
+        dev = self.ca.device
+        gout = gout.to(device=dev, dtype=torch.float32).contiguous()
+        states = []
+        for params, views, buf in sides:
+            if buf is None:
+                states.append(None)
+                continue
+            st = _fa_shim.grad_state(params, views)
+            if st == 2:   # some .grad not bucket views: take them over, once
+                with torch.no_grad():
+                    for p, v in zip(params, views):
+                        if p.grad is None:
+                            v.zero_()
+                        elif p.grad is not v:
+                            v.copy_(p.grad)
+                _fa_shim.bind_grads(params, views)
+                st = 0
+            states.append(st)
+        live = [st for st in states if st is not None]
+        if not live:
+            return
+        acc = any(st == 0 for st in live)
+        if acc:   # a side whose .grad were all None starts from zero
+            for (params, views, buf), st in zip(sides, states):
+                if st == 1:
+                    buf.zero_()
+        (_, _, ba), (_, _, bb) = sides
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _lib.check(_lib.lib.fa_prox_grad_ex(
+            self.plan.handle, self.ca.ptr32, self.ga.ptr32, norms.data_ptr(), gout.data_ptr(),
+            1.0, ba.data_ptr() if ba is not None else self._scratch(dev).data_ptr(),
+            None if bb is None else bb.data_ptr(), _lib.FA_PROX_ACCUMULATE if acc else 0, s),
+            "fa_prox_grad_ex")
+        for (params, views, buf), st in zip(sides, states):
+            if st == 1:
+                _fa_shim.bind_grads(params, views)
+
+    def _scratch(self, dev):
+        """A write-only target for the client side when no client parameter
+        needs a gradient (the kernel always writes grad_a)."""
+        sc = getattr(self, "_sc", None)
+        if sc is None:
+            sc = self._sc = torch.empty_like(self.ca.f32)
+        return sc
 
     def valid(self) -> bool:
         return (getattr(self.client_model, "_fa_arena", None) is self.ca and self.ca.valid()
                 and getattr(self.global_model, "_fa_arena", None) is self.ga and self.ga.valid())
 
-    def __call__(self) -> torch.Tensor:
+    def __call__(self, flat_grads: bool = True) -> torch.Tensor:
+        if flat_grads:
+            _, anchor, _ = self._flat_state()
+            return _ProxFlat.apply(self, anchor)
         return _Prox.apply(self, *self.params)
 
 
-def proximal_term(client_model: torch.nn.Module, global_model: torch.nn.Module) -> torch.Tensor:
+def proximal_term(client_model: torch.nn.Module, global_model: torch.nn.Module,
+                  flat_grads: bool = True) -> torch.Tensor:
     """Σ_k ||w_k − w_t,k||₂ over zip(client.parameters(), global.parameters()),
     differentiable w.r.t. both (train_fedprox.py:113-115).  The bound term is
-    cached on the client module (no global registry)."""
+    cached on the client module (no global registry).
+
+    ``flat_grads=True`` (default): ``loss.backward()`` reaches ONE graph node,
+    whose backward adds the gradients into both models' ``.grad`` (made views
+    of a flat gradient bucket per model, rebound after ``zero_grad(
+    set_to_none=True)``), as autograd's accumulation would — for training
+    steps (train_fedprox.py:117-127).  ``torch.autograd.grad`` w.r.t. the
+    parameters, double backward and per-parameter gradient hooks need the
+    per-parameter node: ``flat_grads=False``."""
     cache = client_model.__dict__.setdefault("_fa_prox", {})
     t = cache.get(id(global_model))
     if t is None or t.global_model is not global_model or not t.valid():
         t = cache[id(global_model)] = ProximalTerm(client_model, global_model)
-    return t()
+    return t(flat_grads)

@@ -205,6 +205,21 @@ int fa_reduce(const fa_plan *plan, const float *const *c32,
               const int64_t *const *c64, int n, const float *weights,
               float *out32, int64_t *out64, unsigned flags, void *stream);
 
+/* fa_reduce with a caller-owned device pointer table: above
+ * FA_INLINE_CLIENTS clients the client pointers (and weights) travel in a
+ * device table; fa_reduce takes it from a library pool and uploads it with a
+ * host memcpy, fa_reduce_tab writes it into `table` (fa_table_bytes(n)
+ * bytes of device memory, 8-B aligned) with kernels launched on `stream` —
+ * no allocation and no host copy, so the call can be captured into a HIP
+ * graph (hipStreamBeginCapture) and replayed.  `table` must stay allocated
+ * and untouched while any launch or graph replay that uses it can run.
+ * table may be NULL when n <= FA_INLINE_CLIENTS. */
+size_t fa_table_bytes(int n);
+int fa_reduce_tab(const fa_plan *plan, const float *const *c32,
+                  const int64_t *const *c64, int n, const float *weights,
+                  void *table, float *out32, int64_t *out64, unsigned flags,
+                  void *stream);
+
 /* ---- chained segments: client shards reduced in the exact order ----------
  * The cascade walks the N clients in slot order with four
  * level accumulators; its state after rows 0..k-1 is those accumulators.
@@ -282,6 +297,12 @@ int fa_prox_norms(const fa_norm_plan *plan, const float *a, const float *b,
 int fa_prox_grad(const fa_norm_plan *plan, const float *a, const float *b,
                  const float *norms, const float *gout, float alpha,
                  float *grad_a, float *grad_b, void *stream);
+/* FA_PROX_ACCUMULATE: grad_a += (...), grad_b -= (...) instead (autograd's
+ * in-place gradient accumulation, for .grad tensors that are bucket views). */
+#define FA_PROX_ACCUMULATE 1u
+int fa_prox_grad_ex(const fa_norm_plan *plan, const float *a, const float *b,
+                    const float *norms, const float *gout, float alpha,
+                    float *grad_a, float *grad_b, unsigned flags, void *stream);
 
 /* Streaming copy (bandwidth ceiling calibration for the roofline). */
 int fa_copy_f32(const float *src, float *dst, int64_t numel, void *stream);

@@ -226,6 +226,8 @@ bool run_case(const Case& c, const Layout& L) {
           Rank& k = R[r];
           (void)hipSetDevice(0);
           k.rc = fa_comm_init_rank(W, r, uid, FA_COMM_UID_BYTES, &k.comm);
+          // the loopback pairs sends and receives on the host: never captured
+          if (!k.rc) k.rc = fa_comm_set_graphs(k.comm, 0);
           if (!k.rc) k.rc = create_plan(c, L, k);
           if (!k.rc) k.rc = hipStreamCreate(&k.st) == hipSuccess ? 0 : -1;
           if (!k.rc) {

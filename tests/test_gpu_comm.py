@@ -341,3 +341,74 @@ def test_python_chain_aggregator_one_rank_nccl():
         assert torch.equal(out64, want64)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("form", ["chained16", "blocked", "sharded", "rs_gather", "striped"])
+@pytest.mark.parametrize("n", [20, 300])
+def test_captured_rounds_replay_bit_exact(form, n):
+    """a native round's schedule is captured into a HIP
+    graph on its first step and replayed by one launch afterwards
+    (fa_comm_set_graphs).  The replays follow in-place changes of the client
+    buckets (the graph holds pointers, not values), a new output buffer is a
+    new capture, and every result equals the uncaptured executor's and one
+    GPU's reduce, bit for bit — at 300 slots too, where the tails and the
+    stripe take the graph's own device pointer tables."""
+    from feddct_amd import comm as C
+    torch.cuda.set_device(DEV)
+    man = load_manifest("wrnsl16_8_sf4_c10_main" if n > 20 else "wrn16_8_c10")
+    layout = BucketLayout.from_manifest(man)
+    clients = make_clients(layout, man, range(n), DEV, mode=synth.MODE_ADVERSARIAL)
+    l32, l64 = [c[0] for c in clients], [c[1] for c in clients]
+    mask = _layout_pad_mask(layout)
+
+    def make(comm, o32, o64):
+        kw = dict(final="reduce", root=0)
+        if form == "chained16":
+            return C.NativeChainedAggregator(layout, l32, l64, n, o32, o64, comm, nchunks=16, **kw)
+        if form == "blocked":
+            return C.NativeBlockedAggregator(layout, l32, l64, n, o32, o64, comm, **kw)
+        if form == "striped":
+            return C.NativeStripedAggregator(layout, l32, l64, n, o32, o64, comm, **kw)
+        ex = C.FA_XCHG_RS_GATHER if form == "rs_gather" else C.FA_XCHG_REDUCE
+        return C.NativeShardedAggregator(layout, l32, l64, n, o32, o64, comm, nchunks=8,
+                                         exchange=ex, **kw)
+
+    results = {}
+    for graphs in (False, True):
+        comm = C.Comm.single()
+        comm.set_graphs(graphs)
+        o32 = torch.full_like(clients[0][0], float("nan"))
+        o64 = torch.full_like(clients[0][1], -7)
+        agg = make(comm, o32, o64)
+        got = []
+        for step in range(3):
+            if step == 2:          # the clients change in place between rounds
+                for c in clients:
+                    c[0].mul_(-0.5)
+                    c[1].add_(3)
+            agg.step()
+            torch.cuda.synchronize()
+            got.append((o32[mask].clone(), o64.clone()))
+        if step == 2:
+            for c in clients:       # restore for the other executor
+                c[0].mul_(-2.0)
+                c[1].sub_(3)
+        # a new output buffer: another capture, same bits
+        p32 = torch.full_like(o32, float("nan"))
+        p64 = torch.full_like(o64, -7)
+        make(comm, p32, p64).step()
+        torch.cuda.synchronize()
+        got.append((p32[mask].clone(), p64.clone()))
+        results[graphs] = got
+        comm.close()
+    want32, want64 = _single_gpu(layout, clients)
+    for graphs, got in results.items():
+        for i, (g32, g64) in enumerate(got):
+            if i == 2:
+                continue
+            assert torch.equal(g32.view(torch.int32), want32[mask].view(torch.int32)), (graphs, i)
+            assert torch.equal(g64, want64), (graphs, i)
+    for a, b in zip(results[False], results[True]):
+        assert torch.equal(a[0].view(torch.int32), b[0].view(torch.int32))
+        assert torch.equal(a[1], b[1])
+    assert not torch.equal(results[True][2][0], results[True][1][0])  # step 2 saw the change

@@ -261,8 +261,9 @@ def test_broadcast_forms_and_bcast_only(lib, n, form):
     if form.endswith("noxcd"):
         fl |= lib.FA_PLAN_TUNE_BCAST_NOXCD
     kw = dict(order=lib.FA_ORDER_TORCH_GPU, n=n) if form == "tgpu" else {}
-    if form == "tgpu" and n < 2:
-        pytest.skip("the torch-GPU order needs N >= 2")
+    if form == "tgpu" and not 2 <= n <= 128:
+        pytest.skip("the torch-GPU order: N >= 2, and no row split past 16 warps (N=300 "
+                    "splits the 7-element key 32 ways)")
     plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
                     flags=fl, **kw)
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -624,6 +625,37 @@ def test_proximal_term_matches_reference_loop(same):
         torch.testing.assert_close(p.grad, p_ref.grad, rtol=1e-5, atol=1e-8, msg=n)
     for p, p_ref in zip(g.parameters(), g_ref.parameters()):
         torch.testing.assert_close(p.grad, p_ref.grad, rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("set_to_none", [True, False])
+def test_proximal_term_flat_grads_in_a_training_loop(set_to_none):
+    """The one-node proximal term (r03, flat_grads=True) inside the
+    reference's step (train_fedprox.py:112-127): task loss + mu/2 * term,
+    gradients accumulated over two iterations before each optimizer step
+    (iters_to_accumulate), zero_grad either way.  Gradients and parameters
+    track the per-parameter autograd form step by step."""
+    from feddct_amd.prox import proximal_term
+    runs = {}
+    for flat in (True, False):
+        c, g = _prox_models(2)
+        opt = torch.optim.SGD(c.parameters(), lr=0.05, momentum=0.9)
+        gen = torch.Generator(device=DEV).manual_seed(3)
+        hist = []
+        for it in range(6):
+            x = torch.randn(4, 7, device=DEV, generator=gen)
+            loss = c[3](x).square().sum() + 0.005 * proximal_term(c, g, flat_grads=flat)
+            loss.backward()
+            if it % 2 == 1:
+                hist.append([p.grad.clone() for p in c.parameters()]
+                            + [p.grad.clone() for p in g.parameters()])
+                opt.step()
+                opt.zero_grad(set_to_none=set_to_none)
+        runs[flat] = (hist, [p.detach().clone() for p in c.parameters()])
+    for ga, gb in zip(runs[True][0], runs[False][0]):
+        for a, b in zip(ga, gb):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+    for a, b in zip(runs[True][1], runs[False][1]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
 
 
 def test_proximal_term_tracks_training_and_aggregation():

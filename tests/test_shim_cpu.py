@@ -1,0 +1,41 @@
+"""CPU: the _fa_shim gradient-binding helpers behind the one-node proximal
+term (feddct_amd/prox.py, r03): .grad made views of a flat bucket, the state
+check, and autograd's in-place accumulation landing in the bucket."""
+import pytest
+import torch
+
+_fa_shim = pytest.importorskip("feddct_amd._fa_shim")
+
+
+def _params():
+    ps = tuple(torch.nn.Parameter(torch.randn(3, 4)) for _ in range(3))
+    buf = torch.zeros(40)
+    views = tuple(buf[i * 12:(i + 1) * 12].view(3, 4) for i in range(3))
+    return ps, buf, views
+
+
+def test_grad_state_and_binding():
+    ps, buf, views = _params()
+    assert _fa_shim.grad_state(ps, views) == 1          # all None
+    _fa_shim.bind_grads(ps, views)
+    assert _fa_shim.grad_state(ps, views) == 0          # all bound
+    assert all(p.grad.data_ptr() == v.data_ptr() for p, v in zip(ps, views))
+    ps[0].grad = None
+    assert _fa_shim.grad_state(ps, views) == 2          # mixed
+    ps[0].grad = torch.zeros(3, 4)
+    assert _fa_shim.grad_state(ps, views) == 2          # a grad that is not the view
+
+
+def test_autograd_accumulates_into_the_bucket():
+    ps, buf, views = _params()
+    _fa_shim.bind_grads(ps, views)
+    (ps[1] * 2).sum().backward()
+    (ps[1] * 3).sum().backward()
+    assert torch.equal(buf[12:24], torch.full((12,), 5.0))
+    assert _fa_shim.grad_state(ps, views) == 0
+
+
+def test_bind_grads_refuses_mismatched_views():
+    ps, buf, _ = _params()
+    with pytest.raises(ValueError):
+        _fa_shim.bind_grads(ps, tuple(buf[:12] for _ in ps))

@@ -5,7 +5,7 @@ before any xGMI traffic — the local floor of bench N>1.  One JSON line per
 form: GPU time per step (HIP events over K steps) and host issue time per
 step (wall time of the K step() calls, no sync inside).
 
-    python tools/native_round_cost.py [K]
+    python tools/native_round_cost.py [K] [--no-graphs]
 """
 import json
 import os
@@ -38,7 +38,7 @@ def timed(fn, k, w=10):
 
 
 def main():
-    k = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    k = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 50
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     man = load_manifest("wrn16_8_c10")
@@ -48,7 +48,9 @@ def main():
     l32, l64 = [c[0] for c in cl], [c[1] for c in cl]
     ref32, ref64 = torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])
     red = Reducer(lay, cl, ref32, ref64)
+    graphs = "--no-graphs" not in sys.argv   # r03: rounds replayed from captured graphs
     comm = C.Comm.single()
+    comm.set_graphs(graphs)
     forms = {"plain_reduce": lambda o32, o64: Reducer(lay, cl, o32, o64, plan=red.plan)}
     forms["blocked"] = lambda o32, o64: C.NativeBlockedAggregator(
         lay, l32, l64, n, o32, o64, comm, final="reduce", root=0).step
@@ -75,7 +77,8 @@ def main():
         us, host = timed(fn, k)
         exact = bool(torch.equal(o32[mask].view(torch.int32), ref32[mask].view(torch.int32))
                      and torch.equal(o64, ref64))
-        print(json.dumps({"form": name, "gpu_us": round(us, 1), "host_issue_us": round(host, 1),
+        print(json.dumps({"form": name, "graphs": graphs, "gpu_us": round(us, 1),
+                          "host_issue_us": round(host, 1),
                           "GBps": round(nb / us / 1e3, 1), "bit_exact": exact}), flush=True)
     comm.close()
 

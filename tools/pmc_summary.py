@@ -13,6 +13,7 @@ import glob
 import json
 import os
 import sys
+import time
 
 KERNEL = "reduce_kernel"
 
@@ -63,6 +64,10 @@ def main():
         "bench_kernel_us_same_run": (bench_line or {}).get("roofline", {}).get("kernel_us"),
         "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --kernel-only "
                    "--no-cpu-baseline --steps 100 --warmup 100",
+        # where and when the counters were taken (the bench line cites them)
+        "date_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+        "host": os.uname().nodename,
+        "gpu": (bench_line or {}).get("gpu"),
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1)

@@ -3,7 +3,7 @@
 // same allocation scheme.  Standalone lab binary (not the product):
 //   hipcc --offload-arch=gfx950 -O3 -o tools/reducelab tools/reducelab.hip
 // One JSON line per (variant, N, round); GB/s counts N inputs + 1 output.
-// `reducelab hashed`: every buffer filled with non-zero hashed values first
+// `reducelab hashed [pipe]`: every buffer filled with non-zero hashed values first
 // (zero-filled buffers stream faster on this chip than real data,
 // tools/bcastlab.hip; the r02 numbers before this option were on zeros).
 #include <hip/hip_runtime.h>
@@ -106,6 +106,44 @@ __global__ __launch_bounds__(256) void nsum_park(Ptrs p, float* out, int64_t nv,
   }
 }
 
+// r03: G consecutive tiles per workgroup, software-
+// pipelined across tiles — tile g's loads (all N*U) are issued, THEN tile
+// g-1's result is stored, so every store leaves behind a full tile of loads
+// in flight (the write does not wait behind its own tile's reads).
+template <int N, int U, int G>
+__global__ __launch_bounds__(256) void nsum_pipe(Ptrs p, float* out, int64_t nv, int ntiles) {
+  const int t0 = blockIdx.x * G;
+  f4 prev[U];
+  int64_t prevb = -1;
+#pragma unroll 1
+  for (int g = 0; g < G; ++g) {
+    const int t = t0 + g;
+    if (t >= ntiles) break;
+    const int64_t b = (int64_t)t * U * 256 + threadIdx.x;
+    f4 x[N][U];
+#pragma unroll
+    for (int c = 0; c < N; ++c)
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[c][u] = ld(p.c[c], b + u * 256);
+    if (prevb >= 0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) st(out, prevb + u * 256, prev[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f4 acc = f4{0, 0, 0, 0};
+#pragma unroll
+      for (int c = 0; c < N; ++c) acc += x[c][u];
+      prev[u] = acc;
+    }
+    prevb = b;
+  }
+  if (prevb >= 0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) st(out, prevb + u * 256, prev[u]);
+  }
+}
+
 __global__ __launch_bounds__(256) void copy1(const float* s, float* d, int64_t nv) {
   const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (v < nv) st(d, v, ld(s, v));
@@ -201,6 +239,31 @@ int main(int argc, char** argv) {
 #define PARK(N, G)                                                                               \
   rep("park_G" #G, N,                                                                            \
       time_us([&] { nsum_park<N, G><<<(t1 + G - 1) / G, 256>>>(p, out, nv, t1); }, 20), 1);
+#define PIPE(N, U, G, T)                                                                         \
+  rep("pipe_U" #U "_G" #G "_rot2", N, time_us([&] {                                              \
+        flip ^= 1;                                                                               \
+        nsum_pipe<N, U, G><<<(T + G - 1) / G, 256>>>(flip ? p2 : p, flip ? out2 : out, nv, T);   \
+      }, 20), 1);
+  if (argc > 2 && strcmp(argv[2], "pipe") == 0) {   // r03: the cross-tile pipeline A/B only
+    for (int r = 0; r < 3; ++r) {
+      rep("rw_U1_rot2", 5, time_us([&] {
+            flip ^= 1;
+            nsum<5, 1, 0><<<t1, 256>>>(flip ? p2 : p, flip ? out2 : out, nv, t1, 1);
+          }, 20), 1);
+      rep("rw_U2_rot2", 5, time_us([&] {
+            flip ^= 1;
+            nsum<5, 2, 0><<<t2, 256>>>(flip ? p2 : p, flip ? out2 : out, nv, t2, 1);
+          }, 20), 1);
+      PIPE(5, 1, 2, t1) PIPE(5, 1, 4, t1) PIPE(5, 1, 8, t1)
+      PIPE(5, 2, 2, t2) PIPE(5, 2, 4, t2)
+      PIPE(20, 1, 2, t1) PIPE(20, 2, 2, t2)
+      rep("rw_U2_rot2", 20, time_us([&] {
+            flip ^= 1;
+            nsum<20, 2, 0><<<t2, 256>>>(flip ? p2 : p, flip ? out2 : out, nv, t2, 1);
+          }, 20), 1);
+    }
+    return 0;
+  }
   for (int r = 0; r < 2; ++r) {
     rep("copy1", 1, time_us([&] { copy1<<<t1, 256>>>(bufs[0], out, nv); }, 20), 1);
     RUN(5) RUN(20)
