@@ -49,7 +49,7 @@ FA_PLAN_TUNE_TGPU_NARROW = 0x200000
 FA_PLAN_TUNE_BCAST_TILES = 0x400000
 FA_PLAN_TUNE_BCAST_TABLE = 0x800000
 FA_PLAN_TUNE_BCAST_REVERSE = 0x1000000
-FA_PLAN_TUNE_BCAST_NOXCD = 0x2000000
+FA_PLAN_TUNE_BCAST_XCD = 0x2000000
 FA_ORDER_TORCH_CPU = 0
 FA_ORDER_TORCH_GPU = 1
 

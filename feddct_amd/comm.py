@@ -185,8 +185,8 @@ class Comm:
         return cls(1, 0, unique_id())
 
     def set_graphs(self, enable: bool) -> None:
-        """Captured rounds on / off (fedagg_comm.h fa_comm_set_graphs; on by
-        default): each round's schedule replayed from a HIP graph."""
+        """Captured rounds on / off (fedagg_comm.h fa_comm_set_graphs; off by
+        default, see there): each round's schedule replayed from a HIP graph."""
         _lib.check(lib().fa_comm_set_graphs(self.handle, int(bool(enable))),
                    "fa_comm_set_graphs")
 

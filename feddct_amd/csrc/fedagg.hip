@@ -547,10 +547,10 @@ __global__ __launch_bounds__(kBlock) void bcast_kernel(BcastArgs a, int64_t nume
                                                        uint32_t parts, uint32_t groups,
                                                        uint32_t gsize) {
   const int64_t nv = numel / 4;
-  const uint32_t total = bcast_blocks(parts, groups, true);
+  const uint32_t total = bcast_blocks(parts, groups, false);
   for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
     uint32_t p, g;
-    if (!bcast_part(v, parts, groups, true, &p, &g)) continue;
+    if (!bcast_part(v, parts, groups, false, &p, &g)) continue;
     const int c0 = (int)(g * gsize);
     const int c1 = min(a.n, c0 + (int)gsize);
     const int64_t v0 = (int64_t)p * 2 * kBlock + threadIdx.x, v1 = v0 + kBlock;
@@ -857,7 +857,10 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
                     : (pflags & FA_PLAN_TUNE_BATCH8)  ? 8
                     : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (small ? 8 : 16);
   const unsigned cap = (pflags >> 8) & 0xFu;  // FA_PLAN_TUNE_BLOCKS_PER_CU(c)
-  t_dyn_lds = cap ? (160u * 1024u / cap) & ~1023u : 0;
+  // (the scalar tiles' static LDS stage counts against the cap's share)
+  t_dyn_lds = cap ? (size_t)std::max<long>(
+                        0, (long)((160u * 1024u / cap) & ~1023u) - (long)(kStageFloats * 4))
+                  : 0;
   t_grid_cap = 256 * (int)((pflags >> 12) & 0xFu);  // FA_PLAN_TUNE_PERSIST(k)
   switch (vec_u) {
     case 1:
@@ -1343,7 +1346,7 @@ hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, b
     const int64_t i = plan->has64 ? plan->info.i64_numel : 0;
     const int64_t parts =
         f > 0 ? std::max<int64_t>(1, (f / 4 + 2 * kBlock - 1) / (2 * kBlock)) : 0;
-    const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_NOXCD) ? 0 : 1;
+    const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_XCD) ? 1 : 0;
     const int64_t np = parts + (i > 0 ? 1 : 0);
     if ((np + 8) * groups > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
     const int64_t total = bcast_blocks((uint32_t)np, groups, xcd);
@@ -1354,7 +1357,7 @@ hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, b
   } else if (ntiles > 0) {
     // ntiles * groups < 2^32: n clients of ntiles 4-16 KB tiles would
     // outgrow any GPU's memory long before
-    const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_NOXCD) ? 0 : 1;
+    const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_XCD) ? 1 : 0;
     const unsigned grid =
         (unsigned)std::min<int64_t>(bcast_blocks((uint32_t)ntiles, groups, xcd), 1ll << 30);
     hipLaunchKernelGGL(bcast_group_kernel, dim3(grid), dim3(kBlock), 0, st, a, groups, gsize,
@@ -1688,7 +1691,7 @@ int fa_broadcast_f32(const float* src, float* const* dst, int n, int64_t numel, 
     if ((parts + 8) * groups > (int64_t)UINT32_MAX)
       return set_err(FA_E_RANGE, "fa_broadcast_f32: numel=%lld", (long long)numel);
     const unsigned grid =
-        (unsigned)std::min<int64_t>(bcast_blocks((uint32_t)parts, groups, true), 1ll << 30);
+        (unsigned)std::min<int64_t>(bcast_blocks((uint32_t)parts, groups, false), 1ll << 30);
     hipLaunchKernelGGL(bcast_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a, numel,
                        (uint32_t)parts, groups, gsize);
     HIP_TRY(hipGetLastError());

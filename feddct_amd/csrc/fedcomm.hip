@@ -65,7 +65,7 @@ struct fa_comm {
   ncclComm_t nc = nullptr;
   int nranks = 0, rank = 0, device = 0;
   hipStream_t cs = nullptr;  // communication stream
-  bool graphs = true;        // replay rounds from captured HIP graphs (fa_comm_set_graphs)
+  bool graphs = false;       // replay rounds from captured HIP graphs (fa_comm_set_graphs)
 };
 
 namespace {
@@ -1398,7 +1398,13 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
 // captured into a HIP graph once per (root, weights, buffers) and replayed by
 // one hipGraphLaunch on the caller's stream — the executor issued ~12 µs of
 // host calls per step (chained at 16 chunks: 190 µs of host issue per round,
-// profiles/r02_native_round_cost.jsonl).  The capture runs on the plan's own
+// profiles/r02_native_round_cost.jsonl).  Measured r03 on one rank
+// (profiles/r03_native_round_cost_{graphs,nographs}.jsonl): the replay's
+// host time is still ~9 µs per node (chained_16 184 vs 192 µs: ROCm 7.0's
+// graph launch submits node by node), and its GPU time gains on the blocked
+// and striped rounds (244 vs 259, 188 vs 214 µs) but loses where the
+// schedule overlaps its two streams (sharded 357 vs 290 µs, chained 181 vs
+// 171 µs) — so it is off by default (fa_comm_set_graphs).  The capture runs on the plan's own
 // stream (the caller's may be the legacy null stream, which cannot be
 // captured); kernels over more than FA_INLINE_CLIENTS rows take pointer
 // tables the graph owns (fa_reduce_tab).  A round whose other kernels exceed

@@ -483,13 +483,69 @@ __device__ float inner_seq(const Src& src, int64_t e, int n) {
   return fin;
 }
 
+// Scalar tiles (ILP-4 tails, unaligned cascade columns, M == 1 keys, int64
+// keys) hold 1-256 columns of a few tensors, each column walked over the N
+// rows in its order by one thread: N dependent round trips to HBM per thread
+// made them latency-bound — resnet110sl sf4 at N = 25 (1,240 scalar tiles,
+// 0.75 % of the elements) spent 20.6 us in them against 21.5 us for all its
+// vector tiles (r03, bench other_configs).  When the tile's N x count values
+// fit kStageFloats, the whole workgroup first stages them into LDS with
+// independent loads (the value each order reads: the fp32 value, weighted
+// products and int64 -> fp32 conversions applied as the direct path applies
+// them), then each column's thread runs its order from LDS.  32 KB of LDS
+// per workgroup costs no occupancy: the reduce kernels are VGPR-bound at
+// 3 workgroups per CU (156-170 VGPRs; 3 x 32 KB < 160 KB).
+constexpr int kStageFloats = 8192;
+struct SrcLds {
+  const float* stage;
+  int count;
+  int64_t start;
+  __device__ float operator()(int i, int64_t e) const {
+    return stage[i * count + (int)(e - start)];
+  }
+};
+
 template <bool WEIGHTED>
 __device__ void tile_scalar(KArgs& a, Tile t) {
+  __shared__ float stage[kStageFloats];
   const int j = threadIdx.x;
+  const int n = a.n;
+  const bool staged = n * t.count <= kStageFloats;
+  if (staged) {
+    const int tot = n * t.count;
+    const bool f32 = t.kind <= K_F32_INNER;
+    for (int k = j; k < tot; k += kBlock) {
+      const int i = k / t.count;
+      const int64_t e = t.start + (k - i * t.count);
+      stage[k] = f32 ? SrcF32{a, WEIGHTED}(i, e) : SrcI64{a}(i, e);
+    }
+    __syncthreads();
+  }
   if (j >= t.count) return;
   const int64_t e = t.start + j;
-  const int n = a.n;
   const float fn = (float)n;
+  if (staged) {
+    SrcLds src{stage, t.count, t.start};
+    float s;
+    const int k = t.kind;
+    if (k == K_F32_CASC_S || k == K_I64_CASC) s = cascade_seq(src, e, 0, 1, n);
+    else if (k == K_F32_ILP4 || k == K_I64_ILP4) s = ilp4_seq(src, e, 0, 1, n);
+    else s = inner_seq(src, e, n);
+    s = __fadd_rn(0.f, s);
+    if (k <= K_F32_INNER) {
+      const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
+      const float r = sum_only ? s : __fdiv_rn(s, fn);
+      a.out32[e] = r;
+      if (a.flags & FA_F_BCAST)
+        for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
+    } else {
+      const int64_t r = (int64_t)__fdiv_rn(s, fn);
+      a.out64[e] = r;
+      if (a.flags & FA_F_BCAST)
+        for (int i = 0; i < n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
+    }
+    return;
+  }
   if (t.kind <= K_F32_INNER) {
     SrcF32 src{a, WEIGHTED};
     float s;

@@ -106,9 +106,11 @@ extern "C" {
                                               their buckets flat by default    */
 #define FA_PLAN_TUNE_BCAST_REVERSE 0x1000000u /* tuning: the flat broadcast walks the
                                                  bucket from its end            */
-#define FA_PLAN_TUNE_BCAST_NOXCD 0x2000000u /* tuning: the flat broadcast's client
-                                                groups of a part on consecutive
-                                                blocks (r02 form) instead of one XCD */
+#define FA_PLAN_TUNE_BCAST_XCD 0x2000000u /* tuning: the broadcast's client groups
+                                              of a part on one XCD (blocks b, b+8,
+                                              ...: one source fetch) instead of on
+                                              consecutive blocks (measured r03: the
+                                              round 3.7 % slower, kept for A/B)   */
 #define FA_PLAN_TUNE_BCAST_TILES 0x400000u /* tuning: FA_F_BCAST as one workgroup per
                                               tile writing every client (r01 form) */
 #define FA_PLAN_TUNE_TGPU_NARROW 0x200000u /* tuning: torch-GPU order, S = 1 tensors in

@@ -64,12 +64,16 @@ int fa_comm_init_rank(int nranks, int rank, const unsigned char *id, int len,
 int fa_comm_init(int ndev, const int *devs, fa_comm **comms);
 int fa_comm_destroy(fa_comm *comm);
 int fa_comm_info(const fa_comm *comm, int *nranks, int *rank, int *device);
-/* Captured rounds (default on): in the one-process-per-GPU model each
+/* Captured rounds (default OFF; measured r03: a replay still costs ~9 µs of
+ * host time per graph node on ROCm 7.0, and the replay loses the schedule's
+ * two-stream overlap — faster for the blocked and striped rounds on one rank,
+ * slower for the sharded and chained ones): in the
+ * one-process-per-GPU model each
  * round's whole schedule — RCCL groups, kernels, stream joins — is captured
  * into a HIP graph the first time a plan runs with a given (root, weights,
  * buffer pointers) and replayed by one graph launch on the caller's stream
- * afterwards (up to 4 such graphs per plan, most recently used kept).  Off:
- * every round re-issues its schedule from the host.  Rounds whose kernels
+ * afterwards (up to 4 such graphs per plan, most recently used kept).  Off
+ * (default): every round re-issues its schedule from the host.  Rounds whose kernels
  * cannot be captured (a rank holding more than FA_INLINE_CLIENTS slots) or
  * whose capture the runtime refuses run uncaptured either way. */
 int fa_comm_set_graphs(fa_comm *comm, int enable);

@@ -244,12 +244,12 @@ def test_bcast_of_a_partial_plan_leaves_other_keys_alone(lib, which):
 
 
 @pytest.mark.parametrize("n", [1, 7, 20, 21, 300])
-@pytest.mark.parametrize("form", ["flat", "flat_noxcd", "table", "table_noxcd", "tgpu"])
+@pytest.mark.parametrize("form", ["flat", "flat_xcd", "table", "table_xcd", "tgpu"])
 def test_broadcast_forms_and_bcast_only(lib, n, form):
     """Every broadcast form writes the global state into every client —
     FA_F_BCAST after the reduce and FA_F_BCAST_ONLY alone (the reference's
-    initial sync, train_fedavg.py:244-250) — with XCD-paired client groups
-    (default, r03) and r02's consecutive groups, client counts that leave a
+    initial sync, train_fedavg.py:244-250) — with consecutive client groups
+    (default) and XCD-paired ones (tuning, r03), client counts that leave a
     short last group, and part counts that are not a multiple of 8."""
     from feddct_amd._lib import FA_F_BCAST, FA_F_BCAST_ONLY
     man = _rand_manifest(None, [100, 4096, 7, 3000, 1, 64, 20000])
@@ -258,8 +258,8 @@ def test_broadcast_forms_and_bcast_only(lib, n, form):
     fl = lib.FA_PLAN_GAPS_ARE_PADDING
     if form.startswith("table"):
         fl |= lib.FA_PLAN_TUNE_BCAST_TABLE
-    if form.endswith("noxcd"):
-        fl |= lib.FA_PLAN_TUNE_BCAST_NOXCD
+    if form.endswith("xcd"):
+        fl |= lib.FA_PLAN_TUNE_BCAST_XCD
     kw = dict(order=lib.FA_ORDER_TORCH_GPU, n=n) if form == "tgpu" else {}
     if form == "tgpu" and not 2 <= n <= 128:
         pytest.skip("the torch-GPU order: N >= 2, and no row split past 16 warps (N=300 "

@@ -16,7 +16,7 @@ import bench  # noqa: E402
 
 
 def main():
-    parts = sys.argv[1:] or ["other", "next"]
+    parts = [p for a in sys.argv[1:] for p in a.split(":")] or ["other", "next"]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     if "other" in parts:

@@ -3,9 +3,9 @@ train_fedavg.py:145-149) against its two kernels alone, in ONE process,
 interleaved, HIP events:
 
   reduce          fa_reduce, no broadcast
-  bcast[_noxcd]   FA_F_BCAST_ONLY: the broadcast launch alone (XCD-paired
-                  client groups, default / r02's consecutive groups)
-  round[_noxcd]   FA_F_BCAST: reduce + broadcast launch
+  bcast[_xcd]     FA_F_BCAST_ONLY: the broadcast launch alone (consecutive
+                  client groups, the default / XCD-paired groups)
+  round[_xcd]   FA_F_BCAST: reduce + broadcast launch
   round_st_plain  the reduce's result stores temporal (the broadcast's source
                   may stay in the MALL)
 
@@ -39,15 +39,15 @@ def main():
         return _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
                          flags=_lib.FA_PLAN_GAPS_ARE_PADDING | fl)
 
-    NX = _lib.FA_PLAN_TUNE_BCAST_NOXCD
+    XC = _lib.FA_PLAN_TUNE_BCAST_XCD
     B, BO = _lib.FA_F_BCAST, _lib.FA_F_BCAST_ONLY
-    p0, pnx, pst = plan(), plan(NX), plan(_lib.FA_PLAN_TUNE_ST_PLAIN)
+    p0, pnx, pst = plan(), plan(XC), plan(_lib.FA_PLAN_TUNE_ST_PLAIN)
     v = {
         "reduce": Reducer(lay, cl, o32, o64, plan=p0),
         "bcast": Reducer(lay, cl, o32, o64, flags=BO, plan=p0),
-        "bcast_noxcd": Reducer(lay, cl, o32, o64, flags=BO, plan=pnx),
+        "bcast_xcd": Reducer(lay, cl, o32, o64, flags=BO, plan=pnx),
         "round": Reducer(lay, cl, o32, o64, flags=B, plan=p0),
-        "round_noxcd": Reducer(lay, cl, o32, o64, flags=B, plan=pnx),
+        "round_xcd": Reducer(lay, cl, o32, o64, flags=B, plan=pnx),
         "round_st_plain": Reducer(lay, cl, o32, o64, flags=B, plan=pst),
     }
     times = {k: [] for k in v}
@@ -71,8 +71,8 @@ def main():
                           "us_min": round(ts[0], 2)}), flush=True)
     print(json.dumps({"exp": "round_summary",
                       "round_over_sum": round(med["round"] / (med["reduce"] + med["bcast"]), 4),
-                      "noxcd_round_over_sum": round(med["round_noxcd"] /
-                                                    (med["reduce"] + med["bcast_noxcd"]), 4)}),
+                      "xcd_round_over_sum": round(med["round_xcd"] /
+                                                    (med["reduce"] + med["bcast_xcd"]), 4)}),
           flush=True)
 
 
