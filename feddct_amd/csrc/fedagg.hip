@@ -104,8 +104,14 @@ __global__ __launch_bounds__(kBlock) void bcast_tiles_kernel(ReduceArgs args) {
         }
       }
     } else if ((int)threadIdx.x < t.count) {
-      const int64_t e = t.start + threadIdx.x;
-      if (!kind_is64(t.kind)) {
+      int64_t e = t.start + threadIdx.x;
+      bool is64 = kind_is64(t.kind);
+      if ((t.kind & 0xFF) == K_SCALAR_PACKED) {
+        const int64_t ent = a.sidx[e];
+        e = ent >> 4;
+        is64 = kind_is64((int)(ent & 15));
+      }
+      if (!is64) {
         const float r = a.out32[e];
         for (int i = 0; i < a.n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
       } else {
@@ -182,8 +188,14 @@ __global__ __launch_bounds__(kBlock) void bcast_group_kernel(ReduceArgs args, ui
         }
       }
     } else if ((int)threadIdx.x < t.count) {
-      const int64_t e = t.start + threadIdx.x;
-      if (!kind_is64(t.kind)) {
+      int64_t e = t.start + threadIdx.x;
+      bool is64 = kind_is64(t.kind);
+      if (kb == K_SCALAR_PACKED) {  // a packed column: its element and kind
+        const int64_t ent = a.sidx[e];
+        e = ent >> 4;
+        is64 = kind_is64((int)(ent & 15));
+      }
+      if (!is64) {
         const float r = a.out32[e];
         for (int c = c0; c < c1; ++c) const_cast<float*>(cptr32(a, c))[e] = r;
       } else {
@@ -660,6 +672,10 @@ struct fa_plan {
   Tile* d_tiles_alt = nullptr;
   int ntiles_alt = 0;
   int nscalar_alt = 0;
+  // the device tables' own counts: their scalar tiles are packed (r03,
+  // K_SCALAR_PACKED; info.* keep the host view of the layout's tiles)
+  int nt_dev = 0, ns_dev = 0, nt_alt_dev = 0, ns_alt_dev = 0;
+  int64_t* d_sidx = nullptr;  // packed scalar columns: (element << 4) | kind
   unsigned flags = 0;
   bool has32 = false;  // the tile table touches the fp32 bucket
   bool has64 = false;  // ... the int64 bucket
@@ -984,6 +1000,79 @@ hipError_t table_fill(void* dst, const std::vector<char>& host, hipStream_t st) 
 }
 }  // namespace
 
+namespace {
+// The device form of a host tile table: its scalar tiles' columns, sorted by
+// kind (a wave then mostly runs one order), packed kPackCols per K_SCALAR_PACKED
+// tile with their entries appended to `sidx`; the vector tiles follow
+// unchanged.  *nscalar = packed tiles (they lead the table, as the scalar
+// tiles did).
+std::vector<Tile> pack_scalar(const std::vector<Tile>& t, std::vector<int64_t>* sidx,
+                              int* nscalar, unsigned flags) {
+  // tuning: FA_PLAN_TUNE_PACK(c) -> kPackCols >> c columns per tile,
+  // FA_PLAN_TUNE_SCALAR_LAST -> the packed tiles after the vector tiles
+  const int pack = kPackCols >> ((flags >> 26) & 3u);
+  const bool last = (flags & FA_PLAN_TUNE_SCALAR_LAST) != 0;
+  std::vector<std::pair<int, int64_t>> cols;
+  std::vector<Tile> vec;
+  for (const Tile& x : t) {
+    if (x.kind == K_F32_VEC) {
+      vec.push_back(x);
+      continue;
+    }
+    for (int32_t c = 0; c < x.count; ++c) cols.emplace_back(x.kind, x.start + c);
+  }
+  std::stable_sort(cols.begin(), cols.end(),
+                   [](const std::pair<int, int64_t>& u, const std::pair<int, int64_t>& v) {
+                     return u.first < v.first;
+                   });
+  std::vector<Tile> out;
+  const int64_t base = (int64_t)sidx->size();
+  for (const auto& c : cols) sidx->push_back((c.second << 4) | c.first);
+  for (size_t c = 0; c < cols.size(); c += pack)
+    out.push_back(Tile{base + (int64_t)c, (int32_t)std::min<size_t>(pack, cols.size() - c),
+                       K_SCALAR_PACKED});
+  if (last) {
+    *nscalar = 0;
+    vec.insert(vec.end(), out.begin(), out.end());
+    return vec;
+  }
+  *nscalar = (int)out.size();
+  out.insert(out.end(), vec.begin(), vec.end());
+  return out;
+}
+
+// Upload a CPU-order plan's device tables (main + optional alt) and the
+// shared scalar index.
+hipError_t upload_tables(fa_plan* p, const std::vector<Tile>& tiles,
+                         const std::vector<Tile>& alt) {
+  std::vector<int64_t> sidx;
+  const std::vector<Tile> dm = pack_scalar(tiles, &sidx, &p->ns_dev, p->flags);
+  p->nt_dev = (int)dm.size();
+  std::vector<Tile> da;
+  if (!alt.empty()) {
+    da = pack_scalar(alt, &sidx, &p->ns_alt_dev, p->flags);
+    p->nt_alt_dev = (int)da.size();
+  }
+  hipError_t e = hipSuccess;
+  if (!dm.empty()) {
+    e = hipMalloc(&p->d_tiles, dm.size() * sizeof(Tile));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_tiles, dm.data(), dm.size() * sizeof(Tile), hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess && !da.empty()) {
+    e = hipMalloc(&p->d_tiles_alt, da.size() * sizeof(Tile));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_tiles_alt, da.data(), da.size() * sizeof(Tile), hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess && !sidx.empty()) {
+    e = hipMalloc(&p->d_sidx, sidx.size() * sizeof(int64_t));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_sidx, sidx.data(), sidx.size() * sizeof(int64_t), hipMemcpyHostToDevice);
+  }
+  return e;
+}
+}  // namespace
+
 extern "C" {
 
 const char* fa_version(void) { return FA_VERSION_STR; }
@@ -1029,19 +1118,11 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
     p->nscalar_alt = ia.ntiles_tail;
   }
   hipError_t e = hipGetDevice(&p->device);
-  if (e == hipSuccess && !tiles.empty()) {
-    e = hipMalloc(&p->d_tiles, tiles.size() * sizeof(Tile));
-    if (e == hipSuccess)
-      e = hipMemcpy(p->d_tiles, tiles.data(), tiles.size() * sizeof(Tile), hipMemcpyHostToDevice);
-  }
-  if (e == hipSuccess && !alt.empty()) {
-    e = hipMalloc(&p->d_tiles_alt, alt.size() * sizeof(Tile));
-    if (e == hipSuccess)
-      e = hipMemcpy(p->d_tiles_alt, alt.data(), alt.size() * sizeof(Tile), hipMemcpyHostToDevice);
-  }
+  if (e == hipSuccess) e = upload_tables(p, tiles, alt);
   if (e != hipSuccess) {
     if (p->d_tiles) (void)hipFree(p->d_tiles);
     if (p->d_tiles_alt) (void)hipFree(p->d_tiles_alt);
+    if (p->d_sidx) (void)hipFree(p->d_sidx);
     delete p;
     return set_err(FA_E_HIP, "fa_plan_create: %s", hipGetErrorString(e));
   }
@@ -1297,13 +1378,10 @@ int fa_plan_create_from_tiles(const fa_tile_desc* tiles, int ntiles, int64_t f32
   p->flags = flags;
   set_kinds(p, t);
   hipError_t e = hipGetDevice(&p->device);
-  if (e == hipSuccess && !t.empty()) {
-    e = hipMalloc(&p->d_tiles, t.size() * sizeof(Tile));
-    if (e == hipSuccess)
-      e = hipMemcpy(p->d_tiles, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice);
-  }
+  if (e == hipSuccess) e = upload_tables(p, t, {});
   if (e != hipSuccess) {
     if (p->d_tiles) (void)hipFree(p->d_tiles);
+    if (p->d_sidx) (void)hipFree(p->d_sidx);
     delete p;
     return set_err(FA_E_HIP, "fa_plan_create_from_tiles: %s", hipGetErrorString(e));
   }
@@ -1316,6 +1394,7 @@ int fa_plan_destroy(fa_plan* plan) {
   if (plan->d_fac) HIP_TRY(hipFree(plan->d_fac));
   if (plan->d_tiles) HIP_TRY(hipFree(plan->d_tiles));
   if (plan->d_tiles_alt) HIP_TRY(hipFree(plan->d_tiles_alt));
+  if (plan->d_sidx) HIP_TRY(hipFree(plan->d_sidx));
   delete plan;
   return FA_OK;
 }
@@ -1452,8 +1531,10 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
   if (flags & FA_F_BCAST_ONLY) {
     // the broadcast alone (the reference's initial sync, train_fedavg.py:
     // 244-250, and :148-149 without the reduce): out32/out64 -> every client
-    a.ntiles = in.ntiles;
-    hipError_t e = launch_bcast(plan, a, n, in.ntiles, plan->order != FA_ORDER_TORCH_GPU, st);
+    const int nt = plan->order == FA_ORDER_TORCH_GPU ? in.ntiles : plan->nt_dev;
+    a.ntiles = nt;
+    a.sidx = plan->d_sidx;
+    hipError_t e = launch_bcast(plan, a, n, nt, plan->order != FA_ORDER_TORCH_GPU, st);
     if (table) {
       hipError_t e2 = hipFreeAsync(table, st);
       if (e == hipSuccess) e = e2;
@@ -1499,15 +1580,16 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
     if (e != hipSuccess) return set_err(FA_E_HIP, "torch-GPU-order launch: %s", hipGetErrorString(e));
     return FA_OK;
   }
-  int ntiles = in.ntiles, vec_u = plan->vec_u;
-  a.nscalar = in.ntiles_tail;
+  int ntiles = plan->nt_dev, vec_u = plan->vec_u;
+  a.nscalar = plan->ns_dev;
+  a.sidx = plan->d_sidx;
   // 1024-float tiles for unweighted N >= 64, and for the fused broadcast
   // (tuning form) at any N (cfg2 round: 313 vs 318 us, tools/exp_bcast.py)
   if (plan->d_tiles_alt && !weights &&
       (n >= 64 || ((flags & FA_F_BCAST) && (plan->flags & FA_PLAN_TUNE_FUSED_BCAST)))) {
     a.tiles = plan->d_tiles_alt;
-    ntiles = plan->ntiles_alt;
-    a.nscalar = plan->nscalar_alt;
+    ntiles = plan->nt_alt_dev;
+    a.nscalar = plan->ns_alt_dev;
     vec_u = 1;
   }
   a.ntiles = ntiles;
@@ -1594,7 +1676,7 @@ int fa_reduce_chain(const fa_plan* plan, const float* const* c32, int n, const f
   a.lev_out = (int)lout;
   a.plane = ch->plane;
   a.flags = flags | (weights ? 0x100u : 0u);
-  a.ntiles = plan->info.ntiles;
+  a.ntiles = plan->nt_dev;
   hipStream_t s = (hipStream_t)stream;
   void* table = nullptr;
   if (n <= kInline) {

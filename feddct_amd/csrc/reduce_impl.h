@@ -32,6 +32,10 @@ enum TileKind : int32_t {
   K_I64_TGPU_IN = 10,
   K_F32_TGPU_V = 11,  // [N, M>=2], 16-B aligned run: 4 elements per lane, up to 1024
   K_F32_TGPU_W = 12,  // the same with S = 1: 8 elements per lane (2 x 16 B), up to 2048
+  // device tables only (r03): the plan's scalar tiles (kinds 1-6) packed,
+  // up to 256 elements of any tensors per tile; `start` indexes the plan's
+  // scalar index, whose entries are (bucket element << 4) | kind
+  K_SCALAR_PACKED = 13,
 };
 
 __host__ __device__ inline bool kind_is64(int kind) {
@@ -83,6 +87,7 @@ struct ReduceArgs {
   float* st_out;
   int64_t plane;
   const float* tfac;  // torch-GPU order: per-tile mean factor fl(M)/fl(N*M)
+  const int64_t* sidx;  // packed scalar tiles' entries (K_SCALAR_PACKED)
   const float* const* tab32;
   const int64_t* const* tab64;
   const float* tabw;
@@ -433,7 +438,7 @@ struct SrcI64 {
 // The four level accumulators are named variables (a runtime-indexed array
 // would live in scratch).
 template <class Src>
-__device__ float cascade_seq(const Src& src, int64_t e, int first, int stride,
+__device__ __forceinline__ float cascade_seq(const Src& src, int64_t e, int first, int stride,
                              int count) {
   const int lp = level_power(count);
   const int step = 1 << lp, mask = step - 1;
@@ -458,7 +463,7 @@ __device__ float cascade_seq(const Src& src, int64_t e, int first, int stride,
 
 // ATen row_sum: ILP-4 over rows first + k*stride (count rows).
 template <class Src>
-__device__ float ilp4_seq(const Src& src, int64_t e, int first, int stride,
+__device__ __forceinline__ float ilp4_seq(const Src& src, int64_t e, int first, int stride,
                           int count) {
   const int q = count / 4;
   float p0 = cascade_seq(src, e, first, 4 * stride, q);
@@ -474,7 +479,7 @@ __device__ float ilp4_seq(const Src& src, int64_t e, int first, int stride,
 // ATen vectorized_inner_sum (M == 1, n >= 8): 8 lanes, each an ILP-4 over
 // the n/8 vectors; scalar tail into a fresh +0; then lanes 0..7 in order.
 template <class Src>
-__device__ float inner_seq(const Src& src, int64_t e, int n) {
+__device__ __forceinline__ float inner_seq(const Src& src, int64_t e, int n) {
   if (n < 8) return ilp4_seq(src, e, 0, 1, n);
   const int nv = n / 8;
   float fin = 0.f;
@@ -484,74 +489,39 @@ __device__ float inner_seq(const Src& src, int64_t e, int n) {
 }
 
 // Scalar tiles (ILP-4 tails, unaligned cascade columns, M == 1 keys, int64
-// keys) hold 1-256 columns of a few tensors, each column walked over the N
-// rows in its order by one thread: N dependent round trips to HBM per thread
-// made them latency-bound — resnet110sl sf4 at N = 25 (1,240 scalar tiles,
-// 0.75 % of the elements) spent 20.6 us in them against 21.5 us for all its
-// vector tiles (r03, bench other_configs).  When the tile's N x count values
-// fit kStageFloats, the whole workgroup first stages them into LDS with
-// independent loads (the value each order reads: the fp32 value, weighted
-// products and int64 -> fp32 conversions applied as the direct path applies
-// them), then each column's thread runs its order from LDS.  32 KB of LDS
-// per workgroup costs no occupancy: the reduce kernels are VGPR-bound at
-// 3 workgroups per CU (156-170 VGPRs; 3 x 32 KB < 160 KB).
+// keys): one column walked over the N rows in its order by one thread.  Up
+// to r02 each tensor's scalar columns were a tile of their own (1 to 31
+// columns in a 256-thread workgroup) and each thread loaded its rows in its
+// order, N dependent round trips to HBM: resnet110sl sf4 at N = 25 — 1,240
+// such tiles, 0.75 % of its elements — spent 20.6 us in them against
+// 21.5 us for all its vector tiles (r03, bench other_configs).  Now the
+// plan packs every scalar column of the layout, sorted by kind, into tiles
+// of kPackCols (K_SCALAR_PACKED; the plan's scalar index holds each
+// column's bucket element and kind); a workgroup stages its columns' N
+// values into LDS with independent loads (the value each order reads:
+// weighted products and int64 -> fp32 conversions applied as the direct
+// loads apply them), then runs each column's order from LDS.  32 KB of LDS
+// per workgroup costs the reduce kernels no occupancy: they are VGPR-bound
+// at 3 workgroups per CU (156-170 VGPRs).
 constexpr int kStageFloats = 8192;
-struct SrcLds {
+struct SrcLdsCol {
   const float* stage;
-  int count;
-  int64_t start;
-  __device__ float operator()(int i, int64_t e) const {
-    return stage[i * count + (int)(e - start)];
-  }
+  int m;    // columns staged
+  int col;  // this thread's column
+  __device__ float operator()(int i, int64_t) const { return stage[i * m + col]; }
 };
 
-template <bool WEIGHTED>
-__device__ void tile_scalar(KArgs& a, Tile t) {
-  __shared__ float stage[kStageFloats];
-  const int j = threadIdx.x;
+// One scalar column's order, result and broadcast (kind: K_F32_* 1-3, K_I64_* 4-6).
+template <bool WEIGHTED, class SrcF, class SrcI>
+__device__ __forceinline__ void scalar_column(KArgs& a, const SrcF& sf, const SrcI& si, int64_t e,
+                                              int kind) {
   const int n = a.n;
-  const bool staged = n * t.count <= kStageFloats;
-  if (staged) {
-    const int tot = n * t.count;
-    const bool f32 = t.kind <= K_F32_INNER;
-    for (int k = j; k < tot; k += kBlock) {
-      const int i = k / t.count;
-      const int64_t e = t.start + (k - i * t.count);
-      stage[k] = f32 ? SrcF32{a, WEIGHTED}(i, e) : SrcI64{a}(i, e);
-    }
-    __syncthreads();
-  }
-  if (j >= t.count) return;
-  const int64_t e = t.start + j;
   const float fn = (float)n;
-  if (staged) {
-    SrcLds src{stage, t.count, t.start};
+  if (kind <= K_F32_INNER) {
     float s;
-    const int k = t.kind;
-    if (k == K_F32_CASC_S || k == K_I64_CASC) s = cascade_seq(src, e, 0, 1, n);
-    else if (k == K_F32_ILP4 || k == K_I64_ILP4) s = ilp4_seq(src, e, 0, 1, n);
-    else s = inner_seq(src, e, n);
-    s = __fadd_rn(0.f, s);
-    if (k <= K_F32_INNER) {
-      const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
-      const float r = sum_only ? s : __fdiv_rn(s, fn);
-      a.out32[e] = r;
-      if (a.flags & FA_F_BCAST)
-        for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
-    } else {
-      const int64_t r = (int64_t)__fdiv_rn(s, fn);
-      a.out64[e] = r;
-      if (a.flags & FA_F_BCAST)
-        for (int i = 0; i < n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
-    }
-    return;
-  }
-  if (t.kind <= K_F32_INNER) {
-    SrcF32 src{a, WEIGHTED};
-    float s;
-    if (t.kind == K_F32_CASC_S) s = cascade_seq(src, e, 0, 1, n);
-    else if (t.kind == K_F32_ILP4) s = ilp4_seq(src, e, 0, 1, n);
-    else s = inner_seq(src, e, n);
+    if (kind == K_F32_CASC_S) s = cascade_seq(sf, e, 0, 1, n);
+    else if (kind == K_F32_ILP4) s = ilp4_seq(sf, e, 0, 1, n);
+    else s = inner_seq(sf, e, n);
     s = __fadd_rn(0.f, s);  // sum_out: out (=+0) += value
     const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
     const float r = sum_only ? s : __fdiv_rn(s, fn);
@@ -559,17 +529,72 @@ __device__ void tile_scalar(KArgs& a, Tile t) {
     if (a.flags & FA_F_BCAST)
       for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
   } else {
-    SrcI64 src{a};
     float s;
-    if (t.kind == K_I64_CASC) s = cascade_seq(src, e, 0, 1, n);
-    else if (t.kind == K_I64_ILP4) s = ilp4_seq(src, e, 0, 1, n);
-    else s = inner_seq(src, e, n);
+    if (kind == K_I64_CASC) s = cascade_seq(si, e, 0, 1, n);
+    else if (kind == K_I64_ILP4) s = ilp4_seq(si, e, 0, 1, n);
+    else s = inner_seq(si, e, n);
     s = __fadd_rn(0.f, s);
     // load_state_dict copy_: fp32 -> int64 truncates toward zero
     const int64_t r = (int64_t)__fdiv_rn(s, fn);
     a.out64[e] = r;
     if (a.flags & FA_F_BCAST)
       for (int i = 0; i < n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
+  }
+}
+
+// A packed tile holds up to kPackCols columns, one per lane of wave 0.  The
+// staging spreads the rows over the workgroup's 4 waves (wave w: rows w,
+// w+4, ...; the row is wave-uniform, so its client pointer is a scalar load
+// and each lane loads its column's value), 8 rows in flight per lane; then
+// wave 0 runs every column's order from LDS.  More rows than fit
+// kStageFloats / kPackCols: the columns in sub-batches of kStageFloats / N.
+constexpr int kPackCols = 64;
+
+template <bool WEIGHTED>
+__device__ __forceinline__ void tile_scalar_packed(KArgs& a, Tile t) {
+  __shared__ float stage[kStageFloats];
+  const int n = a.n;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (n > kStageFloats) {  // (N > 8192) direct loads, one column per lane of wave 0
+    if (wv == 0 && lane < t.count) {
+      const int64_t ent = a.sidx[t.start + lane];
+      scalar_column<WEIGHTED>(a, SrcF32{a, WEIGHTED}, SrcI64{a}, ent >> 4, (int)(ent & 15));
+    }
+    return;
+  }
+  const int sub = min(kPackCols, kStageFloats / n);  // columns staged at once
+  for (int c0 = 0; c0 < t.count; c0 += sub) {
+    const int m = min(sub, t.count - c0);
+    const bool mine = lane < m;
+    int64_t e = 0;
+    int kind = K_F32_ILP4;
+    if (mine) {
+      const int64_t ent = a.sidx[t.start + c0 + lane];
+      e = ent >> 4;
+      kind = (int)(ent & 15);
+    }
+    const bool f32 = kind <= K_F32_INNER;
+    constexpr int R = 8;  // rows in flight per lane
+    for (int i0 = wv; i0 < n; i0 += 4 * R) {
+      float x[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int r = i0 + 4 * u;
+        if (r < n && mine) x[u] = f32 ? SrcF32{a, WEIGHTED}(r, e) : SrcI64{a}(r, e);
+      }
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int r = i0 + 4 * u;
+        if (r < n && mine) stage[r * m + lane] = x[u];
+      }
+    }
+    __syncthreads();
+    if (wv == 0 && mine) {
+      const SrcLdsCol src{stage, m, lane};
+      scalar_column<WEIGHTED>(a, src, src, e, kind);
+    }
+    __syncthreads();
   }
 }
 
@@ -589,7 +614,7 @@ __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
     else
       tile_vec<U, B, false, DEEP, WEIGHTED, POL, CHAIN>(a, t.start, t.count);
   } else if (!CHAIN) {
-    tile_scalar<WEIGHTED>(a, t);
+    tile_scalar_packed<WEIGHTED>(a, t);
   }
 }
 
