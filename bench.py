@@ -439,7 +439,9 @@ def scalar_share(dev, name, n, steps, warmup):
     cl = make_clients(lay, list(zip(mans, ("0.", "1."))), range(n), dev)
     o32, o64 = torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])
     info, tiles = _lib.build_tiles_host(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel)
+    cols = int(tiles[tiles[:, 2] != 0][:, 1].sum())
     out = {"scalar_tiles": int(info["ntiles_tail"]), "vector_tiles": int(info["ntiles_cascade"]),
+           "scalar_columns": cols, "packed_scalar_tiles": -(-cols // 64),
            "scalar_elems_frac": round(info["tail_elems"] / max(1, info["tail_elems"]
                                                                 + info["cascade_elems"]), 5)}
     for part, sel in (("scalar_tiles_alone_us", tiles[:, 2] != 0),

@@ -58,9 +58,6 @@ def FA_PLAN_TUNE_BLOCKS_PER_CU(c):
     return (int(c) & 0xF) << 8
 
 
-FA_PLAN_TUNE_SCALAR_LAST = 0x10000000
-
-
 def FA_PLAN_TUNE_PACK(c):
     return (int(c) & 3) << 26
 

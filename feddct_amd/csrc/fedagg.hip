@@ -675,7 +675,8 @@ struct fa_plan {
   // the device tables' own counts: their scalar tiles are packed (r03,
   // K_SCALAR_PACKED; info.* keep the host view of the layout's tiles)
   int nt_dev = 0, ns_dev = 0, nt_alt_dev = 0, ns_alt_dev = 0;
-  int64_t* d_sidx = nullptr;  // packed scalar columns: (element << 4) | kind
+  int64_t* d_sidx = nullptr;  // packed scalar columns: (element << 4) | kind, -1 unused
+  int64_t sidx_alt_off = 0;   // the alt table's region of d_sidx
   unsigned flags = 0;
   bool has32 = false;  // the tile table touches the fp32 bucket
   bool has64 = false;  // ... the int64 bucket
@@ -1008,10 +1009,9 @@ namespace {
 // tiles did).
 std::vector<Tile> pack_scalar(const std::vector<Tile>& t, std::vector<int64_t>* sidx,
                               int* nscalar, unsigned flags) {
-  // tuning: FA_PLAN_TUNE_PACK(c) -> kPackCols >> c columns per tile,
-  // FA_PLAN_TUNE_SCALAR_LAST -> the packed tiles after the vector tiles
+  // tuning: FA_PLAN_TUNE_PACK(c) -> kPackCols >> c columns per tile (the
+  // entry stride stays kPackCols: tile k's entries at k * kPackCols)
   const int pack = kPackCols >> ((flags >> 26) & 3u);
-  const bool last = (flags & FA_PLAN_TUNE_SCALAR_LAST) != 0;
   std::vector<std::pair<int, int64_t>> cols;
   std::vector<Tile> vec;
   for (const Tile& x : t) {
@@ -1026,15 +1026,11 @@ std::vector<Tile> pack_scalar(const std::vector<Tile>& t, std::vector<int64_t>* 
                      return u.first < v.first;
                    });
   std::vector<Tile> out;
-  const int64_t base = (int64_t)sidx->size();
-  for (const auto& c : cols) sidx->push_back((c.second << 4) | c.first);
-  for (size_t c = 0; c < cols.size(); c += pack)
-    out.push_back(Tile{base + (int64_t)c, (int32_t)std::min<size_t>(pack, cols.size() - c),
-                       K_SCALAR_PACKED});
-  if (last) {
-    *nscalar = 0;
-    vec.insert(vec.end(), out.begin(), out.end());
-    return vec;
+  for (size_t c = 0; c < cols.size(); c += pack) {
+    const int cnt = (int)std::min<size_t>(pack, cols.size() - c);
+    out.push_back(Tile{(int64_t)sidx->size(), cnt, K_SCALAR_PACKED});
+    for (int i = 0; i < kPackCols; ++i)
+      sidx->push_back(i < cnt ? (cols[c + i].second << 4) | cols[c + i].first : -1);
   }
   *nscalar = (int)out.size();
   out.insert(out.end(), vec.begin(), vec.end());
@@ -1050,7 +1046,12 @@ hipError_t upload_tables(fa_plan* p, const std::vector<Tile>& tiles,
   p->nt_dev = (int)dm.size();
   std::vector<Tile> da;
   if (!alt.empty()) {
-    da = pack_scalar(alt, &sidx, &p->ns_alt_dev, p->flags);
+    // the alt table's packed tiles index their own region of the scalar
+    // index (the kernels get its base: tile k's entries at base + k * kPackCols)
+    std::vector<int64_t> sa;
+    da = pack_scalar(alt, &sa, &p->ns_alt_dev, p->flags);
+    p->sidx_alt_off = (int64_t)sidx.size();
+    sidx.insert(sidx.end(), sa.begin(), sa.end());
     p->nt_alt_dev = (int)da.size();
   }
   hipError_t e = hipSuccess;
@@ -1590,6 +1591,7 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
     a.tiles = plan->d_tiles_alt;
     ntiles = plan->nt_alt_dev;
     a.nscalar = plan->ns_alt_dev;
+    a.sidx = plan->d_sidx ? plan->d_sidx + plan->sidx_alt_off : nullptr;
     vec_u = 1;
   }
   a.ntiles = ntiles;

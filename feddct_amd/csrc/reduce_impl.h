@@ -550,30 +550,32 @@ __device__ __forceinline__ void scalar_column(KArgs& a, const SrcF& sf, const Sr
 // kStageFloats / kPackCols: the columns in sub-batches of kStageFloats / N.
 constexpr int kPackCols = 64;
 
+// Packed tile k's entries sit at sidx[k * kPackCols, +kPackCols) (unused
+// slots -1), so a scalar workgroup needs no tile descriptor: its first load
+// is its entries, one dependent round trip fewer on the critical path of
+// these latency-bound workgroups.
 template <bool WEIGHTED>
-__device__ __forceinline__ void tile_scalar_packed(KArgs& a, Tile t) {
+__device__ __forceinline__ void tile_scalar_packed(KArgs& a, int k) {
   __shared__ float stage[kStageFloats];
   const int n = a.n;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t* ents = a.sidx + (int64_t)k * kPackCols;
   if (n > kStageFloats) {  // (N > 8192) direct loads, one column per lane of wave 0
-    if (wv == 0 && lane < t.count) {
-      const int64_t ent = a.sidx[t.start + lane];
-      scalar_column<WEIGHTED>(a, SrcF32{a, WEIGHTED}, SrcI64{a}, ent >> 4, (int)(ent & 15));
+    if (wv == 0) {
+      const int64_t ent = ents[lane];
+      if (ent >= 0)
+        scalar_column<WEIGHTED>(a, SrcF32{a, WEIGHTED}, SrcI64{a}, ent >> 4, (int)(ent & 15));
     }
     return;
   }
   const int sub = min(kPackCols, kStageFloats / n);  // columns staged at once
-  for (int c0 = 0; c0 < t.count; c0 += sub) {
-    const int m = min(sub, t.count - c0);
-    const bool mine = lane < m;
-    int64_t e = 0;
-    int kind = K_F32_ILP4;
-    if (mine) {
-      const int64_t ent = a.sidx[t.start + c0 + lane];
-      e = ent >> 4;
-      kind = (int)(ent & 15);
-    }
+  for (int c0 = 0; c0 < kPackCols; c0 += sub) {
+    const int m = min(sub, kPackCols - c0);
+    const int64_t ent = lane < m ? ents[c0 + lane] : -1;
+    const bool mine = ent >= 0;
+    const int64_t e = mine ? ent >> 4 : 0;
+    const int kind = mine ? (int)(ent & 15) : K_F32_ILP4;
     const bool f32 = kind <= K_F32_INNER;
     constexpr int R = 8;  // rows in flight per lane
     for (int i0 = wv; i0 < n; i0 += 4 * R) {
@@ -600,6 +602,12 @@ __device__ __forceinline__ void tile_scalar_packed(KArgs& a, Tile t) {
 
 template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN>
 __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
+  if constexpr (!CHAIN) {
+    if (ti < a.nscalar) {  // the packed scalar tiles lead the table
+      tile_scalar_packed<WEIGHTED>(a, ti);
+      return;
+    }
+  }
   if (a.xcd_swz && ti >= a.nscalar) {
     // bijective: blocks i and i+8 share an XCD (round-robin dispatch); XCD x
     // gets the contiguous tile range [x*q + min(x,r), ...) of the vector tiles
@@ -613,8 +621,6 @@ __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
       tile_vec<U, B, true, DEEP, WEIGHTED, POL, CHAIN>(a, t.start, t.count);
     else
       tile_vec<U, B, false, DEEP, WEIGHTED, POL, CHAIN>(a, t.start, t.count);
-  } else if (!CHAIN) {
-    tile_scalar_packed<WEIGHTED>(a, t);
   }
 }
 

@@ -117,8 +117,6 @@ extern "C" {
                                               1024-element tiles (r02 form)      */
 /* tuning: packed scalar tiles of 64 >> c columns (c = 0..3; default 64) */
 #define FA_PLAN_TUNE_PACK(c) (((unsigned)(c) & 3u) << 26)
-/* tuning: the packed scalar tiles after the vector tiles (default: first) */
-#define FA_PLAN_TUNE_SCALAR_LAST 0x10000000u
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
 #define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
 /* tuning: persistent grid of 256*k workgroups striding over the tiles */

@@ -1,6 +1,7 @@
 """Experiment (r03): the packed scalar tiles (K_SCALAR_PACKED) of the
 reference's BN-heavy FedDCT layouts — pack size 64 / 32 / 16 / 8 columns per
-tile, packed tiles first (default) or after the vector tiles — on the joint
+tile (r03: placing them after the vector tiles measured no better), vector
+tiles of 2048 (default), 4096 and 1024 floats — on the joint
 main + proxy bucket, rotated past the MALL, interleaved in one process.
 Every variant's output is checked against the default's bits.
 
@@ -32,12 +33,15 @@ def main():
             sets.append((cl, torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])))
         G = _lib.FA_PLAN_GAPS_ARE_PADDING
         variants = {}
-        for c, cols in enumerate((64, 32, 16, 8)):
-            for last in (False, True):
-                fl = G | _lib.FA_PLAN_TUNE_PACK(c) | (_lib.FA_PLAN_TUNE_SCALAR_LAST if last else 0)
-                plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel, flags=fl)
-                variants[f"pack{cols}_{'last' if last else 'first'}"] = [
-                    Reducer(lay, cl, o32, o64, plan=plan) for cl, o32, o64 in sets]
+        for te in (2048, 4096, 1024):
+            for c, cols in enumerate((64, 32, 16, 8)):
+                if te != 2048 and cols not in (64, 16):
+                    continue
+                fl = G | _lib.FA_PLAN_TUNE_PACK(c)
+                plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
+                                 tile_elems=te, flags=fl)
+                variants[f"tile{te}_pack{cols}"] = [Reducer(lay, cl, o32, o64, plan=plan)
+                                                    for cl, o32, o64 in sets]
         ref = None
         times = {k: [] for k in variants}
         for r in range(rounds):
