@@ -50,6 +50,7 @@ FA_PLAN_TUNE_BCAST_TILES = 0x400000
 FA_PLAN_TUNE_BCAST_TABLE = 0x800000
 FA_PLAN_TUNE_BCAST_REVERSE = 0x1000000
 FA_PLAN_TUNE_BCAST_XCD = 0x2000000
+FA_PLAN_TUNE_NO_BALANCE = 0x10000000
 FA_ORDER_TORCH_CPU = 0
 FA_ORDER_TORCH_GPU = 1
 
@@ -76,6 +77,7 @@ EXPORTS = [
     "fa_prox_grad_ex",
     "fa_read_probe_f32", "fa_chain_levels", "fa_reduce_chain", "fa_torch_gpu_config",
     "fa_plan_create_order", "fa_table_bytes", "fa_reduce_tab",
+    "fa_plan_balance_host", "fa_plan_launch_shape",
 ]
 
 
@@ -127,6 +129,8 @@ def _load():
                                            ctypes.POINTER(_P)]),
         "fa_reduce": (_I, [_P, _P, _P, _I, _P, _P, _P, ctypes.c_uint, _P]),
         "fa_table_bytes": (ctypes.c_size_t, [_I]),
+        "fa_plan_balance_host": (_I, [_P, _I, _I, _I, _I, _P, _I]),
+        "fa_plan_launch_shape": (_I, [_P, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
         "fa_reduce_tab": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, ctypes.c_uint, _P]),
         "fa_mean_f32": (_I, [_P, _I, _I64, _P, _P, _I, _P]),
         "fa_weighted_f32": (_I, [_P, _P, _I, _I64, _P, _P, _I, _P]),
@@ -205,6 +209,26 @@ def build_tiles_host(segs32, f32_numel, segs64=(), i64_numel=0, tile_elems=0,
     return {f: getattr(info, f) for f, _ in FaPlanInfo._fields_}, tiles
 
 
+def balance_host(vec_tiles, tile_elems=2048, nscalar=0, slots=768):
+    """The plan's balanced re-cut of vector tiles (fa_plan_balance_host),
+    computed on the host: ndarray of (start, count, kind), or None when the
+    plain cut is kept."""
+    vec = np.asarray(vec_tiles, np.int64).reshape(-1, 3)
+    arr = (FaTileDesc * max(1, len(vec)))()
+    for i, (s, c, k) in enumerate(vec):
+        arr[i].start, arr[i].count, arr[i].kind = int(s), int(c), int(k)
+    cap = 2 * len(vec) + 2 * int(slots) + 16
+    out = (FaTileDesc * max(1, cap))()
+    rc = lib.fa_plan_balance_host(arr, len(vec), int(tile_elems), int(nscalar), int(slots),
+                                  out, cap)
+    if rc < 0:
+        check(rc, "fa_plan_balance_host")
+    if rc == 0:
+        return None
+    return np.array([(out[i].start, out[i].count, out[i].kind) for i in range(rc)],
+                    np.int64).reshape(-1, 3)
+
+
 class Plan:
     """Owning wrapper of an ``fa_plan`` (device-resident tile table); built
     from a layout's segments, or from an explicit tile subset (``tiles``)."""
@@ -235,6 +259,14 @@ class Plan:
         info = FaPlanInfo()
         check(lib.fa_plan_get_info(h, ctypes.byref(info)), "fa_plan_get_info")
         self.info = {f: getattr(info, f) for f, _ in FaPlanInfo._fields_}
+
+    def launch_shape(self, n, weighted=False):
+        """(tiles, resident-workgroup slots) a plain fa_reduce call with n
+        clients launches with (the balanced table when one applies)."""
+        nt, sl = _I(), _I()
+        check(lib.fa_plan_launch_shape(self.handle, int(n), int(bool(weighted)), ctypes.byref(nt),
+                                       ctypes.byref(sl)), "fa_plan_launch_shape")
+        return nt.value, sl.value
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -25,6 +25,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <queue>
 #include <string>
 #include <vector>
 
@@ -677,6 +678,16 @@ struct fa_plan {
   int nt_dev = 0, ns_dev = 0, nt_alt_dev = 0, ns_alt_dev = 0;
   int64_t* d_sidx = nullptr;  // packed scalar columns: (element << 4) | kind, -1 unused
   int64_t sidx_alt_off = 0;   // the alt table's region of d_sidx
+  // balanced tables (r03): the vector tiles re-cut so that packed + vector
+  // tiles fill whole rounds of `slots` resident workgroups (balance_vec);
+  // their packed tiles are the main table's (same scalar index region)
+  struct BalTable {
+    int u = 0, slots = 0;
+    Tile* d = nullptr;
+    int nt = 0;
+    bool alt = false;  // cut from the alt (1024-float) table: its scalar index region
+  };
+  std::vector<BalTable> bal;
   unsigned flags = 0;
   bool has32 = false;  // the tile table touches the fp32 bucket
   bool has64 = false;  // ... the int64 bucket
@@ -835,6 +846,130 @@ int build_tiles(const std::vector<fa_seg>& s32, const std::vector<fa_seg>& s64, 
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// Clients per load batch of the reduce kernel a call runs (launch_reduce).
+int pick_batch(int n, int vec_u, unsigned pflags) {
+  const int b = (pflags & FA_PLAN_TUNE_BATCH1)    ? 1
+                : (pflags & FA_PLAN_TUNE_BATCH4)  ? 4
+                : (pflags & FA_PLAN_TUNE_BATCH8)  ? 8
+                : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (n < 16 ? 8 : 16);
+  return (vec_u == 4 && b == 16) ? 8 : b;  // no 16-client kernels at U = 4
+}
+
+// ------------------------------------------------------ balanced tables --
+// One workgroup per tile: a launch of T equal tiles over `slots` resident
+// workgroups (CUs x workgroups per CU) runs ceil(T / slots) rounds, and a
+// part-filled last round costs nearly a whole one — measured r03 on one
+// fp32 tensor of T x 2048 floats at N = 20 (tools/exp_batch_cross.py,
+// profiles/r03_exp_batch_cross.jsonl): 768 tiles on 768 slots 22.4 us, 1,024
+// tiles 34.0 us, 1,536 tiles 42.2 us.  The plan therefore also keeps tables
+// whose vector tiles are re-cut, per slot count, so that packed + vector
+// tiles fill whole rounds; a call takes the table cut for the kernel it runs.
+constexpr double kKeepFill = 0.97;  // last round at least this full: keep the plain table
+constexpr int64_t kMinTile = 256;   // never cut vector tiles below this (elements)
+
+// Resident workgroups of the reduce kernel (U, B, deep, weighted) on device
+// `dev`, queried once per process (0: unknown -> the plain table).
+int kernel_slots(int dev, int u, int b, bool deep, bool w) {
+  static std::mutex mu;
+  static std::map<int64_t, int> cache;
+  const int64_t key = ((((int64_t)dev * 8 + u) * 32 + b) * 2 + deep) * 2 + w;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int occ = 0;
+  switch (u * 100 + b) {
+    case 101: occ = occupancy_u<1, 1>(deep, w); break;
+    case 104: occ = occupancy_u<1, 4>(deep, w); break;
+    case 108: occ = occupancy_u<1, 8>(deep, w); break;
+    case 116: occ = occupancy_u<1, 16>(deep, w); break;
+    case 201: occ = occupancy_u<2, 1>(deep, w); break;
+    case 204: occ = occupancy_u<2, 4>(deep, w); break;
+    case 208: occ = occupancy_u<2, 8>(deep, w); break;
+    case 216: occ = occupancy_u<2, 16>(deep, w); break;
+    case 401: occ = occupancy_u<4, 1>(deep, w); break;
+    case 404: occ = occupancy_u<4, 4>(deep, w); break;
+    case 408: occ = occupancy_u<4, 8>(deep, w); break;
+    default: break;
+  }
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 0;
+  const int slots = occ > 0 && cus > 0 ? occ * cus : 0;
+  cache[key] = slots;
+  return slots;
+}
+
+// The slot count a plain (non-chain) reduce call runs on; 0 where a tuning
+// flag shapes the grid itself (persistent grid, per-CU cap, issue-all form).
+int call_slots(int dev, int n, int vec_u, bool w, unsigned pflags) {
+  if (pflags & (FA_PLAN_TUNE_NO_BALANCE | FA_PLAN_TUNE_ISSUE_ALL | (0xFu << 8) | (0xFu << 12)))
+    return 0;
+  return kernel_slots(dev, vec_u, pick_batch(n, vec_u, pflags), n >= 256, w);
+}
+
+// The vector tiles of `tiles` (cut at cmax elements), re-cut for `slots`:
+// k = ceil((nscalar + T) / slots) rounds, k * slots - nscalar vector tiles,
+// handed out run by run (a run = adjacent vector tiles) to the run whose
+// tiles are largest, boundaries on 64-element (256 B) lines, no tile above
+// cmax or (when split further) below kMinTile.  Empty: keep the plain table.
+std::vector<Tile> balance_vec(const std::vector<Tile>& tiles, int cmax, int nscalar, int slots) {
+  std::vector<std::pair<int64_t, int64_t>> runs;  // [start, end)
+  int64_t t0 = 0;
+  for (const Tile& x : tiles) {
+    if (x.kind != K_F32_VEC) continue;
+    ++t0;
+    if (!runs.empty() && runs.back().second == x.start) runs.back().second += x.count;
+    else runs.emplace_back(x.start, x.start + x.count);
+  }
+  if (t0 == 0 || slots <= 0) return {};
+  const int64_t have = t0 + nscalar;
+  const int64_t k = (have + slots - 1) / slots;
+  if ((double)have >= kKeepFill * (double)(k * slots)) return {};
+  const int64_t target = k * slots - nscalar;
+  std::vector<int64_t> m(runs.size());
+  std::priority_queue<std::pair<double, size_t>> pq;  // (tile size, run), largest first
+  int64_t total = 0;
+  for (size_t r = 0; r < runs.size(); ++r) {
+    const int64_t len = runs[r].second - runs[r].first;
+    m[r] = (len + cmax - 1) / cmax;
+    total += m[r];
+    pq.emplace((double)len / (double)m[r], r);
+  }
+  while (total < target && !pq.empty()) {
+    const size_t r = pq.top().second;
+    pq.pop();
+    const int64_t len = runs[r].second - runs[r].first;
+    if ((double)len / (double)(m[r] + 1) < (double)kMinTile) break;  // every run is as small
+    ++m[r];
+    ++total;
+    pq.emplace((double)len / (double)m[r], r);
+  }
+  if (total == t0) return {};
+  std::vector<Tile> out;
+  out.reserve((size_t)total + 16);
+  for (size_t r = 0; r < runs.size(); ++r) {
+    const int64_t s = runs[r].first, e = runs[r].second, len = e - s;
+    for (int64_t mm = m[r];; ++mm) {
+      const size_t mark = out.size();
+      int64_t prev = s;
+      bool ok = true;
+      for (int64_t j = 1; j <= mm; ++j) {
+        const int64_t b = j == mm ? e : ((s + j * len / mm) & ~(int64_t)63);
+        if (b <= prev) continue;  // (a boundary rounded onto the previous one)
+        if (b - prev > cmax) {
+          ok = false;
+          break;
+        }
+        out.push_back(Tile{prev, (int32_t)(b - prev), K_F32_VEC});
+        prev = b;
+      }
+      if (ok) break;
+      out.resize(mark);  // rounding pushed a tile past cmax: one more tile
+    }
+  }
+  return out;
+}
+
 hipError_t launch_chain(const ReduceArgs& a, int ntiles, int vec_u, hipStream_t st) {
   const bool deep = a.n_total >= 256;
   const bool w = a.flags & 0x100u;
@@ -868,11 +1003,7 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   // weighted reductions take the mean's 16-client batches too since the
   // batch's weights are read once up front (r02 sweep, same box: weighted
   // U2xB16 140.5 us vs U2xB8 143.3 us, unweighted 143.0 us)
-  const bool small = a.n < 16;
-  const int b_env = (pflags & FA_PLAN_TUNE_BATCH1)    ? 1
-                    : (pflags & FA_PLAN_TUNE_BATCH4)  ? 4
-                    : (pflags & FA_PLAN_TUNE_BATCH8)  ? 8
-                    : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (small ? 8 : 16);
+  const int b_env = pick_batch(a.n, vec_u, pflags);
   const unsigned cap = (pflags >> 8) & 0xFu;  // FA_PLAN_TUNE_BLOCKS_PER_CU(c)
   // (the scalar tiles' static LDS stage counts against the cap's share)
   t_dyn_lds = cap ? (size_t)std::max<long>(
@@ -1070,6 +1201,53 @@ hipError_t upload_tables(fa_plan* p, const std::vector<Tile>& tiles,
     if (e == hipSuccess)
       e = hipMemcpy(p->d_sidx, sidx.data(), sidx.size() * sizeof(int64_t), hipMemcpyHostToDevice);
   }
+  // balanced tables for every slot count a call on this plan may run on
+  // (main table: 8- and 16-client kernels, deep or not, weighted or not; the
+  // alt table: its unweighted 16-client kernels)
+  if (e != hipSuccess || (p->flags & (FA_PLAN_TUNE_NO_BALANCE | FA_PLAN_TUNE_ISSUE_ALL |
+                                      (0xFu << 8) | (0xFu << 12))))
+    return e;
+  struct Req {
+    int u, slots;
+    const std::vector<Tile>* host;
+    const std::vector<Tile>* dev;
+    int ns;
+  };
+  std::vector<Req> reqs;
+  auto want = [&](int u, int slots, const std::vector<Tile>* host, const std::vector<Tile>* dev,
+                  int ns) {
+    if (slots <= 0) return;
+    for (const Req& q : reqs)
+      if (q.u == u && q.slots == slots && q.dev == dev) return;
+    reqs.push_back(Req{u, slots, host, dev, ns});
+  };
+  for (int b : {8, 16})
+    for (int deep = 0; deep < 2; ++deep)
+      for (int w = 0; w < 2; ++w)
+        want(p->vec_u, kernel_slots(p->device, p->vec_u, pick_batch(b, p->vec_u, p->flags),
+                                    deep != 0, w != 0),
+             &tiles, &dm, p->ns_dev);
+  if (!da.empty())
+    for (int deep = 0; deep < 2; ++deep)
+      want(1, kernel_slots(p->device, 1, pick_batch(64, 1, p->flags), deep != 0, false), &alt,
+           &da, p->ns_alt_dev);
+  for (const Req& q : reqs) {
+    const std::vector<Tile> v =
+        balance_vec(*q.host, q.u * 4 * kBlock, q.ns, q.slots);
+    if (v.empty()) continue;
+    std::vector<Tile> t(q.dev->begin(), q.dev->begin() + q.ns);  // the packed tiles lead
+    t.insert(t.end(), v.begin(), v.end());
+    fa_plan::BalTable b;
+    b.u = q.u;
+    b.slots = q.slots;
+    b.nt = (int)t.size();
+    b.alt = q.dev == &da;
+    e = hipMalloc(&b.d, t.size() * sizeof(Tile));
+    if (e == hipSuccess)
+      e = hipMemcpy(b.d, t.data(), t.size() * sizeof(Tile), hipMemcpyHostToDevice);
+    if (b.d) p->bal.push_back(b);
+    if (e != hipSuccess) return e;
+  }
   return e;
 }
 }  // namespace
@@ -1121,10 +1299,7 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess) e = upload_tables(p, tiles, alt);
   if (e != hipSuccess) {
-    if (p->d_tiles) (void)hipFree(p->d_tiles);
-    if (p->d_tiles_alt) (void)hipFree(p->d_tiles_alt);
-    if (p->d_sidx) (void)hipFree(p->d_sidx);
-    delete p;
+    (void)fa_plan_destroy(p);  // frees whatever was uploaded
     return set_err(FA_E_HIP, "fa_plan_create: %s", hipGetErrorString(e));
   }
   *out = p;
@@ -1376,7 +1551,7 @@ int fa_plan_create_from_tiles(const fa_tile_desc* tiles, int ntiles, int64_t f32
   fa_plan* p = new fa_plan();
   p->info = in;
   p->vec_u = tile_elems / (4 * kBlock);
-  p->flags = flags;
+  p->flags = flags | FA_PLAN_TUNE_NO_BALANCE;  // the caller's tiles are the ones launched
   set_kinds(p, t);
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess) e = upload_tables(p, t, {});
@@ -1396,6 +1571,8 @@ int fa_plan_destroy(fa_plan* plan) {
   if (plan->d_tiles) HIP_TRY(hipFree(plan->d_tiles));
   if (plan->d_tiles_alt) HIP_TRY(hipFree(plan->d_tiles_alt));
   if (plan->d_sidx) HIP_TRY(hipFree(plan->d_sidx));
+  for (const fa_plan::BalTable& b : plan->bal)
+    if (b.d) HIP_TRY(hipFree(b.d));
   delete plan;
   return FA_OK;
 }
@@ -1446,6 +1623,84 @@ hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, b
   return hipGetLastError();
 }
 }  // namespace
+
+}  // extern "C"
+namespace {
+// The table, packed-tile count, scalar index and tile width a plain reduce
+// call runs with (fa_reduce; fa_plan_launch_shape reports it).
+struct Launch {
+  const Tile* tiles;
+  int nt, ns;
+  const int64_t* sidx;
+  int vec_u;
+  int slots;  // resident workgroups of its kernel (0: unknown / tuning grid)
+};
+Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) {
+  Launch L{plan->d_tiles, plan->nt_dev, plan->ns_dev, plan->d_sidx, plan->vec_u, 0};
+  bool alt = false;
+  // 1024-float tiles for unweighted N >= 64, and for the fused broadcast
+  // (tuning form) at any N (cfg2 round: 313 vs 318 us, tools/exp_bcast.py)
+  if (plan->d_tiles_alt && !weighted &&
+      (n >= 64 || ((flags & FA_F_BCAST) && (plan->flags & FA_PLAN_TUNE_FUSED_BCAST)))) {
+    L.tiles = plan->d_tiles_alt;
+    L.nt = plan->nt_alt_dev;
+    L.ns = plan->ns_alt_dev;
+    L.sidx = plan->d_sidx ? plan->d_sidx + plan->sidx_alt_off : nullptr;
+    L.vec_u = 1;
+    alt = true;
+  }
+  if (!plan->bal.empty()) {
+    // the table cut for the slot count of the kernel this call runs
+    L.slots = call_slots(plan->device, n, L.vec_u, weighted, plan->flags);
+    for (const fa_plan::BalTable& b : plan->bal)
+      if (b.slots == L.slots && b.u == L.vec_u && b.alt == alt) {
+        L.tiles = b.d;
+        L.nt = b.nt;
+        break;
+      }
+  }
+  return L;
+}
+}  // namespace
+
+extern "C" {
+
+int fa_plan_balance_host(const fa_tile_desc* vec, int nvec, int tile_elems, int nscalar,
+                         int slots, fa_tile_desc* out, int cap) {
+  if (nvec < 0 || (nvec > 0 && !vec) || nscalar < 0 || slots < 0 || cap < 0 ||
+      (cap > 0 && !out))
+    return set_err(FA_E_INVAL, "fa_plan_balance_host: bad arguments");
+  if (tile_elems != 4 * kBlock && tile_elems != 8 * kBlock && tile_elems != 16 * kBlock)
+    return set_err(FA_E_INVAL, "tile_elems must be 1024, 2048 or 4096 (got %d)", tile_elems);
+  std::vector<Tile> t;
+  for (int i = 0; i < nvec; ++i) {
+    if (vec[i].kind != K_F32_VEC || vec[i].count < 4 || vec[i].count % 4 ||
+        vec[i].count > tile_elems || vec[i].start % 4)
+      return set_err(FA_E_INVAL, "fa_plan_balance_host: tile %d is not a vector tile", i);
+    t.push_back(Tile{vec[i].start, vec[i].count, vec[i].kind});
+  }
+  const std::vector<Tile> b = balance_vec(t, tile_elems, nscalar, slots);
+  if ((int64_t)b.size() > (int64_t)cap)
+    return set_err(FA_E_RANGE, "fa_plan_balance_host: %zu tiles > cap %d", b.size(), cap);
+  for (size_t i = 0; i < b.size(); ++i) out[i] = fa_tile_desc{b[i].start, b[i].count, b[i].kind};
+  return (int)b.size();
+}
+
+int fa_plan_launch_shape(const fa_plan* plan, int n, int weighted, int* ntiles, int* slots) {
+  if (!plan || !ntiles || !slots || n < 1)
+    return set_err(FA_E_INVAL, "fa_plan_launch_shape: bad arguments");
+  if (plan->order == FA_ORDER_TORCH_GPU) {
+    *ntiles = plan->info.ntiles;
+    *slots = 0;
+    return FA_OK;
+  }
+  const Launch L = select_launch(plan, n, weighted != 0, 0);
+  *ntiles = L.nt;
+  *slots = L.slots ? L.slots
+                   : call_slots(plan->device, n, L.vec_u, weighted != 0,
+                                plan->flags & ~FA_PLAN_TUNE_NO_BALANCE);
+  return FA_OK;
+}
 
 size_t fa_table_bytes(int n) { return n > kInline ? ((size_t)n * 20 + 7) / 8 * 8 : 0; }
 
@@ -1581,19 +1836,11 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
     if (e != hipSuccess) return set_err(FA_E_HIP, "torch-GPU-order launch: %s", hipGetErrorString(e));
     return FA_OK;
   }
-  int ntiles = plan->nt_dev, vec_u = plan->vec_u;
-  a.nscalar = plan->ns_dev;
-  a.sidx = plan->d_sidx;
-  // 1024-float tiles for unweighted N >= 64, and for the fused broadcast
-  // (tuning form) at any N (cfg2 round: 313 vs 318 us, tools/exp_bcast.py)
-  if (plan->d_tiles_alt && !weights &&
-      (n >= 64 || ((flags & FA_F_BCAST) && (plan->flags & FA_PLAN_TUNE_FUSED_BCAST)))) {
-    a.tiles = plan->d_tiles_alt;
-    ntiles = plan->nt_alt_dev;
-    a.nscalar = plan->ns_alt_dev;
-    a.sidx = plan->d_sidx ? plan->d_sidx + plan->sidx_alt_off : nullptr;
-    vec_u = 1;
-  }
+  const Launch L = select_launch(plan, n, weights != nullptr, flags);
+  a.tiles = L.tiles;
+  a.nscalar = L.ns;
+  a.sidx = L.sidx;
+  const int ntiles = L.nt, vec_u = L.vec_u;
   a.ntiles = ntiles;
   a.xcd_swz = (plan->flags & FA_PLAN_TUNE_XCD) ? 1 : 0;
   const bool split_bcast = (flags & FA_F_BCAST) && !(plan->flags & FA_PLAN_TUNE_FUSED_BCAST);

@@ -500,10 +500,12 @@ __device__ __forceinline__ float inner_seq(const Src& src, int64_t e, int n) {
 // column's bucket element and kind); a workgroup stages its columns' N
 // values into LDS with independent loads (the value each order reads:
 // weighted products and int64 -> fp32 conversions applied as the direct
-// loads apply them), then runs each column's order from LDS.  32 KB of LDS
-// per workgroup costs the reduce kernels no occupancy: they are VGPR-bound
-// at 3 workgroups per CU (156-170 VGPRs).
-constexpr int kStageFloats = 8192;
+// loads apply them), then runs each column's order from LDS.  The stage is
+// 16 KB (64 columns x 64 rows at once): the 16-client kernels are VGPR-bound
+// at 3 workgroups per CU (156-176 VGPRs), and the 8-client ones (91-126) at
+// 4-5, which a 32 KB stage capped at 4 (measured r03: tile counts of 1,280
+// ran as two rounds of 1,024, tools/exp_batch_cross.py).
+constexpr int kStageFloats = 4096;
 struct SrcLdsCol {
   const float* stage;
   int m;    // columns staged
@@ -681,13 +683,34 @@ hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, int pol,
   }
 }
 
+// Resident workgroups per CU of launch_u<U, B>'s kernel for this call shape
+// (default cache policy, no dynamic LDS); 0 if the runtime cannot say.  The
+// plan cuts its balanced tile tables for these counts (fedagg.hip).
+template <int U, int B>
+int occupancy_u(bool deep, bool w) {
+  int nb = 0;
+  hipError_t e;
+  if (deep)
+    e = w ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, true, true, 3>), kBlock, 0)
+          : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, true, false, 3>), kBlock, 0);
+  else
+    e = w ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, false, true, 3>), kBlock, 0)
+          : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, false, false, 3>), kBlock,
+                0);
+  return e == hipSuccess ? nb : 0;
+}
 
 }  // namespace fa_k
 
 // The (U, B) launcher instantiations, each in one fedagg_k*.hip unit.
 #define FA_K_LAUNCH_U(EXT, U, B)                                                      \
   EXT template hipError_t fa_k::launch_u<U, B>(const fa_k::ReduceArgs&, int, bool, bool, int, \
-                                                hipStream_t);
+                                                hipStream_t);                                 \
+  EXT template int fa_k::occupancy_u<U, B>(bool, bool);
 #define FA_K_LAUNCH_CHAIN(EXT, U, B)                                                          \
   EXT template hipError_t fa_k::launch_chain_ub<U, B>(const fa_k::ReduceArgs&, int, bool, bool, \
                                                        hipStream_t);

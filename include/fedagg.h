@@ -115,6 +115,11 @@ extern "C" {
                                               tile writing every client (r01 form) */
 #define FA_PLAN_TUNE_TGPU_NARROW 0x200000u /* tuning: torch-GPU order, S = 1 tensors in
                                               1024-element tiles (r02 form)      */
+#define FA_PLAN_TUNE_NO_BALANCE 0x10000000u /* tuning: launch the plain tile table
+                                               only (by default a call whose tiles
+                                               leave the last round of resident
+                                               workgroups under 97 % full runs a
+                                               table re-cut to whole rounds)     */
 /* tuning: packed scalar tiles of 64 >> c columns (c = 0..3; default 64) */
 #define FA_PLAN_TUNE_PACK(c) (((unsigned)(c) & 3u) << 26)
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
@@ -174,6 +179,26 @@ int fa_plan_get_info(const fa_plan *plan, fa_plan_info *info);
 int fa_plan_create_from_tiles(const fa_tile_desc *tiles, int ntiles,
                               int64_t f32_numel, int64_t i64_numel,
                               int tile_elems, unsigned flags, fa_plan **out);
+
+/* ---- balanced tile tables (r03) --------------------------------------------
+ * One workgroup per tile: T tiles over `slots` resident workgroups run
+ * ceil(T / slots) rounds, and a part-filled last round costs nearly a full
+ * one.  fa_plan_create also keeps, per slot count of the reduce kernels a
+ * call may run (queried from the runtime), a table whose vector tiles are
+ * re-cut so that packed scalar + vector tiles fill whole rounds (unless the
+ * plain table's last round is already >= 97 % full, or
+ * FA_PLAN_TUNE_NO_BALANCE).  Any cut reduces bit-identically: the order is
+ * per column.
+ * fa_plan_balance_host: that re-cut on the host — `vec` are vector tiles
+ * (kind 0, at most tile_elems each), `nscalar` the packed scalar tiles
+ * that lead the launch; writes the new vector tiles to `out` (cap entries)
+ * and returns their count, 0 when the plain cut is kept, < 0 on error.
+ * fa_plan_launch_shape: the tiles and resident-workgroup slots a plain
+ * fa_reduce call with n clients (weighted or not) launches with. */
+int fa_plan_balance_host(const fa_tile_desc *vec, int nvec, int tile_elems,
+                         int nscalar, int slots, fa_tile_desc *out, int cap);
+int fa_plan_launch_shape(const fa_plan *plan, int n, int weighted, int *ntiles,
+                         int *slots);
 
 /* ---- summation order ------------------------------------------------------
  * FA_ORDER_TORCH_CPU (every plan's default): torch's CPU stack(...).mean(0),
