@@ -858,13 +858,22 @@ int pick_batch(int n, int vec_u, unsigned pflags) {
 // ------------------------------------------------------ balanced tables --
 // One workgroup per tile: a launch of T equal tiles over `slots` resident
 // workgroups (CUs x workgroups per CU) runs ceil(T / slots) rounds, and a
-// part-filled last round costs nearly a whole one — measured r03 on one
-// fp32 tensor of T x 2048 floats at N = 20 (tools/exp_batch_cross.py,
-// profiles/r03_exp_batch_cross.jsonl): 768 tiles on 768 slots 22.4 us, 1,024
-// tiles 34.0 us, 1,536 tiles 42.2 us.  The plan therefore also keeps tables
-// whose vector tiles are re-cut, per slot count, so that packed + vector
-// tiles fill whole rounds; a call takes the table cut for the kernel it runs.
-constexpr double kKeepFill = 0.97;  // last round at least this full: keep the plain table
+// part-filled round costs nearly a whole one while the launch is only one or
+// two rounds long — measured r03 on one fp32 tensor of T x 2048 floats
+// (tools/exp_batch_cross.py, profiles/r03_exp_batch_cross*.jsonl), N = 20,
+// 16-client kernel on 768 slots: 384 tiles 16.1 us, re-cut to 768 13.4 us;
+// 768 tiles 22.7 us; 1,024 tiles 33.5 us, on the 8-client kernel's 1,280
+// slots (one round) 28.3 us.  Past two rounds the tail is a small share and
+// a re-cut (smaller, partial tiles) costs more than it saves: cfg4 weighted
+// 144.2 vs 142.0 us, cfg5 185.5 vs 181.4 us, cfg3 43.7 vs 43.5 us re-cut vs
+// plain (profiles/r03_exp_tune_balance.jsonl).  So a call of N >= 16
+// clients whose plain table (a) part-fills ONE round of the 16-client kernel
+// runs a table re-cut to fill it, (b) needs two rounds of the 16-client
+// kernel but one of the 8-client kernel runs the 8-client kernel (resnet110sl
+// sf4 N = 25, 923 tiles: 23.0 vs 26.3 us plain, 23.9 re-cut), and (c) runs
+// the plain table otherwise.  N < 16 (8-client kernel already) always runs
+// plain: at N = 5 a re-cut is no gain (384 tiles 7.8 vs 9.0 us).
+constexpr double kKeepFill = 0.97;  // the round at least this full: keep the plain table
 constexpr int64_t kMinTile = 256;   // never cut vector tiles below this (elements)
 
 // Resident workgroups of the reduce kernel (U, B, deep, weighted) on device
@@ -907,8 +916,21 @@ int call_slots(int dev, int n, int vec_u, bool w, unsigned pflags) {
   return kernel_slots(dev, vec_u, pick_batch(n, vec_u, pflags), n >= 256, w);
 }
 
+// Case (b) above: the batch a plain call of n clients runs with, given the
+// plain table's tile count — 8 instead of 16 when that turns two rounds into
+// one.  Explicit batch tuning flags and grid-shaping flags keep their batch.
+int round_batch(int dev, int n, int vec_u, bool w, unsigned pflags, int ntiles) {
+  const int b = pick_batch(n, vec_u, pflags);
+  if (b != 16 || (pflags & (FA_PLAN_TUNE_BATCH16 | FA_PLAN_TUNE_NO_BALANCE |
+                            FA_PLAN_TUNE_ISSUE_ALL | (0xFu << 8) | (0xFu << 12))))
+    return b;
+  const int s16 = kernel_slots(dev, vec_u, 16, n >= 256, w);
+  const int s8 = kernel_slots(dev, vec_u, 8, n >= 256, w);
+  return (s16 > 0 && s8 > s16 && ntiles > s16 && ntiles <= s8) ? 8 : 16;
+}
+
 // The vector tiles of `tiles` (cut at cmax elements), re-cut for `slots`:
-// k = ceil((nscalar + T) / slots) rounds, k * slots - nscalar vector tiles,
+// only when they part-fill a single round (k = 1: slots - nscalar vector tiles),
 // handed out run by run (a run = adjacent vector tiles) to the run whose
 // tiles are largest, boundaries on 64-element (256 B) lines, no tile above
 // cmax or (when split further) below kMinTile.  Empty: keep the plain table.
@@ -924,7 +946,7 @@ std::vector<Tile> balance_vec(const std::vector<Tile>& tiles, int cmax, int nsca
   if (t0 == 0 || slots <= 0) return {};
   const int64_t have = t0 + nscalar;
   const int64_t k = (have + slots - 1) / slots;
-  if ((double)have >= kKeepFill * (double)(k * slots)) return {};
+  if (k > 1 || (double)have >= kKeepFill * (double)(k * slots)) return {};
   const int64_t target = k * slots - nscalar;
   std::vector<int64_t> m(runs.size());
   std::priority_queue<std::pair<double, size_t>> pq;  // (tile size, run), largest first
@@ -983,7 +1005,7 @@ hipError_t launch_chain(const ReduceArgs& a, int ntiles, int vec_u, hipStream_t 
 
 
 hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pflags,
-                         hipStream_t st) {
+                         hipStream_t st, int batch = 0) {
   // DEEP (n >= 256): cascade levels 2-3 and the constant-space table loads
   const bool deep = a.n >= 256;
   const bool w = a.flags & 0x100u;  // internal: weighted
@@ -1003,7 +1025,7 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   // weighted reductions take the mean's 16-client batches too since the
   // batch's weights are read once up front (r02 sweep, same box: weighted
   // U2xB16 140.5 us vs U2xB8 143.3 us, unweighted 143.0 us)
-  const int b_env = pick_batch(a.n, vec_u, pflags);
+  const int b_env = batch > 0 ? batch : pick_batch(a.n, vec_u, pflags);
   const unsigned cap = (pflags >> 8) & 0xFu;  // FA_PLAN_TUNE_BLOCKS_PER_CU(c)
   // (the scalar tiles' static LDS stage counts against the cap's share)
   t_dyn_lds = cap ? (size_t)std::max<long>(
@@ -1202,7 +1224,7 @@ hipError_t upload_tables(fa_plan* p, const std::vector<Tile>& tiles,
       e = hipMemcpy(p->d_sidx, sidx.data(), sidx.size() * sizeof(int64_t), hipMemcpyHostToDevice);
   }
   // balanced tables for every slot count a call on this plan may run on
-  // (main table: 8- and 16-client kernels, deep or not, weighted or not; the
+  // (main table: the 16-client kernels, deep or not, weighted or not; the
   // alt table: its unweighted 16-client kernels)
   if (e != hipSuccess || (p->flags & (FA_PLAN_TUNE_NO_BALANCE | FA_PLAN_TUNE_ISSUE_ALL |
                                       (0xFu << 8) | (0xFu << 12))))
@@ -1221,12 +1243,12 @@ hipError_t upload_tables(fa_plan* p, const std::vector<Tile>& tiles,
       if (q.u == u && q.slots == slots && q.dev == dev) return;
     reqs.push_back(Req{u, slots, host, dev, ns});
   };
-  for (int b : {8, 16})
-    for (int deep = 0; deep < 2; ++deep)
-      for (int w = 0; w < 2; ++w)
-        want(p->vec_u, kernel_slots(p->device, p->vec_u, pick_batch(b, p->vec_u, p->flags),
-                                    deep != 0, w != 0),
-             &tiles, &dm, p->ns_dev);
+  // (only the 16-client kernels' calls are re-cut: N < 16 runs plain)
+  for (int deep = 0; deep < 2; ++deep)
+    for (int w = 0; w < 2; ++w)
+      if (pick_batch(16, p->vec_u, p->flags) == 16)
+        want(p->vec_u, kernel_slots(p->device, p->vec_u, 16, deep != 0, w != 0), &tiles, &dm,
+             p->ns_dev);
   if (!da.empty())
     for (int deep = 0; deep < 2; ++deep)
       want(1, kernel_slots(p->device, 1, pick_batch(64, 1, p->flags), deep != 0, false), &alt,
@@ -1634,9 +1656,10 @@ struct Launch {
   const int64_t* sidx;
   int vec_u;
   int slots;  // resident workgroups of its kernel (0: unknown / tuning grid)
+  int batch;  // clients per load batch of its kernel
 };
 Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) {
-  Launch L{plan->d_tiles, plan->nt_dev, plan->ns_dev, plan->d_sidx, plan->vec_u, 0};
+  Launch L{plan->d_tiles, plan->nt_dev, plan->ns_dev, plan->d_sidx, plan->vec_u, 0, 0};
   bool alt = false;
   // 1024-float tiles for unweighted N >= 64, and for the fused broadcast
   // (tuning form) at any N (cfg2 round: 313 vs 318 us, tools/exp_bcast.py)
@@ -1649,9 +1672,13 @@ Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) 
     L.vec_u = 1;
     alt = true;
   }
-  if (!plan->bal.empty()) {
+  // the batch: 8 where that runs the plain table in one round instead of two
+  L.batch = round_batch(plan->device, n, L.vec_u, weighted, plan->flags, L.nt);
+  L.slots = call_slots(plan->device, n, L.vec_u, weighted, plan->flags);
+  if (L.batch != pick_batch(n, L.vec_u, plan->flags)) {
+    L.slots = kernel_slots(plan->device, L.vec_u, L.batch, n >= 256, weighted);
+  } else if (!plan->bal.empty()) {
     // the table cut for the slot count of the kernel this call runs
-    L.slots = call_slots(plan->device, n, L.vec_u, weighted, plan->flags);
     for (const fa_plan::BalTable& b : plan->bal)
       if (b.slots == L.slots && b.u == L.vec_u && b.alt == alt) {
         L.tiles = b.d;
@@ -1845,7 +1872,7 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
   a.xcd_swz = (plan->flags & FA_PLAN_TUNE_XCD) ? 1 : 0;
   const bool split_bcast = (flags & FA_F_BCAST) && !(plan->flags & FA_PLAN_TUNE_FUSED_BCAST);
   if (split_bcast) a.flags &= ~FA_F_BCAST;
-  hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st);
+  hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st, L.batch);
   if (e == hipSuccess && split_bcast) e = launch_bcast(plan, a, n, ntiles, true, st);
   if (table) {
     hipError_t e2 = hipFreeAsync(table, st);

@@ -1,9 +1,10 @@
 """Balanced tile tables (fa_plan_balance_host, r03) on the host: the re-cut
 vector tiles cover exactly the plain tiles' elements (so any reduction over
 them is the same per-column order), stay within the kernel's tile width, sit
-on 64-element lines, and with the packed scalar tiles fill whole rounds of
-the slot count — or the plain cut is kept when its last round is >= 97 %
-full.  No GPU."""
+on 64-element lines, and with the packed scalar tiles fill the one round of
+the slot count they part-fill — or the plain cut is kept when that round is
+>= 97 % full or the launch needs more than one round (measured: re-cutting a
+multi-round launch is slower, fedagg.hip balance_vec).  No GPU."""
 import numpy as np
 import pytest
 
@@ -41,8 +42,8 @@ def _check(plain, cut, width, nscalar, slots):
             assert (s + c) % 64 == 0
 
 
-@pytest.mark.parametrize("t,slots", [(1024, 768), (1280, 768), (2560, 768), (1280, 1024),
-                                     (5380, 768), (4096, 1280)])
+@pytest.mark.parametrize("t,slots", [(384, 768), (700, 768), (1000, 1280), (200, 1024),
+                                     (1100, 1280)])
 def test_one_run_fills_whole_rounds(t, slots):
     plain = _vec_tiles([(0, t * 2048)])
     cut = _lib.balance_host(plain, 2048, 0, slots)
@@ -53,8 +54,10 @@ def test_one_run_fills_whole_rounds(t, slots):
     assert sizes.max() - sizes.min() <= 64
 
 
-@pytest.mark.parametrize("t,ns,slots", [(768, 0, 768), (5358, 2, 768), (3070, 0, 1024)])
-def test_full_last_round_keeps_plain_cut(t, ns, slots):
+@pytest.mark.parametrize("t,ns,slots", [(768, 0, 768), (5358, 2, 768), (3070, 0, 1024),
+                                        (750, 5, 768), (1024, 0, 768), (1280, 0, 768),
+                                        (2560, 0, 768), (5380, 0, 768), (4096, 0, 1280)])
+def test_full_or_multi_round_keeps_plain_cut(t, ns, slots):
     assert _lib.balance_host(_vec_tiles([(0, t * 2048)]), 2048, ns, slots) is None
 
 
@@ -62,8 +65,8 @@ def test_runs_with_gaps_and_ragged_ends():
     runs = [(0, 96_000), (96_064, 100_032), (200_000, 200_032), (204_800, 3_000_000),
             (3_000_064, 3_001_024)]
     plain = _vec_tiles(runs)
-    cut = _lib.balance_host(plain, 2048, 155, 768)
-    _check(plain, cut, 2048, 155, 768)
+    cut = _lib.balance_host(plain, 2048, 155, 2048)
+    _check(plain, cut, 2048, 155, 2048)
     for s, c, _ in cut:   # no tile crosses a gap
         assert any(rs <= s and s + c <= re for rs, re in runs)
 
@@ -79,8 +82,8 @@ def test_small_layout_floor():
 @pytest.mark.parametrize("width", [1024, 4096])
 def test_other_tile_widths(width):
     plain = _vec_tiles([(0, 1000 * width)], width)
-    cut = _lib.balance_host(plain, width, 3, 768)
-    _check(plain, cut, width, 3, 768)
+    cut = _lib.balance_host(plain, width, 3, 1280)
+    _check(plain, cut, width, 3, 1280)
 
 
 @pytest.mark.parametrize("name,slots", [("wrn16_8_c100", 768), ("wrn16_8_c10", 1280),
@@ -93,7 +96,7 @@ def test_reference_layouts(name, slots):
     cut = _lib.balance_host(vec, 2048, ns, slots)
     if cut is None:
         k = -(-(len(vec) + ns) // slots)
-        assert len(vec) + ns >= 0.97 * k * slots
+        assert k > 1 or len(vec) + ns >= 0.97 * k * slots
     else:
         _check(vec, cut, 2048, ns, slots)
 

@@ -1,11 +1,13 @@
-"""GPU: balanced tile tables (r03).  A plan keeps, per slot count of the
-reduce kernels a call may run, a table whose vector tiles are re-cut to fill
-whole rounds of resident workgroups (fedagg.hip balance_vec).  Each call
-here runs once through the plan's choice and once through the plain table
-(FA_PLAN_TUNE_NO_BALANCE): the results must be the same bits, and the
-launch shape must be the re-cut one where the plain cut leaves its last
-round part-filled.  The layouts' reference digests go through the balanced
-tables in test_gpu_sweep / test_gpu_parity as well."""
+"""GPU: launch shapes by round count (r03).  A call of N >= 16 clients whose
+plain tile table part-fills one round of the 16-client kernel's resident
+workgroups runs a table re-cut to fill it; one that needs two rounds of the
+16-client kernel but one of the 8-client kernel runs the 8-client kernel;
+everything else runs the plain table (fedagg.hip balance_vec / round_batch).
+Each call here runs once through the plan's choice and once through the
+plain table with the default batch (FA_PLAN_TUNE_NO_BALANCE): the results
+must be the same bits, and the launch shape must be the one the rule names.
+The layouts' reference digests go through the same choice in test_gpu_sweep
+/ test_gpu_parity as well."""
 import ctypes
 
 import pytest
@@ -54,6 +56,8 @@ def _run(lib, plan, cl, n, weights):
 
 CASES = [("one_tensor_1024", 20, False), ("one_tensor_1280", 16, False),
          ("one_tensor_1280", 5, False), ("one_tensor_300", 300, False),
+         ("one_tensor_384", 20, False), ("one_tensor_384", 20, True), ("one_tensor_600", 5, False),
+         ("one_tensor_3000", 17, False),
          ("wrn16_8_c100", 20, False), ("wrn16_8_c100", 20, True), ("wrn16_8_c10", 20, False),
          ("wrnsl16_8_sf4_c10_joint", 5, False), ("resnet110sl_sf4_c100_joint", 25, False),
          ("wrnsl16_8_sf32_c100_joint", 3, False), ("wrnsl16_8_sf2_c100_joint", 48, True)]
@@ -79,20 +83,22 @@ def test_balanced_table_same_bits(lib, name, n, weighted):
     assert torch.equal(a64, b64)
     assert not torch.isnan(a32[lay.segs32[0][0]:lay.segs32[0][0] + lay.segs32[0][1]]).any()
     nt_b, slots = pb.launch_shape(n, weighted)
-    nt_p, slots_p = pp.launch_shape(n, weighted)
-    assert slots > 0 and slots == slots_p and slots % 256 == 0
-    k = -(-nt_p // slots)
-    if nt_p >= 0.97 * k * slots:
-        assert nt_b == nt_p          # the plain cut already fills its last round
+    nt_p, slots_p = pp.launch_shape(n, weighted)   # the default batch's slots
+    assert slots > 0 and slots_p > 0 and slots % 256 == 0
+    s8 = pp.launch_shape(5, weighted)[1] if n >= 16 else slots_p
+    if n < 16 or nt_p > s8 or (nt_p <= slots_p and nt_p >= 0.97 * slots_p):
+        assert (nt_b, slots) == (nt_p, slots_p)    # plain table, default batch
+    elif nt_p <= slots_p:
+        assert nt_p < nt_b <= slots_p and slots == slots_p   # one round, re-cut to fill it
     else:
-        assert nt_p < nt_b <= k * slots
+        assert (nt_b, slots) == (nt_p, s8)         # two rounds of 16 -> one of 8
 
 
 def test_occupancy_of_the_default_kernels(lib):
     """The slot counts the tables are cut for: 16-client batches 3 workgroups
     per CU (VGPR-bound), 8-client batches more (the 16 KB scalar stage no
     longer caps them at 4)."""
-    man, lay = _layout("one_tensor_1024")
+    man, lay = _layout("one_tensor_5380")
     p = lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel)
     cus = torch.cuda.get_device_properties(DEV).multi_processor_count
     _, s16 = p.launch_shape(20)

@@ -1,0 +1,143 @@
+"""A/B of two libfedagg.so builds in ONE process on the same buffers (r03):
+the headline cfg2 reduce (wrn16_8 C10, N = 20) and other layouts, each
+library's default plan, launches interleaved library by library over
+several rounds, output bits compared between the builds.  Used to tell a
+code change from box-to-box variance.  Only the C ABI both builds share
+is called (fa_plan_create, fa_reduce, fa_synth_fill_*).
+
+    python tools/ab_lib.py LIB_A LIB_B [ROUNDS]
+"""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from feddct_amd import synth  # noqa: E402
+from feddct_amd.layout import KIND_I64, BucketLayout  # noqa: E402
+from feddct_amd.workload import joint_manifest, load_manifest  # noqa: E402
+
+_P, _I, _I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
+         ("cfg3", "wrnsl16_8_sf4_c10", 5, 2), ("resnet110sl", "resnet110sl_sf4_c100", 25, 4)]
+
+
+def load(path):
+    lib = ctypes.CDLL(path)
+    lib.fa_plan_create.argtypes = [_P, _I, _I64, _P, _I, _I64, _I, ctypes.c_uint,
+                                   ctypes.POINTER(_P)]
+    lib.fa_reduce.argtypes = [_P, _P, _P, _I, _P, _P, _P, ctypes.c_uint, _P]
+    lib.fa_synth_fill_f32.argtypes = [_P, _I64, _I, _I, ctypes.c_float, ctypes.c_float, _I, _P]
+    lib.fa_synth_fill_i64.argtypes = [_P, _I64, _I, _I, _I, _P]
+    lib.fa_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+def ok(lib, rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what}: {lib.fa_last_error().decode()}")
+
+
+def segs(arr):
+    a = (_I64 * max(2, 2 * len(arr)))()
+    for i, (o, m) in enumerate(arr):
+        a[2 * i], a[2 * i + 1] = int(o), int(m)
+    return a, len(arr)
+
+
+def layout_of(stem):
+    if os.path.exists(os.path.join(ROOT, "feddct_amd", "manifests", stem + "_main.json")):
+        mans = [load_manifest(stem + "_main"), load_manifest(stem + "_proxy")]
+        return BucketLayout.from_manifest(joint_manifest(mans)), list(zip(mans, ("0.", "1.")))
+    m = load_manifest(stem)
+    return BucketLayout.from_manifest(m), [(m, "")]
+
+
+def fill(lib, lay, parts, c, dev):
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    f32 = torch.zeros(max(lay.f32_numel, 64), dtype=torch.float32, device=dev)
+    i64 = torch.zeros(max(lay.i64_numel, 1), dtype=torch.int64, device=dev)
+    for man, pre in parts:
+        for j, e in enumerate(man["keys"]):
+            s = lay.by_key[pre + e["key"]]
+            if s.alias_of is not None:
+                continue
+            if s.kind == KIND_I64:
+                ok(lib, lib.fa_synth_fill_i64(i64[s.offset:].data_ptr(), s.numel, j, c, 0, st),
+                   "fill")
+            else:
+                mu, sg = synth.key_params(e["key"], tuple(e["shape"]), e["dtype"])
+                ok(lib, lib.fa_synth_fill_f32(f32[s.offset:].data_ptr(), s.numel, j, c, mu, sg, 0,
+                                              st), "fill")
+    return f32, i64
+
+
+def main():
+    paths = sys.argv[1:3]
+    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 7
+    which = sys.argv[4].split(",") if len(sys.argv) > 4 else [c[0] for c in CASES]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    libs = [load(p) for p in paths]
+    G = 0x4   # FA_PLAN_GAPS_ARE_PADDING
+    for name, stem, n, rot in CASES:
+        if name not in which:
+            continue
+        lay, parts = layout_of(stem)
+        weighted = name.endswith("w")
+        wts = (ctypes.c_float * n)(*[(1000.0 + 37 * c) / 1e5 for c in range(n)]) if weighted \
+            else None
+        sets = []
+        for _ in range(rot):
+            cl = [fill(libs[0], lay, parts, c, dev) for c in range(n)]
+            sets.append((cl, torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])))
+        plans = []
+        for lib in libs:
+            a32, n32 = segs(lay.segs32)
+            a64, n64 = segs(lay.segs64)
+            h = _P()
+            ok(lib, lib.fa_plan_create(a32, n32, lay.f32_numel, a64, n64, lay.i64_numel, 0, G,
+                                       ctypes.byref(h)), "plan")
+            plans.append(h)
+        ptrs = [((_P * n)(*[c[0].data_ptr() for c in cl]), (_P * n)(*[c[1].data_ptr() for c in cl]),
+                 o32, o64) for cl, o32, o64 in sets]
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+        def call(k, i):
+            p32, p64, o32, o64 = ptrs[i % rot]
+            ok(libs[k], libs[k].fa_reduce(plans[k], p32, p64, n, wts, o32.data_ptr(),
+                                          o64.data_ptr(), 0, st), "reduce")
+        times = [[], []]
+        outs = [None, None]
+        reps = 60 * rot if n > 10 else 200 * rot
+        for _ in range(rounds):
+            for k in (0, 1):
+                for i in range(3 * rot):
+                    call(k, i)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for i in range(reps):
+                    call(k, i)
+                e1.record()
+                e1.synchronize()
+                times[k].append(e0.elapsed_time(e1) / reps * 1e3)
+                outs[k] = (sets[0][1].clone(), sets[0][2].clone())
+        same = (torch.equal(outs[0][0].view(torch.int32), outs[1][0].view(torch.int32))
+                and torch.equal(outs[0][1], outs[1][1]))
+        nb = lay.algorithmic_bytes(n)
+        rec = {"exp": "ab_lib", "case": name, "n": n, "rot": rot, "same_bits": bool(same)}
+        for k, tag in ((0, "a"), (1, "b")):
+            ts = sorted(times[k])
+            rec[tag] = {"lib": paths[k], "us_median": round(ts[len(ts) // 2], 2),
+                        "us_min": round(ts[0], 2),
+                        "frac": round(nb / ts[len(ts) // 2] / 1e3 / 8000, 4)}
+        print(json.dumps(rec), flush=True)
+        del sets, ptrs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

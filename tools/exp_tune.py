@@ -17,9 +17,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402
-from feddct_amd.workload import Reducer, joint_manifest, load_manifest, make_clients  # noqa: E402
+from feddct_amd.workload import (MANIFEST_DIR, Reducer, joint_manifest, load_manifest,  # noqa: E402
+                                 make_clients)
 
-LAYOUTS = {   # name -> (manifest stem, N, rotated sets)
+LAYOUTS = {   # name -> (manifest stem, N, rotated sets[, weighted]); a stem without
+    # _main/_proxy manifests is one model (cfg2 / cfg4)
+    "cfg2": ("wrn16_8_c10", 20, 1),
+    "cfg4w": ("wrn16_8_c100", 20, 1, True),
     "resnet110sl": ("resnet110sl_sf4_c100", 25, 4),
     "sf32": ("wrnsl16_8_sf32_c100", 3, 6),
     "cfg3": ("wrnsl16_8_sf4_c10", 5, 2),
@@ -44,18 +48,27 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     for lname in which:
-        stem, n, rot = LAYOUTS[lname]
-        mans = [load_manifest(stem + "_main"), load_manifest(stem + "_proxy")]
-        lay = BucketLayout.from_manifest(joint_manifest(mans))
+        stem, n, rot = LAYOUTS[lname][:3]
+        weighted = len(LAYOUTS[lname]) > 3
+        if os.path.exists(os.path.join(MANIFEST_DIR, stem + "_main.json")):
+            mans = [load_manifest(stem + "_main"), load_manifest(stem + "_proxy")]
+            lay = BucketLayout.from_manifest(joint_manifest(mans))
+            parts = list(zip(mans, ("0.", "1.")))
+        else:
+            man = load_manifest(stem)
+            lay = BucketLayout.from_manifest(man)
+            parts = man
+        wts = [float(1000 + 37 * c) for c in range(n)] if weighted else None
         sets = []
         for _ in range(rot):
-            cl = make_clients(lay, list(zip(mans, ("0.", "1."))), range(n), dev)
+            cl = make_clients(lay, parts, range(n), dev)
             sets.append((cl, torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])))
         variants = {}
         for k, (te, fl) in VARIANTS.items():
             plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
                              tile_elems=te, flags=G | fl)
-            variants[k] = [Reducer(lay, cl, o32, o64, plan=plan) for cl, o32, o64 in sets]
+            variants[k] = [Reducer(lay, cl, o32, o64, weights=wts, plan=plan)
+                           for cl, o32, o64 in sets]
         ref = None
         times = {k: [] for k in variants}
         for r in range(rounds):
@@ -79,8 +92,9 @@ def main():
         for k, ts in times.items():
             ts = sorted(ts)
             med = ts[len(ts) // 2]
-            nt, sl = variants[k][0].plan.launch_shape(n)
-            print(json.dumps({"exp": "tune", "layout": stem, "n": n, "variant": k,
+            nt, sl = variants[k][0].plan.launch_shape(n, weighted)
+            print(json.dumps({"exp": "tune", "layout": stem, "n": n, "weighted": weighted,
+                              "variant": k,
                               "launch_tiles": nt, "slots": sl,
                               "us_median": round(med, 2), "us_min": round(ts[0], 2),
                               "GBps": round(nb / med / 1e3, 1),
