@@ -689,14 +689,15 @@ def next_rows(dev, steps=30):
     client, glob = _param_module(layout, dev, 1), _param_module(layout, dev, 2)
     P = sum(p_.numel() for p_ in client.parameters())
 
+    # one step as the reference takes it (train_fedprox.py:113-136): the
+    # optimizer zeroes the CLIENT's gradients (optimizer.zero_grad(), torch's
+    # set_to_none default); the global model's accumulate step after step
     def ours():
         client.zero_grad(set_to_none=True)
-        glob.zero_grad(set_to_none=True)
         proximal_term(client, glob).backward()
 
     def reference():
         client.zero_grad(set_to_none=True)
-        glob.zero_grad(set_to_none=True)
         pt = 0.0
         for w, w_t in zip(client.parameters(), glob.parameters()):
             pt += (w - w_t).norm(2)

@@ -32,6 +32,8 @@ FA_F_BCAST = 1
 FA_F_SUM_ONLY = 2
 FA_F_BCAST_ONLY = 4
 FA_PROX_ACCUMULATE = 1
+FA_PROX_ACCUMULATE_A = 2
+FA_PROX_ACCUMULATE_B = 4
 FA_PLAN_GAPS_ARE_PADDING = 1
 FA_PLAN_TUNE_NO_NT = 2
 FA_PLAN_TUNE_BATCH8 = 4

@@ -191,7 +191,7 @@ constexpr size_t kFinLdsMax = 64 * 1024;  // the default dynamic-LDS limit
 // ACC: the gradients are added to what the buckets hold (grad += d, one
 // rounding — what autograd's AccumulateGrad does in place), for parameters
 // whose .grad are views of the buckets (prox.py's one-node backward).
-template <bool ACC>
+template <bool ACC, bool ACCB>
 __global__ __launch_bounds__(kBlk) void prox_grad(const NormChunk* __restrict__ chunks,
                                                   const float* __restrict__ a,
                                                   const float* __restrict__ b,
@@ -219,11 +219,11 @@ __global__ __launch_bounds__(kBlk) void prox_grad(const NormChunk* __restrict__ 
     const int v = threadIdx.x + u * kBlk;
     if (v < nv) {
       const f4 d = g * (xa[u] - xb[u]);
-      if constexpr (ACC) {
-        st4(qa + v, ld4<kNtLoadBwd>(qa + v) + d);
+      if constexpr (ACC) st4(qa + v, ld4<kNtLoadBwd>(qa + v) + d);
+      else st4(qa + v, d);
+      if constexpr (ACCB) {
         if (gb) st4(qb + v, ld4<kNtLoadBwd>(qb + v) - d);
       } else {
-        st4(qa + v, d);
         if (gb) st4(qb + v, -d);
       }
     }
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kBlk) void prox_grad(const NormChunk* __restrict__ 
     const int64_t e = c.start + j;
     const float d = g * (a[e] - b[e]);
     ga[e] = ACC ? ga[e] + d : d;
-    if (gb) gb[e] = ACC ? gb[e] - d : -d;
+    if (gb) gb[e] = ACCB ? gb[e] - d : -d;
   }
 }
 
@@ -331,16 +331,19 @@ int fa_prox_grad_ex(const fa_norm_plan* p, const float* a, const float* b, const
                     unsigned flags, void* stream) {
   if (!p || !a || !b || !norms || !gout || !grad_a)
     return fa::set_err(FA_E_INVAL, "fa_prox_grad: NULL argument");
-  if (flags & ~FA_PROX_ACCUMULATE) return fa::set_err(FA_E_INVAL, "fa_prox_grad_ex: bad flags");
+  if (flags & ~(FA_PROX_ACCUMULATE | FA_PROX_ACCUMULATE_A | FA_PROX_ACCUMULATE_B))
+    return fa::set_err(FA_E_INVAL, "fa_prox_grad_ex: bad flags");
   if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)grad_a | (uintptr_t)grad_b) & 15u)
     return fa::set_err(FA_E_ALIGN, "fa_prox_grad: buckets must be 16-B aligned");
   if (p->nchunks == 0) return FA_OK;
-  if (flags & FA_PROX_ACCUMULATE)
-    hipLaunchKernelGGL(prox_grad<true>, dim3(p->nchunks), dim3(kBlk), 0, (hipStream_t)stream,
-                       p->d_chunks, a, b, norms, gout, alpha, grad_a, grad_b);
-  else
-    hipLaunchKernelGGL(prox_grad<false>, dim3(p->nchunks), dim3(kBlk), 0, (hipStream_t)stream,
-                       p->d_chunks, a, b, norms, gout, alpha, grad_a, grad_b);
+  // per side: accumulate into the bound .grad, or overwrite (a side whose
+  // .grad were all None: no memset of its bucket first)
+  const bool acc_a = flags & (FA_PROX_ACCUMULATE | FA_PROX_ACCUMULATE_A);
+  const bool acc_b = flags & (FA_PROX_ACCUMULATE | FA_PROX_ACCUMULATE_B);
+  auto k = acc_a ? (acc_b ? prox_grad<true, true> : prox_grad<true, false>)
+                 : (acc_b ? prox_grad<false, true> : prox_grad<false, false>);
+  hipLaunchKernelGGL(k, dim3(p->nchunks), dim3(kBlk), 0, (hipStream_t)stream, p->d_chunks, a, b,
+                     norms, gout, alpha, grad_a, grad_b);
   FA_HIP_TRY(hipGetLastError());
   return FA_OK;
 }

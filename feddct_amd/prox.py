@@ -179,20 +179,18 @@ class ProximalTerm:
                 _fa_shim.bind_grads(params, views)
                 st = 0
             states.append(st)
-        live = [st for st in states if st is not None]
-        if not live:
+        if all(st is None for st in states):
             return
-        acc = any(st == 0 for st in live)
-        if acc:   # a side whose .grad were all None starts from zero
-            for (params, views, buf), st in zip(sides, states):
-                if st == 1:
-                    buf.zero_()
+        # per side: accumulate into bound .grad (state 0), overwrite where
+        # every .grad was None (state 1) — no memset of that bucket first
+        flags = ((_lib.FA_PROX_ACCUMULATE_A if states[0] == 0 else 0)
+                 | (_lib.FA_PROX_ACCUMULATE_B if states[1] == 0 else 0))
         (_, _, ba), (_, _, bb) = sides
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         _lib.check(_lib.lib.fa_prox_grad_ex(
             self.plan.handle, self.ca.ptr32, self.ga.ptr32, norms.data_ptr(), gout.data_ptr(),
             1.0, ba.data_ptr() if ba is not None else self._scratch(dev).data_ptr(),
-            None if bb is None else bb.data_ptr(), _lib.FA_PROX_ACCUMULATE if acc else 0, s),
+            None if bb is None else bb.data_ptr(), flags, s),
             "fa_prox_grad_ex")
         for (params, views, buf), st in zip(sides, states):
             if st == 1:

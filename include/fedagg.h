@@ -329,6 +329,10 @@ int fa_prox_grad(const fa_norm_plan *plan, const float *a, const float *b,
 /* FA_PROX_ACCUMULATE: grad_a += (...), grad_b -= (...) instead (autograd's
  * in-place gradient accumulation, for .grad tensors that are bucket views). */
 #define FA_PROX_ACCUMULATE 1u
+/* ... for one side only (the other is overwritten): a training step whose
+ * optimizer zeroed one model's .grad (set_to_none) and not the other's */
+#define FA_PROX_ACCUMULATE_A 2u
+#define FA_PROX_ACCUMULATE_B 4u
 int fa_prox_grad_ex(const fa_norm_plan *plan, const float *a, const float *b,
                     const float *norms, const float *gout, float alpha,
                     float *grad_a, float *grad_b, unsigned flags, void *stream);

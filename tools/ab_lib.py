@@ -82,7 +82,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     libs = [load(p) for p in paths]
-    G = 0x4   # FA_PLAN_GAPS_ARE_PADDING
+    G = 0x1   # FA_PLAN_GAPS_ARE_PADDING
     for name, stem, n, rot in CASES:
         if name not in which:
             continue

@@ -39,6 +39,9 @@ VARIANTS = {
     "batch16": (0, _lib.FA_PLAN_TUNE_BATCH16),
     "batch8": (0, _lib.FA_PLAN_TUNE_BATCH8),
     "batch4": (0, _lib.FA_PLAN_TUNE_BATCH4),
+    "u4": (4096, 0),
+    "u4_batch4": (4096, _lib.FA_PLAN_TUNE_BATCH4),
+    "u1": (1024, 0),
 }
 
 
