@@ -116,10 +116,9 @@ extern "C" {
 #define FA_PLAN_TUNE_TGPU_NARROW 0x200000u /* tuning: torch-GPU order, S = 1 tensors in
                                               1024-element tiles (r02 form)      */
 #define FA_PLAN_TUNE_NO_BALANCE 0x10000000u /* tuning: launch the plain tile table
-                                               only (by default a call whose tiles
-                                               leave the last round of resident
-                                               workgroups under 97 % full runs a
-                                               table re-cut to whole rounds)     */
+                                               with the default batch only (by
+                                               default the launch shape follows
+                                               the round count, below)          */
 /* tuning: packed scalar tiles of 64 >> c columns (c = 0..3; default 64) */
 #define FA_PLAN_TUNE_PACK(c) (((unsigned)(c) & 3u) << 26)
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
@@ -180,19 +179,22 @@ int fa_plan_create_from_tiles(const fa_tile_desc *tiles, int ntiles,
                               int64_t f32_numel, int64_t i64_numel,
                               int tile_elems, unsigned flags, fa_plan **out);
 
-/* ---- balanced tile tables (r03) --------------------------------------------
+/* ---- launch shape by round count (r03) -------------------------------------
  * One workgroup per tile: T tiles over `slots` resident workgroups run
- * ceil(T / slots) rounds, and a part-filled last round costs nearly a full
- * one.  fa_plan_create also keeps, per slot count of the reduce kernels a
- * call may run (queried from the runtime), a table whose vector tiles are
- * re-cut so that packed scalar + vector tiles fill whole rounds (unless the
- * plain table's last round is already >= 97 % full, or
- * FA_PLAN_TUNE_NO_BALANCE).  Any cut reduces bit-identically: the order is
- * per column.
- * fa_plan_balance_host: that re-cut on the host — `vec` are vector tiles
- * (kind 0, at most tile_elems each), `nscalar` the packed scalar tiles
+ * ceil(T / slots) rounds, and while a launch is one or two rounds long a
+ * part-filled round costs nearly a whole one.  A plain fa_reduce call of
+ * N >= 16 clients therefore (a) runs a table whose vector tiles are re-cut
+ * to fill the round when its plain table part-fills ONE round of the
+ * 16-client kernel (below 97 %), (b) runs the 8-client kernel when that
+ * turns two rounds of the 16-client kernel into one, (c) runs the plain
+ * table otherwise (re-cutting a longer launch measured slower).  N < 16
+ * always runs plain.  Slot counts are queried from the runtime.  Any cut
+ * reduces bit-identically: the order is per column.
+ * fa_plan_balance_host: the re-cut of (a) on the host — `vec` are vector
+ * tiles (kind 0, at most tile_elems each), `nscalar` the packed scalar tiles
  * that lead the launch; writes the new vector tiles to `out` (cap entries)
- * and returns their count, 0 when the plain cut is kept, < 0 on error.
+ * and returns their count, 0 when the plain cut is kept (the round is
+ * >= 97 % full or the launch needs more than one round), < 0 on error.
  * fa_plan_launch_shape: the tiles and resident-workgroup slots a plain
  * fa_reduce call with n clients (weighted or not) launches with. */
 int fa_plan_balance_host(const fa_tile_desc *vec, int nvec, int tile_elems,
