@@ -77,3 +77,37 @@ def test_prox_tiny_and_ragged():
     (norms, total), = _run(segs, numel, a, b)[0]
     torch.testing.assert_close(norms, want, rtol=1e-6, atol=0)
     torch.testing.assert_close(total, want.sum(), rtol=1e-6, atol=0)
+
+
+def test_interleaved_plans():
+    """Two norm plans launched alternately on one stream (each with its own
+    partials buffer): results match torch and are identical launch after
+    launch."""
+    from feddct_amd import _lib
+    from feddct_amd.prox import _NormPlan
+    g = torch.Generator(device=DEV).manual_seed(11)
+    res = []
+    plans = []
+    for numel, nseg in ((300_000, 7), (1_000_000, 40)):
+        cut = np.linspace(0, numel, nseg + 1).astype(np.int64) // 64 * 64
+        segs = np.stack([cut[:-1], cut[1:] - cut[:-1]], 1)
+        a = torch.randn(numel, device=DEV, generator=g)
+        b = torch.randn(numel, device=DEV, generator=g)
+        with torch.cuda.device(DEV):
+            plans.append((_NormPlan(segs, numel), segs, a, b))
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = [[], []]
+    for _ in range(4):
+        for k, (plan, segs, a, b) in enumerate(plans):
+            norms = torch.empty(len(segs), device=DEV)
+            total = torch.empty((), device=DEV)
+            _lib.check(_lib.lib.fa_prox_norms(plan.handle, a.data_ptr(), b.data_ptr(),
+                                              norms.data_ptr(), total.data_ptr(), st))
+            outs[k].append((norms, total))
+    torch.cuda.synchronize()
+    for k, (plan, segs, a, b) in enumerate(plans):
+        want = torch.stack([(a[o:o + m] - b[o:o + m]).norm(2) for o, m in segs])
+        n0, t0 = outs[k][0]
+        torch.testing.assert_close(n0, want, rtol=1e-5, atol=0)
+        for n, t in outs[k][1:]:
+            assert torch.equal(n, n0) and torch.equal(t, t0)

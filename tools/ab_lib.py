@@ -22,7 +22,9 @@ from feddct_amd.workload import joint_manifest, load_manifest  # noqa: E402
 
 _P, _I, _I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
 CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
-         ("cfg3", "wrnsl16_8_sf4_c10", 5, 2), ("resnet110sl", "resnet110sl_sf4_c100", 25, 4)]
+         ("cfg3", "wrnsl16_8_sf4_c10", 5, 2), ("resnet110sl", "resnet110sl_sf4_c100", 25, 4),
+         # torch-ROCm's GPU order (fa_plan_create_order, FA_ORDER_TORCH_GPU)
+         ("cfg2_tgpu", "wrn16_8_c10", 20, 1), ("cfg3_tgpu", "wrnsl16_8_sf4_c10", 5, 2)]
 
 
 def load(path):
@@ -30,6 +32,8 @@ def load(path):
     lib.fa_plan_create.argtypes = [_P, _I, _I64, _P, _I, _I64, _I, ctypes.c_uint,
                                    ctypes.POINTER(_P)]
     lib.fa_reduce.argtypes = [_P, _P, _P, _I, _P, _P, _P, ctypes.c_uint, _P]
+    lib.fa_plan_create_order.argtypes = [_P, _I, _I64, _P, _I, _I64, _I, _I, ctypes.c_uint,
+                                         ctypes.POINTER(_P)]
     lib.fa_synth_fill_f32.argtypes = [_P, _I64, _I, _I, ctypes.c_float, ctypes.c_float, _I, _P]
     lib.fa_synth_fill_i64.argtypes = [_P, _I64, _I, _I, _I, _P]
     lib.fa_last_error.restype = ctypes.c_char_p
@@ -99,8 +103,12 @@ def main():
             a32, n32 = segs(lay.segs32)
             a64, n64 = segs(lay.segs64)
             h = _P()
-            ok(lib, lib.fa_plan_create(a32, n32, lay.f32_numel, a64, n64, lay.i64_numel, 0, G,
-                                       ctypes.byref(h)), "plan")
+            if name.endswith("_tgpu"):
+                ok(lib, lib.fa_plan_create_order(a32, n32, lay.f32_numel, a64, n64, lay.i64_numel,
+                                                 n, 1, G, ctypes.byref(h)), "plan")
+            else:
+                ok(lib, lib.fa_plan_create(a32, n32, lay.f32_numel, a64, n64, lay.i64_numel, 0,
+                                           G, ctypes.byref(h)), "plan")
             plans.append(h)
         ptrs = [((_P * n)(*[c[0].data_ptr() for c in cl]), (_P * n)(*[c[1].data_ptr() for c in cl]),
                  o32, o64) for cl, o32, o64 in sets]
