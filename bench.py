@@ -126,6 +126,90 @@ class PhaseDeadline:
         return False
 
 
+def gpu_state_under_load(fn, max_s=20.0):
+    """Clocks, power and temperatures of this GPU sampled by `rocm-smi` (a
+    child process: it reads the driver's sysfs) WHILE `fn` — the headline's
+    reduce — keeps the GPU busy, so the line says at what clocks its number
+    was taken (box-to-box the same tree measured 133.5-144 us per launch,
+    DESIGN §4).  None when the tool is absent; a dict with "error" when it
+    fails or outlives `max_s`."""
+    import shutil
+    import subprocess
+    exe = shutil.which("rocm-smi") or ("/opt/rocm/bin/rocm-smi"
+                                       if os.path.exists("/opt/rocm/bin/rocm-smi") else None)
+    if exe is None:
+        return None
+    idx = torch.cuda.current_device()
+    try:
+        proc = subprocess.Popen([exe, "-d", str(idx), "--showclocks", "--showpower",
+                                 "--showtemp", "--showmemuse", "--showserial", "--json"],
+                                stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+    except OSError as e:
+        return {"error": repr(e)}
+    t0 = time.perf_counter()
+    launches = 0
+    while proc.poll() is None and time.perf_counter() - t0 < max_s:
+        for _ in range(20):
+            fn()
+        launches += 20
+        torch.cuda.synchronize()
+    if proc.poll() is None:
+        proc.kill()
+        proc.communicate()
+        return {"error": f"rocm-smi still running after {max_s:.0f} s"}
+    st = parse_smi(proc.communicate()[0])
+    if "error" not in st:
+        st = {"sampled_during": f"{launches} headline launches", **st}
+    return st
+
+
+def gpu_state_idle(max_s=20.0):
+    """The same fields before this process allocates anything: memory
+    already allocated on the GPU by others (a box measured with 81 % of its
+    VRAM taken while idle ran this bench 5-7 % slower than boxes at 1 %)."""
+    import shutil
+    import subprocess
+    exe = shutil.which("rocm-smi") or ("/opt/rocm/bin/rocm-smi"
+                                       if os.path.exists("/opt/rocm/bin/rocm-smi") else None)
+    if exe is None:
+        return None
+    idx = int(os.environ.get("LOCAL_RANK", "0"))
+    try:
+        r = subprocess.run([exe, "-d", str(idx), "--showclocks", "--showpower", "--showtemp",
+                            "--showmemuse", "--json"], capture_output=True, text=True,
+                           timeout=max_s)
+    except (OSError, subprocess.TimeoutExpired) as e:
+        return {"error": repr(e)}
+    st = parse_smi(r.stdout)
+    st.pop("serial", None)
+    return st
+
+
+def parse_smi(out: str) -> dict:
+    """The fields gpu_state_under_load reports from `rocm-smi --json` text
+    (warning lines before the JSON are skipped)."""
+    import re
+    try:
+        card = next(iter(json.loads(out[out.index("{"):]).values()))
+    except (ValueError, StopIteration) as e:
+        return {"error": f"unparsed rocm-smi output: {e!r}"}
+
+    def num(key_part):
+        for k, v in card.items():
+            if key_part.lower() in k.lower():
+                m = re.search(r"[-+]?\d+(\.\d+)?", str(v))
+                if m:
+                    return float(m.group(0))
+        return None
+    return {"sclk_mhz": num("sclk clock speed"),
+            "mclk_mhz": num("mclk clock speed"), "fclk_mhz": num("fclk clock speed"),
+            "socket_power_w": num("Current Socket Graphics Package Power"),
+            "junction_c": num("Temperature (Sensor junction)"),
+            "memory_c": num("Temperature (Sensor memory)"),
+            "vram_used_pct": num("GPU Memory Allocated"),
+            "serial": next((str(v) for k, v in card.items() if "serial" in k.lower()), None)}
+
+
 def digest_of(layout, out32, out64, prefix=""):
     """SHA-256 of the keys under ``prefix`` (stripped), as tests/golden does."""
     import hashlib
@@ -1173,6 +1257,12 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if args.same_device:
         local_rank = 0
+    idle_state = None
+    if world == 1 and not args.kernel_only:
+        try:
+            idle_state = gpu_state_idle()
+        except Exception as e:  # noqa: BLE001  (reported, never fatal)
+            idle_state = {"error": repr(e)}
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     group = None
@@ -1194,6 +1284,8 @@ def main():
     torch.cuda.synchronize()
 
     extra = {}
+    if idle_state is not None:
+        extra["gpu_state_idle"] = idle_state
     ncomm = None
     if not multi:
         per = []
@@ -1241,6 +1333,10 @@ def main():
             # any clock ramp across K launches
             timed_launches(reducer, args.steps, 20, per_launch=per)
             extra["headline_launch"] = launch_stats(per)
+            try:
+                extra["gpu_state"] = gpu_state_under_load(reducer)
+            except Exception as e:  # noqa: BLE001  (reported, never fatal)
+                extra["gpu_state"] = {"error": repr(e)}
             with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
                 want = json.load(f)[f"fedavg/{LAYOUT}/n{N_CLIENTS}"]
             got = digest_of(layout, out32, out64)

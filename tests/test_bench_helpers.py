@@ -72,3 +72,20 @@ def test_build_line_keeps_the_bench_contract():
     assert abs(r["frac"] - nb / t_kernel / 1e9 / bench.HBM_PEAK_GBS) < 1e-3
     assert "blocked/native" in line["config"]["parallelism"]
     assert line["config"]["algorithmic_bytes_per_step"] == 2 * nb
+
+
+def test_parse_smi_reads_clocks_power_and_temperatures():
+    """bench.gpu_state_under_load's parser on rocm-smi --json text as the box
+    prints it (a warning line first)."""
+    import bench
+    out = ('WARNING: AMD GPU device(s) is/are in a low-power state.\n'
+           '{"card0": {"Temperature (Sensor junction) (C)": "46.0", '
+           '"Temperature (Sensor memory) (C)": "33.0", "fclk clock speed:": "(1250Mhz)", '
+           '"mclk clock speed:": "(2000Mhz)", "sclk clock speed:": "(2400Mhz)", '
+           '"Current Socket Graphics Package Power (W)": "812.0", '
+           '"GPU Memory Allocated (VRAM%)": "81", "Serial Number": "692533015330"}}')
+    st = bench.parse_smi(out)
+    assert st == {"sclk_mhz": 2400.0, "mclk_mhz": 2000.0, "fclk_mhz": 1250.0,
+                  "socket_power_w": 812.0, "junction_c": 46.0, "memory_c": 33.0,
+                  "vram_used_pct": 81.0, "serial": "692533015330"}
+    assert "error" in bench.parse_smi("no json here")
