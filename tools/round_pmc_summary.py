@@ -1,7 +1,10 @@
 """Per-kernel time and HBM traffic from rocprofv3 runs of tools/round_prof.py
 (kernel trace + separate FETCH_SIZE / WRITE_SIZE passes):
 
-    python tools/round_pmc_summary.py <trace_dir> <fetch_dir> <write_dir> <out.json>
+    python tools/round_pmc_summary.py <trace_dir> <fetch_dir> <write_dir> <out.json> [ALGO]
+
+(ALGO: the launch's algorithmic bytes for another layout than cfg2, e.g. a
+FedDCT sweep layout from round_prof.py's sweep modes.)
 
 Counters are KiB per dispatch (median over dispatches); FETCH_SIZE is also
 given x2, the MI355X_MICROARCH.md §HBM correction for wide coalesced
@@ -24,6 +27,9 @@ ALGO = {"reduce_kernel": N * B + B, "tgpu_kernel": N * B + B, "bcast_group_kerne
 
 def main():
     trace_dir, fetch_dir, write_dir, out = sys.argv[1:5]
+    if len(sys.argv) > 5:
+        for t in ALGO:
+            ALGO[t] = int(sys.argv[5])
     fetch = per_kernel(fetch_dir, "FETCH_SIZE")
     write = per_kernel(write_dir, "WRITE_SIZE")
     res = []
