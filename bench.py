@@ -39,7 +39,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from feddct_amd import _lib  # noqa: E402  (loads libfedagg.so or fails loudly)
+from feddct_amd import _lib, slab  # noqa: E402  (loads libfedagg.so or fails loudly)
 from feddct_amd.layout import BucketLayout  # noqa: E402
 from feddct_amd.workload import Reducer, load_manifest, make_clients  # noqa: E402
 
@@ -432,6 +432,29 @@ def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
                                                torch.equal(out_p64, out64.cpu()))
     del pageable
     return res
+
+
+def separate_allocations_ab(layout, clients, reducer, out32, out64, rounds=3, k=50):
+    """The headline's reduce over its slab-carved buckets (slab.py, the
+    product's storage) against the same values in 20 + 1 separate
+    allocations (the r02 storage), interleaved in this process: on some
+    boxes the separate allocations read ~8 % slower
+    (profiles/r03_exp_alloc.jsonl)."""
+    sep = [(c32.clone(), c64) for c32, c64 in clients]
+    o32 = torch.zeros_like(out32)
+    o64 = torch.zeros_like(out64)
+    red = Reducer(layout, sep, o32, o64, plan=reducer.plan)
+    ts = {"slab": [], "separate": []}
+    for _ in range(rounds):
+        ts["slab"].append(timed_launches(reducer, k, 5)[0])
+        ts["separate"].append(timed_launches(red, k, 5)[0])
+    med = {n: sorted(v)[len(v) // 2] for n, v in ts.items()}
+    out = {f"{n}_us": round(t * 1e6, 2) for n, t in med.items()}
+    out["separate_over_slab"] = round(med["separate"] / med["slab"], 4)
+    out["bit_equal"] = bool(torch.equal(o32.view(torch.int32), out32.view(torch.int32))
+                            and torch.equal(o64, out64))
+    del sep, red
+    return out
 
 
 def other_configs(dev, steps=100, warmup=20):
@@ -1277,7 +1300,9 @@ def main():
     layout = BucketLayout.from_manifest(manifest)
     first = rank * N_CLIENTS
     clients = make_clients(layout, manifest, range(first, first + N_CLIENTS), dev)
-    out32 = torch.zeros_like(clients[0][0])
+    # the global's bucket from the same slab as the clients' (slab.py), as the
+    # drop-in's arenas place them
+    out32 = slab.carve(clients[0][0].numel(), torch.float32, dev)
     out64 = torch.zeros_like(clients[0][1])
     reducer = Reducer(layout, clients, out32, out64)
     nbytes_rank = layout.algorithmic_bytes(N_CLIENTS)
@@ -1306,7 +1331,17 @@ def main():
                                                 torch.cuda.current_stream().cuda_stream))
             tc, _ = timed_launches(copy_big, 100, 3)   # ~33 ms of streaming
             extra["copy_ceiling_GBps"] = round(2 * big.numel() * 4 / tc / 1e9, 1)
-            del big, big2
+            # and its read-only ceiling (the reduce is 95 % reads): the same
+            # 1 GiB read in the reduce's own tile shape, nothing stored
+            sink = torch.zeros(256, dtype=torch.float32, device=dev)
+
+            def read_big():
+                _lib.check(_lib.lib.fa_read_probe_f32(big.data_ptr(), big.numel(),
+                                                      sink.data_ptr(), 0,
+                                                      torch.cuda.current_stream().cuda_stream))
+            tr, _ = timed_launches(read_big, 100, 3)   # ~15 ms of streaming
+            extra["read_ceiling_GBps"] = round(big.numel() * 4 / tr / 1e9, 1)
+            del big, big2, sink
             # weighted variant (client-size weights, BASELINE config 4's extension)
             from feddct_amd.aggregate import client_weights as weights_from_sizes
             w = weights_from_sizes(np.arange(1, N_CLIENTS + 1))
@@ -1321,6 +1356,13 @@ def main():
         # warm-ups
         t_step, wall = timed_launches(reducer, args.steps, args.warmup)
         t_kernel = t_step
+        if "read_ceiling_GBps" in extra:
+            # this box's own bound: the headline as a fraction of the copy and
+            # of the read-only rate measured just before it
+            gbs = nbytes_rank / t_step / 1e9
+            extra["headline_vs_box_ceilings"] = {
+                "copy": round(gbs / extra["copy_ceiling_GBps"], 4),
+                "read_only": round(gbs / extra["read_ceiling_GBps"], 4)}
         if not args.kernel_only:
             timed_launches(wred, max(100, args.steps // 2), 20, per_launch=wper)
             extra["weighted_launch"] = launch_stats(wper)
@@ -1333,6 +1375,8 @@ def main():
             # any clock ramp across K launches
             timed_launches(reducer, args.steps, 20, per_launch=per)
             extra["headline_launch"] = launch_stats(per)
+            extra["slab_vs_separate_allocations"] = separate_allocations_ab(
+                layout, clients, reducer, out32, out64)
             try:
                 extra["gpu_state"] = gpu_state_under_load(reducer)
             except Exception as e:  # noqa: BLE001  (reported, never fatal)

@@ -611,6 +611,24 @@ __global__ __launch_bounds__(kBlock) void read_probe_kernel(const float* __restr
   if ((threadIdx.x & 63) == 0) atomicAdd(out + blockIdx.x, s);
 }
 
+// Read-only probe in the reduce's own shape (grid = 0 in fa_read_probe_f32):
+// one tile of 2 x 1024 floats per workgroup, 2 independent 16-B
+// non-temporal loads per lane, no loop, and no store unless the tile's sum
+// hits a sentinel value (so nothing but the reads reaches HBM).  The lab's
+// fastest read-only form (tools/bwlab.hip one_stream_read_only_U2: 7.0-7.1
+// TB/s, profiles/r01_bwlab.jsonl) — the read ceiling of a box, which the
+// reduce (95 % reads) is compared with; the grid-stride form above runs
+// ~10 % slower.
+__global__ __launch_bounds__(kBlock) void read_tile_kernel(const float* __restrict__ src,
+                                                           int64_t nv, float* __restrict__ out) {
+  const int64_t v0 = blockIdx.x * (int64_t)(2 * kBlock) + threadIdx.x, v1 = v0 + kBlock;
+  f4 a = f4{0.f, 0.f, 0.f, 0.f}, b = a;
+  if (v0 < nv) a = ld4<true>(src + 4 * v0);
+  if (v1 < nv) b = ld4<true>(src + 4 * v1);
+  const f4 s = a + b;
+  if (s.x == 1234.5f && s.y == -1.0f && s.z == 7.0f) out[threadIdx.x] = s.w;
+}
+
 // ------------------------------------------- synthetic state (synth.py) --
 __device__ __forceinline__ uint64_t hash64(uint64_t seed, uint64_t idx) {
   uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx * 0xD1B54A32D192ED03ull;
@@ -2081,10 +2099,17 @@ int fa_synth_fill_i64(int64_t* dst, int64_t numel, int key_index, int client, in
 }
 
 int fa_read_probe_f32(const float* src, int64_t numel, float* out, int grid, void* stream) {
-  if (numel < 4 || !src || !out || grid < 1) return set_err(FA_E_INVAL, "fa_read_probe_f32: bad args");
+  if (numel < 4 || !src || !out || grid < 0) return set_err(FA_E_INVAL, "fa_read_probe_f32: bad args");
   if (!aligned16(src)) return set_err(FA_E_ALIGN, "fa_read_probe_f32: unaligned");
-  hipLaunchKernelGGL(read_probe_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, src,
-                     numel / 4, out);
+  if (grid == 0) {  // one 2048-float tile per workgroup (whole float4s only)
+    const int64_t nv = numel / 4, g = (nv + 2 * kBlock - 1) / (2 * kBlock);
+    if (g > 0x7fffffff) return set_err(FA_E_RANGE, "fa_read_probe_f32: %lld floats", (long long)numel);
+    hipLaunchKernelGGL(read_tile_kernel, dim3((unsigned)g), dim3(kBlock), 0, (hipStream_t)stream,
+                       src, nv, out);
+  } else {
+    hipLaunchKernelGGL(read_probe_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, src,
+                       numel / 4, out);
+  }
   HIP_TRY(hipGetLastError());
   return FA_OK;
 }

@@ -20,7 +20,7 @@ from typing import Sequence
 
 import torch
 
-from . import _lib
+from . import _lib, slab
 from .layout import BucketLayout
 from .partition import range_plans
 
@@ -32,11 +32,12 @@ class HostPipeline:
         self.device = device
         with torch.cuda.device(device):
             self.ranges, self.plan64 = range_plans(layout, nchunks, tile_elems)
-            self.dev32 = [torch.empty(max(layout.f32_numel, 64), dtype=torch.float32,
-                                      device=device) for _ in range(n)]
+            # the staged client buckets side by side in one slab (slab.py)
+            self.dev32 = [slab.carve(max(layout.f32_numel, 64), torch.float32, device)
+                          for _ in range(n)]
             self.dev64 = [torch.empty(max(layout.i64_numel, 1), dtype=torch.int64,
                                       device=device) for _ in range(n)]
-            self.out32 = torch.zeros_like(self.dev32[0])
+            self.out32 = slab.carve(self.dev32[0].numel(), torch.float32, device)
             self.out64 = torch.zeros_like(self.dev64[0])
             self.s_in = torch.cuda.Stream(device)
             self.s_out = torch.cuda.Stream(device)

@@ -14,6 +14,7 @@ from typing import List, Tuple
 import torch
 
 from . import _lib, synth
+from .arena import alloc_buckets
 from .layout import KIND_I64, BucketLayout
 
 MANIFEST_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "manifests")
@@ -58,8 +59,9 @@ def make_clients(layout: BucketLayout, manifest, clients, device,
     parts = manifest if isinstance(manifest, list) else [(manifest, "")]
     out = []
     for c in clients:
-        f32 = torch.zeros(max(layout.f32_numel, 64), dtype=torch.float32, device=device)
-        i64 = torch.zeros(max(layout.i64_numel, 1), dtype=torch.int64, device=device)
+        # the product's own storage: fp32 buckets carved from a shared slab
+        # on a GPU (arena.alloc_buckets, slab.py)
+        f32, i64 = alloc_buckets(layout, torch.device(device))
         for m, prefix in parts:
             fill_client(layout, m, f32, i64, c, mode, prefix)
         out.append((f32, i64))

@@ -341,8 +341,11 @@ int fa_prox_grad_ex(const fa_norm_plan *plan, const float *a, const float *b,
 
 /* Streaming copy (bandwidth ceiling calibration for the roofline). */
 int fa_copy_f32(const float *src, float *dst, int64_t numel, void *stream);
-/* Read-only streaming probe (read-bandwidth ceiling): out[grid] partial sums
- * (accumulated: zero out first). */
+/* Read-only streaming probe (read-bandwidth ceiling): grid > 0 — a
+ * grid-stride loop, out[grid] partial sums (accumulated: zero out first);
+ * grid == 0 — one 2048-float tile per workgroup, the reduce's own load shape,
+ * nothing stored (out: >= 256 floats of scratch, never read; the last numel %
+ * 4 floats are not read). */
 int fa_read_probe_f32(const float *src, int64_t numel, float *out, int grid,
                       void *stream);
 

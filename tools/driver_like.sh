@@ -8,6 +8,6 @@ timeout -k 10 420 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $out 2> ${ou
 python3 - "$out" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print(d["value"], d["roofline"]["frac"], d["copy_ceiling_GBps"], d["round_with_broadcast_us"],
+print(d["value"], d["roofline"]["frac"], d["copy_ceiling_GBps"], d.get("read_ceiling_GBps"), d.get("headline_vs_box_ceilings"), d["round_with_broadcast_us"],
       d["dropin"], d["torch_gpu_order_mode"], d["headline_launch"])
 PY
