@@ -13,7 +13,7 @@ N = 20), one process, interleaved rounds, bits compared:
 plus this box's read-only rate over the same 20 x B bytes (read probe over
 the arena_256 allocation) and a copy of one bucket's worth x 20.
 
-    python tools/exp_alloc.py [ROUNDS]
+    python tools/exp_alloc.py [ROUNDS]     |     python tools/exp_alloc.py order
 """
 import json
 import sys
@@ -31,7 +31,61 @@ N = 20
 MIB2 = 2 << 20
 
 
+def order_mode(rounds):
+    """Separate vs one allocation, alternating in allocation order (sep1,
+    one1, sep2, one2, sep3, one3): does a set's speed follow its form or
+    the order (memory state) it was allocated in?"""
+    dev = torch.device("cuda", 0)
+    man = load_manifest("wrn16_8_c10")
+    lay = BucketLayout.from_manifest(man)
+    nb = lay.algorithmic_bytes(N)
+    plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
+                     flags=_lib.FA_PLAN_GAPS_ARE_PADDING)
+    src = make_clients(lay, man, range(N), dev)
+    n32 = src[0][0].numel()
+    s = (n32 * 4 + 255) // 256 * 256 // 4
+    reds, keep = {}, []
+    for i in range(1, 4):
+        sep = [(c32.clone(), c64) for c32, c64 in src]
+        reds[f"sep{i}"] = Reducer(lay, sep, torch.zeros_like(src[0][0]),
+                                  torch.zeros_like(src[0][1]), plan=plan)
+        a = torch.empty(N * s, dtype=torch.float32, device=dev)
+        keep.append(a)
+        one = []
+        for j in range(N):
+            v = a[j * s:j * s + n32]
+            v.copy_(src[j][0])
+            one.append((v, src[j][1]))
+        reds[f"one{i}"] = Reducer(lay, one, torch.zeros_like(src[0][0]),
+                                  torch.zeros_like(src[0][1]), plan=plan)
+    del src
+    times = {k: [] for k in reds}
+    for _ in range(rounds):
+        for k, fn in reds.items():
+            for _ in range(5):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(50):
+                fn()
+            e1.record()
+            e1.synchronize()
+            times[k].append(e0.elapsed_time(e1) / 50 * 1e3)
+        print("round", file=sys.stderr, flush=True)
+    ref = reds["sep1"].out32.view(torch.int32)
+    for k, ts in times.items():
+        ts = sorted(ts)
+        med = ts[len(ts) // 2]
+        print(json.dumps({"exp": "alloc_order", "variant": k, "us_median": round(med, 2),
+                          "us_min": round(ts[0], 2), "GBps": round(nb / med / 1e3, 1),
+                          "frac": round(nb / med / 1e3 / 8000, 4),
+                          "bit_equal": bool(torch.equal(reds[k].out32.view(torch.int32), ref))}),
+              flush=True)
+
+
 def main():
+    if "order" in sys.argv[1:]:
+        return order_mode(5)
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 7
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
