@@ -5,7 +5,7 @@ before any xGMI traffic — the local floor of bench N>1.  One JSON line per
 form: GPU time per step (HIP events over K steps) and host issue time per
 step (wall time of the K step() calls, no sync inside).
 
-    python tools/native_round_cost.py [K] [--no-graphs]
+    python tools/native_round_cost.py [K] [--no-graphs] [--only=form,form]
 """
 import json
 import os
@@ -70,7 +70,10 @@ def main():
     mask = torch.zeros(lay.f32_numel, dtype=torch.bool, device=dev)
     for o, m in lay.segs32:
         mask[int(o):int(o + m)] = True
+    only = [a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--only=")]
     for name, make in forms.items():
+        if only and name not in only[0].split(","):
+            continue
         o32 = torch.full_like(ref32, float("nan"))
         o64 = torch.zeros_like(ref64)
         fn = make(o32, o64)
