@@ -369,9 +369,11 @@ def _cpu_model():
 def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
     """Client buckets in pinned host memory, result back to host.
     serial:    H2D of N·B, one kernel, D2H of B, one stream;
-    pipelined: feddct_amd/pipeline.py (8 column chunks, H2D / reduce / D2H
+    pipelined: feddct_amd/pipeline.py (column chunks, H2D / reduce / D2H
                overlapped on two copy streams), result to the global only,
-               and with the broadcast (D2H into all N client buckets too);
+               and with the broadcast into all N client buckets too
+               (tapered chunks; pipelined_even8: r02's 8 even chunks; the
+               broadcast fanned out on the CPU, _dma: N D2H copies per chunk);
     serial_pageable: the serial round from ordinary (pageable) host tensors
                and into a pageable result (SURVEY.md §8 d asks for both)."""
     from feddct_amd.pipeline import HostPipeline
@@ -403,15 +405,22 @@ def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
         out_p64.copy_(out64, non_blocking=True)
         torch.cuda.synchronize()
 
-    pipe = HostPipeline(layout, n, out32.device)
+    pipe = HostPipeline(layout, n, out32.device)            # tapered chunks (r03)
+    pipe8 = HostPipeline(layout, n, out32.device, nchunks=8)   # r02's even cut
     h32 = [h[0] for h in host]
     h64 = [h[1] for h in host]
 
     def piped():
         pipe.run(h32, h64, out_h32, out_h64)
 
-    def piped_bcast():
+    def piped_even8():
+        pipe8.run(h32, h64, out_h32, out_h64)
+
+    def piped_bcast():          # broadcast: one D2H per chunk, CPU fan-out
         pipe.run(h32, h64, out_h32, out_h64, h32, h64)
+
+    def piped_bcast_dma():      # broadcast: N + 1 D2H per chunk (r02)
+        pipe.run(h32, h64, out_h32, out_h64, h32, h64, fanout="dma")
 
     res = {"source": "pinned", "algorithmic_bytes": nbytes}
     # the pipelined result is the same bits as the device-resident one
@@ -421,7 +430,9 @@ def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
     res["pipelined_bit_exact"] = bool(torch.equal(out_h32, out32.cpu()) and
                                       torch.equal(out_h64, out64.cpu()))
     for name, fn in (("serial", serial), ("serial_pageable", serial_pageable),
-                     ("pipelined", piped), ("pipelined_with_broadcast", piped_bcast)):
+                     ("pipelined", piped), ("pipelined_even8", piped_even8),
+                     ("pipelined_with_broadcast", piped_bcast),
+                     ("pipelined_with_broadcast_dma", piped_bcast_dma)):
         fn()
         t0 = time.perf_counter()
         for _ in range(reps):

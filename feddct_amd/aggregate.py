@@ -229,7 +229,8 @@ class Engine:
     def _reduce_host(self, layout, ga: ModuleArena, cas: List[ModuleArena], weights, fuse):
         """Host-resident state (the reference's CPU configuration): the
         chunked H2D / reduce / D2H pipeline (pipeline.py) over the modules'
-        pinned arenas; the broadcast is part of the D2H stream."""
+        pinned arenas; the broadcast fans each downloaded chunk out to the
+        clients' host buckets on the CPU while later chunks upload."""
         from .pipeline import HostPipeline
         n = len(cas)
         dev = (ga.device if ga.device.type == "cuda"

@@ -33,17 +33,25 @@ def layout_tiles(layout: BucketLayout, tile_elems: int = 0):
                          layout.segs64.tobytes(), layout.i64_numel, tile_elems)
 
 
-def cut_index(t: np.ndarray, parts: int) -> List[int]:
+def cut_index(t: np.ndarray, parts: int, fractions=None) -> List[int]:
     """Group boundaries (tile indices, len parts+1) of the sorted tiles ``t``
-    into ``parts`` runs of about equal element count, cut only before a
-    vector tile on a 256-B boundary — fedcomm.hip's cut_tiles, the same rule
-    the native schedules use."""
+    into ``parts`` runs of about equal element count (or of the given
+    ``fractions`` of it, which sum to 1), cut only before a vector tile on a
+    256-B boundary — fedcomm.hip's cut_tiles, the same rule the native
+    schedules use."""
     total = int(t[:, 1].sum()) if len(t) else 0
+    if fractions is None:
+        goal = [total * k // parts for k in range(parts)]
+    else:
+        if len(fractions) != parts:
+            raise ValueError("one fraction per part")
+        cum = np.concatenate([[0.0], np.cumsum(fractions)])
+        goal = [int(total * cum[k]) for k in range(parts)]
     cut = [0]
     acc = 0
     for i, (s, c, kind) in enumerate(t):
         k = len(cut)
-        if k < parts and i > 0 and acc >= total * k // parts and kind == 0 and s % 64 == 0:
+        if k < parts and i > 0 and acc >= goal[k] and kind == 0 and s % 64 == 0:
             cut.append(i)
         acc += int(c)
     while len(cut) < parts + 1:
@@ -51,14 +59,15 @@ def cut_index(t: np.ndarray, parts: int) -> List[int]:
     return cut
 
 
-def split_tiles(tiles: np.ndarray, parts: int, f32_numel: int
+def split_tiles(tiles: np.ndarray, parts: int, f32_numel: int, fractions=None
                 ) -> List[Tuple[int, int, np.ndarray]]:
     """Cut the fp32 tiles into ``parts`` contiguous ranges of about equal
-    element count.  Returns [(lo, hi, tiles_in_range)], covering
-    [0, f32_numel) exactly (some ranges may be empty)."""
+    element count (or ``fractions`` of it).  Returns [(lo, hi,
+    tiles_in_range)], covering [0, f32_numel) exactly (some ranges may be
+    empty)."""
     t32 = tiles[tiles[:, 2] < K_I64_MIN]
     t32 = t32[np.argsort(t32[:, 0], kind="stable")]
-    ci = cut_index(t32, parts)
+    ci = cut_index(t32, parts, fractions)
     cuts = [0] + [int(t32[ci[g], 0]) if ci[g] < len(t32) else f32_numel
                   for g in range(1, parts)]
     cuts.append(f32_numel)
@@ -74,14 +83,15 @@ def i64_tiles(tiles: np.ndarray) -> np.ndarray:
     return tiles[tiles[:, 2] >= K_I64_MIN]
 
 
-def range_plans(layout: BucketLayout, parts: int, tile_elems: int = 0, flags=None):
+def range_plans(layout: BucketLayout, parts: int, tile_elems: int = 0, flags=None,
+                fractions=None):
     """[(lo, hi, Plan or None)] for each fp32 range, plus the int64 Plan."""
     if flags is None:
         flags = _lib.FA_PLAN_GAPS_ARE_PADDING
     info, tiles = layout_tiles(layout, tile_elems)
     te = info["tile_elems"]
     out = []
-    for lo, hi, sel in split_tiles(tiles, parts, layout.f32_numel):
+    for lo, hi, sel in split_tiles(tiles, parts, layout.f32_numel, fractions):
         p = (_lib.Plan(None, layout.f32_numel, None, layout.i64_numel, te, flags, tiles=sel)
              if len(sel) else None)
         out.append((lo, hi, p))

@@ -571,7 +571,8 @@ def test_range_plans_union_is_bit_exact(lib, parts):
             assert bits_equal(a, b), s.key
 
 
-def test_host_pipeline_bit_exact_with_broadcast(lib):
+@pytest.mark.parametrize("nchunks,fanout", [(6, "dma"), (6, "host"), (0, "host"), (0, "dma")])
+def test_host_pipeline_bit_exact_with_broadcast(lib, nchunks, fanout):
     from feddct_amd.pipeline import HostPipeline
     from feddct_amd.workload import make_clients
     man = load_manifest("wrn16_8_c10")
@@ -583,7 +584,7 @@ def test_host_pipeline_bit_exact_with_broadcast(lib):
     h64 = [c[1].cpu().pin_memory() for c in cl]
     o32 = torch.zeros_like(h32[0]).pin_memory()
     o64 = torch.zeros_like(h64[0]).pin_memory()
-    pipe = HostPipeline(layout, n, DEV, nchunks=6)
+    pipe = HostPipeline(layout, n, DEV, nchunks=nchunks, fanout=fanout)
     want = buckets_to_state(layout, full32, full64)
 
     def same(b32, b64):
@@ -594,6 +595,13 @@ def test_host_pipeline_bit_exact_with_broadcast(lib):
         assert same(o32, o64)
     pipe.run(h32, h64, o32, o64, h32[1:3], h64[1:3])
     assert same(h32[2], h64[2]) and same(h32[1], h64[1]) and same(o32, o64)
+    # the reference's broadcast: every client's own (input) bucket receives
+    # the global while later chunks still upload from those same buckets
+    for i in (1, 2):
+        h32[i].copy_(cl[i][0].cpu())
+        h64[i].copy_(cl[i][1].cpu())
+    pipe.run(h32, h64, o32, o64, h32, h64)
+    assert same(o32, o64) and all(same(a, b) for a, b in zip(h32, h64))
 
 
 # ------------------------------------------------ FedProx proximal term --
