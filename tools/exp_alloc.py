@@ -13,7 +13,7 @@ N = 20), one process, interleaved rounds, bits compared:
 plus this box's read-only rate over the same 20 x B bytes (read probe over
 the arena_256 allocation) and a copy of one bucket's worth x 20.
 
-    python tools/exp_alloc.py [ROUNDS]     |     python tools/exp_alloc.py order
+    python tools/exp_alloc.py [ROUNDS] [one_tensor]  |  python tools/exp_alloc.py order
 """
 import json
 import sys
@@ -86,15 +86,21 @@ def order_mode(rounds):
 def main():
     if "order" in sys.argv[1:]:
         return order_mode(5)
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 7
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    man = load_manifest("wrn16_8_c10")
+    if "one_tensor" in sys.argv[1:]:   # the same bytes as one 5376 x 2048 tensor
+        man = {"name": "t5376", "keys": [{"key": "w", "shape": [5376, 2048],
+                                          "dtype": "float32"}]}
+    else:
+        man = load_manifest("wrn16_8_c10")
     lay = BucketLayout.from_manifest(man)
     nb = lay.algorithmic_bytes(N)
     plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
                      flags=_lib.FA_PLAN_GAPS_ARE_PADDING)
+    os.environ["FA_SLAB"] = "0"        # "sep": one allocation per bucket
     sep = make_clients(lay, man, range(N), dev)
+    os.environ["FA_SLAB"] = "1"
     n32 = sep[0][0].numel()
     b32 = n32 * 4
 
@@ -112,7 +118,8 @@ def main():
     r256 = (b32 + 255) // 256 * 256
     r2m = (b32 + MIB2 - 1) // MIB2 * MIB2
     strides = {"arena_256": r256, "arena_2m": r2m, "arena_2m_4k": r2m + 4096,
-               "arena_2m_odd": r2m + 65536 + 256}
+               "arena_2m_odd": r2m + 65536 + 256, "arena_256_plus_1m": r256 + (1 << 20),
+               "arena_256_plus_24k": r256 + 24576}
     variants = {"sep": Reducer(lay, sep, torch.zeros_like(sep[0][0]),
                                torch.zeros_like(sep[0][1]), plan=plan)}
     keep = {}
