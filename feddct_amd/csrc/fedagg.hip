@@ -779,14 +779,14 @@ bool flat_bcast_ok(unsigned flags, const std::vector<fa_seg>& s32, int64_t f32_n
 // race two summation orders (and two stores) into the same output.
 int check_disjoint(std::vector<Tile> t, const char* who) {
   std::sort(t.begin(), t.end(), [](const Tile& x, const Tile& y) {
-    const bool x64 = x.kind >= K_I64_CASC, y64 = y.kind >= K_I64_CASC;
+    const bool x64 = kind_is64(x.kind), y64 = kind_is64(y.kind);
     return x64 != y64 ? y64 : x.start < y.start;
   });
   for (size_t i = 1; i < t.size(); ++i)
-    if ((t[i - 1].kind >= K_I64_CASC) == (t[i].kind >= K_I64_CASC) &&
+    if (kind_is64(t[i - 1].kind) == kind_is64(t[i].kind) &&
         t[i - 1].start + t[i - 1].count > t[i].start)
       return set_err(FA_E_INVAL, "%s: tiles overlap at %s element %lld", who,
-                     t[i].kind >= K_I64_CASC ? "int64" : "fp32", (long long)t[i].start);
+                     kind_is64(t[i].kind) ? "int64" : "fp32", (long long)t[i].start);
   return FA_OK;
 }
 
@@ -1415,7 +1415,25 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
   std::vector<Tile> t;
   std::vector<float> fac;
   std::vector<int> order_groups_tmp;
+  // Wide S = 1 runs.  With S = 1 every M > 1 tensor has the same per-element
+  // order (row p into accumulator p % 4, then ((a0 + a1) + a2) + a3), so the
+  // 4-aligned bodies of adjacent such tensors with the same factor (bit for
+  // bit) share one run cut into 2048-element tiles across key boundaries, as
+  // the default plan's vector runs are: no partial tile per key (cfg2: 5432
+  // -> ~5381 tiles).  Gaps join a run only when declared padding.
+  const bool wide_ok = !(flags & FA_PLAN_TUNE_TGPU_NARROW);
+  int64_t run_s = -1, run_e = -1;
+  float run_f = 0.f;
+  auto flush = [&]() {
+    if (run_s < 0) return;
+    for (int64_t c = run_s; c < run_e; c += 8 * kBlock) {
+      t.push_back(Tile{c, (int32_t)std::min<int64_t>(8 * kBlock, run_e - c), K_F32_TGPU_W});
+      fac.push_back(run_f);
+    }
+    run_s = run_e = -1;
+  };
   for (int pass = 0; pass < 2; ++pass) {
+    flush();
     for (const fa_seg& g : pass ? s64 : s32) {
       if (g.numel == 0) continue;
       int S = 1;
@@ -1428,6 +1446,7 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
       // torch's factor: float(num_outputs) / numel, in float
       const float f = (float)g.numel / (float)((int64_t)n * g.numel);
       if (g.numel == 1) {
+        flush();
         const int vec = n >= 128 ? 1 << 16 : 0;  // input-vectorised (tgpu_inner_vec)
         t.push_back(Tile{g.offset, 1, (pass ? K_I64_TGPU_IN : K_F32_TGPU_IN) | (ls << 8) | vec});
         fac.push_back(f);
@@ -1448,11 +1467,28 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
       // element head and tail one element per lane (same order, same factor)
       const int64_t head = std::min<int64_t>((4 - g.offset % 4) % 4, g.numel);
       const int64_t body = (g.numel - head) / 4 * 4;
-      scalar(0, head);
       // S = 1: 2048-element tiles, the default reduce's load shape (r02:
       // 151.9 us on cfg2 with the 1024-element form; FA_PLAN_TUNE_TGPU_NARROW
       // keeps that form for A/B)
-      const bool wide = S == 1 && !(flags & FA_PLAN_TUNE_TGPU_NARROW);
+      const bool wide = S == 1 && wide_ok;
+      if (wide && head == 0 && body > 0) {
+        const bool extend = run_s >= 0 && run_f == f &&
+                            (run_e == g.offset ||
+                             ((flags & FA_PLAN_GAPS_ARE_PADDING) && run_e <= g.offset));
+        if (!extend) flush();
+        if (run_s < 0) {
+          run_s = g.offset;
+          run_f = f;
+        }
+        run_e = g.offset + body;
+        if (body < g.numel) {
+          flush();  // the tail breaks the run
+          scalar(body, g.numel);
+        }
+        continue;
+      }
+      flush();
+      scalar(0, head);
       const int64_t te = wide ? 8 * kBlock : 4 * kBlock;
       for (int64_t c = head; c < head + body; c += te) {
         t.push_back(Tile{g.offset + c, (int32_t)std::min<int64_t>(te, head + body - c),
@@ -1462,6 +1498,9 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
       scalar(head + body, g.numel);
     }
   }
+  flush();
+  rc = check_disjoint(t, "torch-GPU order planner");
+  if (rc) return rc;
   // group the tiles by row split (inner tiles with S = 1): one launch each
   {
     std::vector<int> grp(t.size());

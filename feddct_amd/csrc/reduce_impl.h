@@ -256,6 +256,17 @@ __device__ __forceinline__ void promote(Acc<U, DEEP>& A, int ii, int lp, int mas
   }
 }
 
+// Pointer source of a batch's loads.  POL bit 3 (tuning, n <= the inline
+// count only): the kernarg pointer array read directly, which lets the
+// compiler issue the whole batch's loads back to back instead of one
+// client's loads behind a vmcnt(0) wait (slower at N = 20, r01; swept for
+// small N, r02).
+template <bool TAB, int POL>
+__device__ __forceinline__ const float* bptr(KArgs& a, int i) {
+  if constexpr ((POL & 8) != 0) return a.c32[i];
+  else return vptr32<TAB>(a, i);
+}
+
 // One batch of NB clients starting at b0.  FULL: every lane's U vectors are
 // inside the tile (no per-lane predicate).
 template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool TAB>
@@ -284,17 +295,6 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t
     }
     promote<U, DEEP>(A, r0 + b0 + b + 1, lp, mask);
   }
-}
-
-// Pointer source of a batch's loads.  POL bit 3 (tuning, n <= the inline
-// count only): the kernarg pointer array read directly, which lets the
-// compiler issue the whole batch's loads back to back instead of one
-// client's loads behind a vmcnt(0) wait (slower at N = 20, r01; swept for
-// small N, r02).
-template <bool TAB, int POL>
-__device__ __forceinline__ const float* bptr(KArgs& a, int i) {
-  if constexpr ((POL & 8) != 0) return a.c32[i];
-  else return vptr32<TAB>(a, i);
 }
 
 // The last, partial batch (nb < NB clients): same issue-all-then-add shape,

@@ -165,6 +165,39 @@ def test_kernel_matches_torch_gpu_mean(lib, case):
     assert _vs_torch(layout, cl, out32, out64) == []
 
 
+# (offset, numel) fp32 segments: 4-aligned keys back to back (one wide run
+# across them), a 4-aligned key behind a gap, unaligned heads and ragged
+# tails (each breaks the run), 0-dim keys, and a 2**24 + 12 key whose factor
+# float(M) / float(N M) is not 1/N's (N = 5, 20): the run must break there.
+RUN_SEGS = [(0, 128), (128, 256), (384, 2048 * 3), (6528, 100), (6628, 4100), (10800, 1),
+            (10804, 2052), (12858, 1000), (14000, 2 ** 24 + 12), (14000 + 2 ** 24 + 12, 512)]
+
+
+@pytest.mark.parametrize("flags", [0, 1])   # 1 = FA_PLAN_GAPS_ARE_PADDING
+@pytest.mark.parametrize("n", [5, 20])
+def test_wide_runs_across_keys(lib, flags, n):
+    """S = 1 keys share 2048-element wide runs across key boundaries (r03):
+    bit-exact vs torch's cuda mean per key; without the padding flag no gap
+    element is written, and the factor break keeps each key's own factor."""
+    segs = np.array(RUN_SEGS, np.int64)
+    numel = int(segs[-1, 0] + segs[-1, 1] + 60)
+    g = torch.Generator(device="cpu").manual_seed(n)
+    cl = [torch.randn(numel, generator=g).mul_(1.0 + i).to(DEV) for i in range(n)]
+    plan = lib.Plan(segs, numel, order=lib.FA_ORDER_TORCH_GPU, n=n, flags=flags)
+    out32 = torch.full((numel,), float("nan"), device=DEV)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    lib.check(lib.lib.fa_reduce(plan.handle, lib.ptr_array([c.data_ptr() for c in cl]), None,
+                                n, None, out32.data_ptr(), 0, 0, s), "fa_reduce(gpu order)")
+    torch.cuda.synchronize()
+    covered = torch.zeros(numel, dtype=torch.bool, device=DEV)
+    for off, m in RUN_SEGS:
+        ref = _torch_gpu_mean([c[off:off + m] for c in cl])
+        assert bits_equal(out32[off:off + m].cpu().numpy(), ref.cpu().numpy()), (off, m)
+        covered[off:off + m] = True
+    if not flags:
+        assert torch.isnan(out32[~covered]).all()
+
+
 def test_gpu_order_broadcast_and_errors(lib):
     man = load_manifest("wrnsl16_8_sf4_c10_main")
     layout = BucketLayout.from_manifest(man)
