@@ -888,8 +888,9 @@ int pick_batch(int n, int vec_u, unsigned pflags) {
 // clients whose plain table (a) part-fills ONE round of the 16-client kernel
 // runs a table re-cut to fill it, (b) needs two rounds of the 16-client
 // kernel but one of the 8-client kernel runs the 8-client kernel (resnet110sl
-// sf4 N = 25, 923 tiles: 23.0 vs 26.3 us plain, 23.9 re-cut), and (c) runs
-// the plain table otherwise.  N < 16 (8-client kernel already) always runs
+// sf4 N = 25, 923 tiles: 23.0 vs 26.3 us plain, 23.9 re-cut), (c) spills a
+// few tiles past its last full round: the tail split below (split_tail), and
+// (d) runs the plain table otherwise.  N < 16 (8-client kernel already) always runs
 // plain: at N = 5 a re-cut is no gain (384 tiles 7.8 vs 9.0 us).
 constexpr double kKeepFill = 0.97;  // the round at least this full: keep the plain table
 constexpr int64_t kMinTile = 256;   // never cut vector tiles below this (elements)
@@ -947,6 +948,44 @@ int round_batch(int dev, int n, int vec_u, bool w, unsigned pflags, int ntiles) 
   return (s16 > 0 && s8 > s16 && ntiles > s16 && ntiles <= s8) ? 8 : 16;
 }
 
+// A multi-round launch whose last round holds only r << slots tiles (r03
+// session 4, tools/exp_round_quant.py, profiles/r03_exp_round_quant.jsonl):
+// those r tiles run alone, latency-bound, ~7-8 us after the last full round
+// at N = 20 — cfg2's layout plus 16 / 18 / 25 extra 2048-float tiles (r = 1
+// / 3 / 10 past 7 rounds of 768) reads 139.0 / 142.3 / 143.9 us against
+// 136.3 us at 6.99 rounds, while 300 extra tiles cost only 146.4 us.  So the
+// LAST slots - r vector tiles are split in halves (64-element lines): the
+// table then fills exactly k rounds, its last round made of half tiles, and
+// every earlier tile keeps the full width (re-cutting the whole table
+// instead was slower, see above).  Same process, weighted, split vs plain
+// (profiles/r03_exp_round_quant_tail_split*.jsonl): r = 10 137.9 vs 143.8
+// us, r = 85 139.5 vs 144.0, r = 135 141.5 vs 144.8, r = 285 144.8 vs 146.3,
+// r = 335 145.4 vs 147.6 — a gain at every r up to 0.44 slots, so it is
+// applied for 0 < r <= slots / kTailDiv.
+constexpr int64_t kTailDiv = 2;
+std::vector<Tile> split_tail(const std::vector<Tile>& tiles, int64_t r, int slots) {
+  if (r <= 0 || r * kTailDiv > slots) return {};
+  std::vector<Tile> vec;
+  for (const Tile& x : tiles)
+    if (x.kind == K_F32_VEC) vec.push_back(x);
+  const int64_t m = slots - r;  // tiles to split
+  if ((int64_t)vec.size() < m) return {};
+  std::vector<Tile> out;
+  out.reserve(vec.size() + (size_t)m);
+  const size_t first = vec.size() - (size_t)m;
+  for (size_t i = 0; i < vec.size(); ++i) {
+    const Tile& x = vec[i];
+    const int64_t h = ((int64_t)x.count / 2) & ~(int64_t)63;
+    if (i < first || h < kMinTile / 2) {
+      out.push_back(x);
+      continue;
+    }
+    out.push_back(Tile{x.start, (int32_t)h, K_F32_VEC});
+    out.push_back(Tile{x.start + h, (int32_t)(x.count - h), K_F32_VEC});
+  }
+  return out;
+}
+
 // The vector tiles of `tiles` (cut at cmax elements), re-cut for `slots`:
 // only when they part-fill a single round (k = 1: slots - nscalar vector tiles),
 // handed out run by run (a run = adjacent vector tiles) to the run whose
@@ -964,7 +1003,8 @@ std::vector<Tile> balance_vec(const std::vector<Tile>& tiles, int cmax, int nsca
   if (t0 == 0 || slots <= 0) return {};
   const int64_t have = t0 + nscalar;
   const int64_t k = (have + slots - 1) / slots;
-  if (k > 1 || (double)have >= kKeepFill * (double)(k * slots)) return {};
+  if (k > 1) return split_tail(tiles, have - (k - 1) * slots, slots);
+  if ((double)have >= kKeepFill * (double)(k * slots)) return {};
   const int64_t target = k * slots - nscalar;
   std::vector<int64_t> m(runs.size());
   std::priority_queue<std::pair<double, size_t>> pq;  // (tile size, run), largest first

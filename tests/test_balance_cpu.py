@@ -4,7 +4,10 @@ them is the same per-column order), stay within the kernel's tile width, sit
 on 64-element lines, and with the packed scalar tiles fill the one round of
 the slot count they part-fill — or the plain cut is kept when that round is
 >= 97 % full or the launch needs more than one round (measured: re-cutting a
-multi-round launch is slower, fedagg.hip balance_vec).  No GPU."""
+multi-round launch is slower, fedagg.hip balance_vec), except that a
+multi-round launch spilling r <= slots / 2 tiles past its last full round
+has its last slots - r tiles split in halves (split_tail, r03 session 4).
+No GPU."""
 import numpy as np
 import pytest
 
@@ -55,10 +58,28 @@ def test_one_run_fills_whole_rounds(t, slots):
 
 
 @pytest.mark.parametrize("t,ns,slots", [(768, 0, 768), (5358, 2, 768), (3070, 0, 1024),
-                                        (750, 5, 768), (1024, 0, 768), (1280, 0, 768),
-                                        (2560, 0, 768), (5380, 0, 768), (4096, 0, 1280)])
+                                        (750, 5, 768), (1280, 0, 768),
+                                        (5120 + 700, 0, 1280), (5376 + 385, 0, 768),
+                                        (5376, 0, 768)])
 def test_full_or_multi_round_keeps_plain_cut(t, ns, slots):
     assert _lib.balance_host(_vec_tiles([(0, t * 2048)]), 2048, ns, slots) is None
+
+
+@pytest.mark.parametrize("t,ns,slots", [(5377, 0, 768), (5380, 0, 768), (5376 + 384, 0, 768),
+                                        (5370, 10, 768), (2 * 1280 + 7, 3, 1280), (2560, 0, 768), (1024, 0, 768),
+                                        (4096, 0, 1280)])
+def test_multi_round_tail_split(t, ns, slots):
+    """A few tiles past the last full round: the last slots - r tiles are
+    split in halves, every earlier tile untouched, exactly k rounds."""
+    plain = _vec_tiles([(0, t * 2048)])
+    cut = _lib.balance_host(plain, 2048, ns, slots)
+    _check(plain, cut, 2048, ns, slots)
+    k = -(-(t + ns) // slots)
+    r = t + ns - (k - 1) * slots
+    assert len(cut) == k * slots - ns
+    keep = t - (slots - r)
+    assert np.array_equal(cut[:keep], plain[:keep])
+    assert (cut[keep:, 1] == 1024).all()
 
 
 def test_runs_with_gaps_and_ragged_ends():
@@ -96,7 +117,8 @@ def test_reference_layouts(name, slots):
     cut = _lib.balance_host(vec, 2048, ns, slots)
     if cut is None:
         k = -(-(len(vec) + ns) // slots)
-        assert k > 1 or len(vec) + ns >= 0.97 * k * slots
+        r = len(vec) + ns - (k - 1) * slots
+        assert (k > 1 and 2 * r > slots) or (k == 1 and len(vec) + ns >= 0.97 * k * slots)
     else:
         _check(vec, cut, 2048, ns, slots)
 
