@@ -701,6 +701,7 @@ struct fa_plan {
   // their packed tiles are the main table's (same scalar index region)
   struct BalTable {
     int u = 0, slots = 0;
+    int batch = 16;  // clients per load batch of the kernel it was cut for
     Tile* d = nullptr;
     int nt = 0;
     bool alt = false;  // cut from the alt (1024-float) table: its scalar index region
@@ -991,7 +992,8 @@ std::vector<Tile> split_tail(const std::vector<Tile>& tiles, int64_t r, int slot
 // handed out run by run (a run = adjacent vector tiles) to the run whose
 // tiles are largest, boundaries on 64-element (256 B) lines, no tile above
 // cmax or (when split further) below kMinTile.  Empty: keep the plain table.
-std::vector<Tile> balance_vec(const std::vector<Tile>& tiles, int cmax, int nscalar, int slots) {
+std::vector<Tile> balance_vec(const std::vector<Tile>& tiles, int cmax, int nscalar, int slots,
+                              bool tail_only = false) {
   std::vector<std::pair<int64_t, int64_t>> runs;  // [start, end)
   int64_t t0 = 0;
   for (const Tile& x : tiles) {
@@ -1004,7 +1006,7 @@ std::vector<Tile> balance_vec(const std::vector<Tile>& tiles, int cmax, int nsca
   const int64_t have = t0 + nscalar;
   const int64_t k = (have + slots - 1) / slots;
   if (k > 1) return split_tail(tiles, have - (k - 1) * slots, slots);
-  if ((double)have >= kKeepFill * (double)(k * slots)) return {};
+  if (tail_only || (double)have >= kKeepFill * (double)(k * slots)) return {};
   const int64_t target = k * slots - nscalar;
   std::vector<int64_t> m(runs.size());
   std::priority_queue<std::pair<double, size_t>> pq;  // (tile size, run), largest first
@@ -1288,38 +1290,46 @@ hipError_t upload_tables(fa_plan* p, const std::vector<Tile>& tiles,
                                       (0xFu << 8) | (0xFu << 12))))
     return e;
   struct Req {
-    int u, slots;
+    int u, slots, batch;
     const std::vector<Tile>* host;
     const std::vector<Tile>* dev;
     int ns;
   };
   std::vector<Req> reqs;
-  auto want = [&](int u, int slots, const std::vector<Tile>* host, const std::vector<Tile>* dev,
-                  int ns) {
+  auto want = [&](int u, int slots, int batch, const std::vector<Tile>* host,
+                  const std::vector<Tile>* dev, int ns) {
     if (slots <= 0) return;
     for (const Req& q : reqs)
-      if (q.u == u && q.slots == slots && q.dev == dev) return;
-    reqs.push_back(Req{u, slots, host, dev, ns});
+      if (q.u == u && q.slots == slots && q.batch == batch && q.dev == dev) return;
+    reqs.push_back(Req{u, slots, batch, host, dev, ns});
   };
-  // (only the 16-client kernels' calls are re-cut: N < 16 runs plain)
+  // the 16-client kernels' calls: the whole rule; the calls of N < 16 (the
+  // 8-client kernels): the tail split only (tools/exp_tail_small_n.py: N = 5
+  // / 8 / 12, 1.1-2.9 us per launch; a one-round re-cut is no gain there)
   for (int deep = 0; deep < 2; ++deep)
-    for (int w = 0; w < 2; ++w)
+    for (int w = 0; w < 2; ++w) {
       if (pick_batch(16, p->vec_u, p->flags) == 16)
-        want(p->vec_u, kernel_slots(p->device, p->vec_u, 16, deep != 0, w != 0), &tiles, &dm,
+        want(p->vec_u, kernel_slots(p->device, p->vec_u, 16, deep != 0, w != 0), 16, &tiles,
+             &dm, p->ns_dev);
+      const int b8 = pick_batch(8, p->vec_u, p->flags);
+      if (deep == 0)
+        want(p->vec_u, kernel_slots(p->device, p->vec_u, b8, false, w != 0), b8, &tiles, &dm,
              p->ns_dev);
+    }
   if (!da.empty())
     for (int deep = 0; deep < 2; ++deep)
-      want(1, kernel_slots(p->device, 1, pick_batch(64, 1, p->flags), deep != 0, false), &alt,
-           &da, p->ns_alt_dev);
+      want(1, kernel_slots(p->device, 1, pick_batch(64, 1, p->flags), deep != 0, false),
+           pick_batch(64, 1, p->flags), &alt, &da, p->ns_alt_dev);
   for (const Req& q : reqs) {
     const std::vector<Tile> v =
-        balance_vec(*q.host, q.u * 4 * kBlock, q.ns, q.slots);
+        balance_vec(*q.host, q.u * 4 * kBlock, q.ns, q.slots, q.batch < 16);
     if (v.empty()) continue;
     std::vector<Tile> t(q.dev->begin(), q.dev->begin() + q.ns);  // the packed tiles lead
     t.insert(t.end(), v.begin(), v.end());
     fa_plan::BalTable b;
     b.u = q.u;
     b.slots = q.slots;
+    b.batch = q.batch;
     b.nt = (int)t.size();
     b.alt = q.dev == &da;
     e = hipMalloc(&b.d, t.size() * sizeof(Tile));
@@ -1777,7 +1787,7 @@ Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) 
   } else if (!plan->bal.empty()) {
     // the table cut for the slot count of the kernel this call runs
     for (const fa_plan::BalTable& b : plan->bal)
-      if (b.slots == L.slots && b.u == L.vec_u && b.alt == alt) {
+      if (b.slots == L.slots && b.u == L.vec_u && b.alt == alt && b.batch == L.batch) {
         L.tiles = b.d;
         L.nt = b.nt;
         break;

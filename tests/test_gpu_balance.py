@@ -3,7 +3,8 @@ plain tile table part-fills one round of the 16-client kernel's resident
 workgroups runs a table re-cut to fill it; one that needs two rounds of the
 16-client kernel but one of the 8-client kernel runs the 8-client kernel;
 one that spills r <= slots / 2 tiles past its last full round has its last
-slots - r tiles split in halves (session 4, split_tail); everything else
+slots - r tiles split in halves (session 4, split_tail; at N < 16 too, on
+the 8-client kernels' slots); everything else
 runs the plain table (fedagg.hip balance_vec / round_batch).
 Each call here runs once through the plan's choice and once through the
 plain table with the default batch (FA_PLAN_TUNE_NO_BALANCE): the results
@@ -61,7 +62,8 @@ CASES = [("one_tensor_1024", 20, False), ("one_tensor_1280", 16, False),
          ("one_tensor_384", 20, False), ("one_tensor_384", 20, True), ("one_tensor_600", 5, False),
          ("one_tensor_3000", 17, False), ("one_tensor_5380", 20, False),
          ("one_tensor_5380", 20, True), ("one_tensor_1700", 20, False),
-         ("one_tensor_1700", 300, False),
+         ("one_tensor_1700", 300, False), ("one_tensor_5380", 5, False),
+         ("one_tensor_5380", 12, True), ("one_tensor_5760", 5, False),
          ("wrn16_8_c100", 20, False), ("wrn16_8_c100", 20, True), ("wrn16_8_c10", 20, False),
          ("wrnsl16_8_sf4_c10_joint", 5, False), ("resnet110sl_sf4_c100_joint", 25, False),
          ("wrnsl16_8_sf32_c100_joint", 3, False), ("wrnsl16_8_sf2_c100_joint", 48, True)]
@@ -92,7 +94,7 @@ def test_balanced_table_same_bits(lib, name, n, weighted):
     s8 = pp.launch_shape(5, weighted)[1] if n >= 16 else slots_p
     k = -(-nt_p // slots_p)
     r = nt_p - (k - 1) * slots_p
-    if n >= 16 and nt_p > s8 and 2 * r <= slots_p:
+    if k > 1 and 2 * r <= slots_p and (n < 16 or nt_p > s8):
         assert (nt_b, slots) == (k * slots_p, slots_p)   # tail split: exactly k rounds
     elif n < 16 or nt_p > s8 or (nt_p <= slots_p and nt_p >= 0.97 * slots_p):
         assert (nt_b, slots) == (nt_p, slots_p)    # plain table, default batch
