@@ -812,7 +812,7 @@ def next_rows(dev, steps=30):
     # set_to_none default); the global model's accumulate step after step
     def ours():
         client.zero_grad(set_to_none=True)
-        proximal_term(client, glob).backward()
+        proximal_term(client, glob, flat_grads=True).backward()
 
     def reference():
         client.zero_grad(set_to_none=True)
@@ -823,7 +823,7 @@ def next_rows(dev, steps=30):
 
     ours()
     want = sum((w - w_t).norm(2) for w, w_t in zip(client.parameters(), glob.parameters()))
-    got = proximal_term(client, glob)
+    got = proximal_term(client, glob, flat_grads=True)
     t_ours, _ = timed_launches(ours, steps, 3)
     t_ref, _ = timed_launches(reference, steps, 3)
     # kernel-only: the three launches over the bound arenas

@@ -64,7 +64,7 @@ def run(rounds=3, clients=4, steps=5, mu=0.0, check=None, seed=0, device="cuda")
                 opt.zero_grad()
                 loss = F.cross_entropy(m(x), y)
                 if mu > 0:  # train_fedprox.py:113-116
-                    loss = loss + (mu / 2) * proximal_term(m, global_model)
+                    loss = loss + (mu / 2) * proximal_term(m, global_model, flat_grads=True)
                 loss.backward()
                 opt.step()
         torch.cuda.synchronize()

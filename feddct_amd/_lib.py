@@ -53,6 +53,9 @@ FA_PLAN_TUNE_BCAST_TABLE = 0x800000
 FA_PLAN_TUNE_BCAST_REVERSE = 0x1000000
 FA_PLAN_TUNE_BCAST_XCD = 0x2000000
 FA_PLAN_TUNE_NO_BALANCE = 0x10000000
+FA_PLAN_TUNE_BCAST_R03 = 0x20000000
+FA_PLAN_TUNE_BCAST_U2 = 0x40000000
+FA_PLAN_TUNE_BCAST_G24 = 0x80000000
 FA_ORDER_TORCH_CPU = 0
 FA_ORDER_TORCH_GPU = 1
 
@@ -77,7 +80,7 @@ EXPORTS = [
     "fa_synth_fill_f32", "fa_synth_fill_i64", "fa_copy_f32",
     "fa_norm_plan_create", "fa_norm_plan_destroy", "fa_prox_norms", "fa_prox_grad",
     "fa_prox_grad_ex",
-    "fa_read_probe_f32", "fa_chain_levels", "fa_reduce_chain", "fa_torch_gpu_config",
+    "fa_read_probe_f32", "fa_write_probe_f32", "fa_tune_bcast_store", "fa_chain_levels", "fa_reduce_chain", "fa_torch_gpu_config",
     "fa_plan_create_order", "fa_table_bytes", "fa_reduce_tab",
     "fa_plan_balance_host", "fa_plan_launch_shape",
 ]
@@ -144,6 +147,8 @@ def _load():
         "fa_synth_fill_i64": (_I, [_P, _I64, _I, _I, _I, _P]),
         "fa_copy_f32": (_I, [_P, _P, _I64, _P]),
         "fa_read_probe_f32": (_I, [_P, _I64, _P, _I, _P]),
+        "fa_write_probe_f32": (_I, [_P, _I, _I64, ctypes.c_uint, _P]),
+        "fa_tune_bcast_store": (_I, [_I]),
         "fa_chain_levels": (ctypes.c_uint, [_I, _I]),
         "fa_torch_gpu_config": (_I, [_I, _I64, ctypes.POINTER(_I)]),
         "fa_plan_create_order": (_I, [_P, _I, _I64, _P, _I, _I64, _I, _I, ctypes.c_uint,

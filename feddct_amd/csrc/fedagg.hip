@@ -56,6 +56,7 @@ FA_K_UNITS(extern)
 namespace fa_k {
 thread_local size_t t_dyn_lds = 0;  // tuning: occupancy cap through dynamic LDS
 thread_local int t_grid_cap = 0;     // tuning: persistent grid size
+thread_local int t_bcast_store = 0;  // tuning: the r04 flat broadcast's store policy
 }  // namespace fa_k
 
 namespace {
@@ -254,6 +255,161 @@ __global__ __launch_bounds__(kBlock) void bcast_flat_kernel(ReduceArgs args, uin
         const int64_t r = a.out64[e];
         for (int c = c0; c < c1; ++c) const_cast<int64_t*>(cptr64(a, c))[e] = r;
       }
+    }
+  }
+}
+
+// r04: the round's broadcast with every client pointer a scalar load
+// (sptr32) and a group's G stores back to back.  The two kernels above fetch
+// each destination through cptr32, which the compiler serves with an
+// `s_waitcnt vmcnt(0)` before every client's stores — a wave's previous
+// client's stores had to complete first (ISA checked; vmcnt counts stores on
+// CDNA).  Measured on one box (tools/writelab.hip, 20 x 43.9 MB destinations
+// in one slab, hashed data, profiles/r04_writelab.jsonl): a lab kernel of
+// this shape 127.4 us at U = 1 with all 20 clients in one workgroup (one
+// source fetch: 7.23 TB/s of B read + N*B written; a pure write of the same
+// N*B 124 us = 7.08 TB/s), 134.3 us at U = 2 in groups of 10, against
+// 156.2 us for the r03 product kernel of the U = 2, groups-of-10 shape.
+// One workgroup per (part of U*1024 floats, group of <= G clients); G is the
+// template bound, the host's group size `gsize` <= G.  The int64 bucket is
+// one more part.
+// Store policy of the broadcast's destination stores (tuning,
+// fa_tune_bcast_store): 0 global nt (default), 1 sc1, 2 sc1 nt, 3 sc0 sc1
+// (buffer stores with those cache-policy bits: sc1 writes through and drops
+// the line from the XCD's L2, so the launch ends with no dirty lines to write
+// back), 4 plain.
+template <int SP>
+__device__ __forceinline__ void st_bc(float* base, uint32_t vidx, f4 v) {
+  if constexpr (SP == 0) {
+    stg4<true>(base, vidx, v);
+  } else if constexpr (SP == 4) {
+    stg4<false>(base, vidx, v);
+  } else {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(16 * vidx), 0,
+                                           SP == 1 ? 16 : SP == 2 ? 18 : 17);
+  }
+}
+template <int U, int G, int SP = 0>
+__global__ __launch_bounds__(kBlock) void bcast_flat2_kernel(ReduceArgs args, uint32_t parts,
+                                                             uint32_t groups, uint32_t gsize,
+                                                             int64_t f32_numel,
+                                                             int64_t i64_numel, int xcd) {
+  (void)args;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const uint32_t nparts = parts + (i64_numel > 0 ? 1u : 0u);
+  uint32_t p, g;
+  if (!bcast_part(blockIdx.x, nparts, groups, xcd, &p, &g)) return;
+  const int c0 = (int)(g * gsize);
+  const int cnt = min(a.n - c0, (int)gsize);
+  if (p < parts) {
+    const int64_t nv = f32_numel / 4;
+    const int64_t vb = (int64_t)p * U * kBlock;  // the part's first float4
+    const float* src = a.out32 + 4 * vb;
+    f4 r[U];
+    if (vb + U * kBlock <= nv) {
+      // a whole part (all but possibly the last): no per-lane predicate, and
+      // client 0's stores unconditional (cnt >= 1), so the source loads are
+      // waited for once there and no later store carries a vmcnt wait (the
+      // waitcnt pass merges pending loads across a skipped branch)
+#pragma unroll
+      for (int u = 0; u < U; ++u) r[u] = ldg4<false>(src, threadIdx.x + u * kBlock);
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        if (i == 0 || i < cnt) {
+          float* d = sptr32(a, c0 + i) + 4 * vb;
+#pragma unroll
+          for (int u = 0; u < U; ++u) st_bc<SP>(d, threadIdx.x + u * kBlock, r[u]);
+        }
+      }
+    } else {
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ok[u] = vb + threadIdx.x + u * kBlock < nv;
+        if (ok[u]) r[u] = ldg4<false>(src, threadIdx.x + u * kBlock);
+      }
+      for (int i = 0; i < cnt; ++i) {
+        float* d = sptr32(a, c0 + i) + 4 * vb;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (ok[u]) stg4<true>(d, threadIdx.x + u * kBlock, r[u]);
+      }
+    }
+    // the last part also copies the f32_numel % 4 trailing floats
+    if (p == parts - 1 && (int64_t)threadIdx.x < f32_numel - 4 * nv) {
+      const float x = a.out32[4 * nv + threadIdx.x];
+      for (int i = 0; i < cnt; ++i) sptr32(a, c0 + i)[4 * nv + threadIdx.x] = x;
+    }
+  } else {
+    for (int64_t e = threadIdx.x; e < i64_numel; e += kBlock) {
+      const int64_t x = a.out64[e];
+      for (int i = 0; i < cnt; ++i) sptr64(a, c0 + i)[e] = x;
+    }
+  }
+}
+
+// The same over the plan's tile table (plans whose segments do not cover
+// the bucket, and torch-GPU-order rounds): one workgroup per (tile, group of
+// <= G clients); a vector tile's U <= 4 float4 per lane load before the
+// group's stores.
+template <int G>
+__global__ __launch_bounds__(kBlock) void bcast_group2_kernel(ReduceArgs args, uint32_t groups,
+                                                              uint32_t gsize, int xcd) {
+  (void)args;
+  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  uint32_t ti, g;
+  if (!bcast_part(blockIdx.x, (uint32_t)a.ntiles, groups, xcd, &ti, &g)) return;
+  const int c0 = (int)(g * gsize);
+  const int cnt = min(a.n - c0, (int)gsize);
+  const Tile t = a.tiles[ti];
+  const int kb = t.kind & 0xFF;
+  if (kb == K_F32_VEC || kb == K_F32_TGPU_V || kb == K_F32_TGPU_W) {
+    const uint32_t nv = (uint32_t)t.count / 4;
+    f4 r[4];
+    if (nv == 2 * kBlock) {
+      // a full 2048-float tile (the default width): unpredicated, client 0's
+      // stores unconditional (see bcast_flat2_kernel)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) r[u] = ldg4<false>(a.out32 + t.start, threadIdx.x + u * kBlock);
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        if (i == 0 || i < cnt) {
+          float* d = sptr32(a, c0 + i) + t.start;
+#pragma unroll
+          for (int u = 0; u < 2; ++u) stg4<true>(d, threadIdx.x + u * kBlock, r[u]);
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t vi = threadIdx.x + u * kBlock;
+      if (vi < nv) r[u] = ldg4<false>(a.out32 + t.start, vi);
+    }
+    for (int i = 0; i < cnt; ++i) {
+      float* d = sptr32(a, c0 + i) + t.start;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t vi = threadIdx.x + u * kBlock;
+        if (vi < nv) stg4<true>(d, vi, r[u]);
+      }
+    }
+  } else if ((int)threadIdx.x < t.count) {
+    int64_t e = t.start + threadIdx.x;
+    bool is64 = kind_is64(t.kind);
+    if (kb == K_SCALAR_PACKED) {  // a packed column: its element and kind
+      const int64_t ent = a.sidx[e];
+      e = ent >> 4;
+      is64 = kind_is64((int)(ent & 15));
+    }
+    if (!is64) {
+      const float x = a.out32[e];
+      for (int i = 0; i < cnt; ++i) sptr32(a, c0 + i)[e] = x;
+    } else {
+      const int64_t x = a.out64[e];
+      for (int i = 0; i < cnt; ++i) sptr64(a, c0 + i)[e] = x;
     }
   }
 }
@@ -609,6 +765,35 @@ __global__ __launch_bounds__(kBlock) void read_probe_kernel(const float* __restr
   float s = acc.x + acc.y + acc.z + acc.w;
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if ((threadIdx.x & 63) == 0) atomicAdd(out + blockIdx.x, s);
+}
+
+// Write-only probe in the round broadcast's own shape (fa_write_probe_f32,
+// r04): one workgroup per (1024-float part, group of <= gsize
+// destinations), one 16-B non-temporal store per lane per destination, the
+// values non-zero and non-repeating (an integer hash of the element index
+// and `seed`, computed in registers: nothing is read).  Zero-filled or
+// constant stores are no write ceiling on this chip.
+__device__ __forceinline__ float probe_val(uint32_t i) {
+  i ^= i >> 16;
+  i *= 0x7feb352du;
+  i ^= i >> 15;
+  i *= 0x846ca68bu;
+  i ^= i >> 16;
+  return __fmul_rn((float)(int32_t)((i >> 8) | 1u) - 8388608.0f, 1.0f / 8388608.0f);
+}
+__global__ __launch_bounds__(kBlock) void write_probe_kernel(BcastArgs a, int64_t numel,
+                                                             uint32_t parts, uint32_t groups,
+                                                             uint32_t gsize, uint32_t seed) {
+  uint32_t p, g;
+  if (!bcast_part(blockIdx.x, parts, groups, false, &p, &g)) return;
+  const int c0 = (int)(g * gsize);
+  const int c1 = min(a.n, c0 + (int)gsize);
+  const int64_t nv = numel / 4;
+  const int64_t v = (int64_t)p * kBlock + threadIdx.x;
+  if (v >= nv) return;
+  const uint32_t b = (uint32_t)(4 * v) ^ seed;
+  const f4 x = {probe_val(b), probe_val(b + 1), probe_val(b + 2), probe_val(b + 3)};
+  for (int c = c0; c < c1; ++c) st4<true>(a.dst[c] + 4 * v, x);
 }
 
 // Read-only probe in the reduce's own shape (grid = 0 in fa_read_probe_f32):
@@ -1718,10 +1903,63 @@ namespace {
 // groups per tile through the tile table otherwise (or with
 // FA_PLAN_TUNE_BCAST_TABLE); r01's one-workgroup-per-tile form with
 // FA_PLAN_TUNE_BCAST_TILES (CPU-order tables only: tiles_ok).
+// r04 default: bcast_flat2_kernel / bcast_group2_kernel (scalar pointer
+// loads), client groups of <= kBcastGroupMax = 10 (FA_PLAN_TUNE_BCAST_G24:
+// <= 24, one source fetch for N <= 24), U = 1 float4 per lane per part
+// (FA_PLAN_TUNE_BCAST_U2: 2); the r02/r03 kernels with
+// FA_PLAN_TUNE_BCAST_R03.  Groups of <= 10 against <= 24 inside the cfg2
+// round, same process, seven client placements (tools/exp_round2.py,
+// tools/exp_contig.py; profiles/r04_exp_round2*.jsonl, r04_exp_contig.jsonl):
+// 283.6-308.6 vs 289.2-318.9 us, every time faster, although the <= 24 form
+// is the faster one alone (146-148 us; the r03 kernels 156 us) and fetches
+// the source once; the r03 kernels 287.6-310.5 us.
+constexpr int kBcastGroupMax = 10;
+extern "C++" template <int G>
+void launch_bcast2(const fa_plan* plan, ReduceArgs& a, int ntiles, uint32_t groups,
+                   uint32_t gsize, int xcd, hipStream_t st) {
+  if (plan->flat_bcast && !(plan->flags & FA_PLAN_TUNE_BCAST_TABLE)) {
+    const int64_t f = plan->has32 ? plan->info.f32_numel : 0;
+    const int64_t i = plan->has64 ? plan->info.i64_numel : 0;
+    const int U = (plan->flags & FA_PLAN_TUNE_BCAST_U2) ? 2 : 1;
+    const int64_t parts = f > 0 ? std::max<int64_t>(1, (f / 4 + U * kBlock - 1) / (U * kBlock)) : 0;
+    const int64_t np = parts + (i > 0 ? 1 : 0);
+    if (np == 0) return;
+    const unsigned grid = bcast_blocks((uint32_t)np, groups, xcd);
+#define FA_BC2(U_, SP_)                                                                   \
+  hipLaunchKernelGGL((bcast_flat2_kernel<U_, G, SP_>), dim3(grid), dim3(kBlock), 0, st, a, \
+                     (uint32_t)parts, groups, gsize, f, i, xcd)
+    if (U == 2) FA_BC2(2, 0);
+    else if (t_bcast_store == 1) FA_BC2(1, 1);
+    else if (t_bcast_store == 2) FA_BC2(1, 2);
+    else if (t_bcast_store == 3) FA_BC2(1, 3);
+    else if (t_bcast_store == 4) FA_BC2(1, 4);
+    else FA_BC2(1, 0);
+#undef FA_BC2
+  } else if (ntiles > 0) {
+    const unsigned grid = bcast_blocks((uint32_t)ntiles, groups, xcd);
+    hipLaunchKernelGGL((bcast_group2_kernel<G>), dim3(grid), dim3(kBlock), 0, st, a, groups,
+                       gsize, xcd);
+  }
+}
+
 hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, bool tiles_ok,
                         hipStream_t st) {
   a.flags |= FA_F_BCAST;
   if (n <= 0) return hipSuccess;
+  if (!(plan->flags & FA_PLAN_TUNE_BCAST_R03) && !(tiles_ok && (plan->flags & FA_PLAN_TUNE_BCAST_TILES))) {
+    const int gmax = (plan->flags & FA_PLAN_TUNE_BCAST_G24) ? 24 : kBcastGroupMax;
+    const uint32_t groups = (uint32_t)((n + gmax - 1) / gmax);
+    const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
+    const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_XCD) ? 1 : 0;
+    // grids stay below 2^32 blocks: n clients of >= 4 KB parts would outgrow
+    // any GPU's memory long before
+    const int64_t units = plan->flat_bcast ? (plan->info.f32_numel / 1024 + 2) : ntiles;
+    if ((units + 8) * (int64_t)groups > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
+    if (gsize <= 8) launch_bcast2<8>(plan, a, ntiles, groups, gsize, xcd, st);
+    else if (gsize <= 16) launch_bcast2<16>(plan, a, ntiles, groups, gsize, xcd, st);
+    else launch_bcast2<24>(plan, a, ntiles, groups, gsize, xcd, st);
+    return hipGetLastError();
+  }
   const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
   const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
   if (tiles_ok && (plan->flags & FA_PLAN_TUNE_BCAST_TILES)) {
@@ -2161,6 +2399,37 @@ int fa_broadcast_f32(const float* src, float* const* dst, int n, int64_t numel, 
                        (uint32_t)parts, groups, gsize);
     HIP_TRY(hipGetLastError());
   }
+  return FA_OK;
+}
+
+int fa_tune_bcast_store(int policy) {
+  if (policy < 0 || policy > 4) return set_err(FA_E_INVAL, "fa_tune_bcast_store: %d", policy);
+  const int old = t_bcast_store;
+  t_bcast_store = policy;
+  return old;
+}
+
+int fa_write_probe_f32(float* const* dst, int n, int64_t numel, unsigned seed, void* stream) {
+  if (n < 0 || n > kBcastInline) return set_err(FA_E_RANGE, "fa_write_probe_f32: n=%d", n);
+  if (numel < 0 || (numel > 0 && n > 0 && !dst))
+    return set_err(FA_E_INVAL, "fa_write_probe_f32: bad args");
+  if (n == 0 || numel < 4) return FA_OK;
+  BcastArgs a;
+  memset(&a, 0, sizeof a);
+  a.n = n;
+  for (int i = 0; i < n; ++i) {
+    if (!dst[i] || !aligned16(dst[i]))
+      return set_err(FA_E_ALIGN, "fa_write_probe_f32: dst %d NULL or unaligned", i);
+    a.dst[i] = dst[i];
+  }
+  const int64_t parts = (numel / 4 + kBlock - 1) / kBlock;
+  const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
+  const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
+  if (parts * groups > (int64_t)UINT32_MAX)
+    return set_err(FA_E_RANGE, "fa_write_probe_f32: numel=%lld", (long long)numel);
+  hipLaunchKernelGGL(write_probe_kernel, dim3((unsigned)(parts * groups)), dim3(kBlock), 0,
+                     (hipStream_t)stream, a, numel, (uint32_t)parts, groups, gsize, seed);
+  HIP_TRY(hipGetLastError());
   return FA_OK;
 }
 

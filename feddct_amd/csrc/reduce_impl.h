@@ -131,6 +131,24 @@ __device__ __forceinline__ const float* vptr32(KArgs& a, int i) {
   else return cptr32(a, i);
 }
 
+// Destination pointer of a store loop, through SCALAR loads only: the
+// kernarg array, or the device table through the constant address space
+// (read-only for the launch).  cptr32's table arm is a generic global load,
+// and the compiler serves the runtime choice between the two arms with an
+// `s_waitcnt vmcnt(0)` before each client's stores (ISA checked, r04); vmcnt
+// counts stores on CDNA, so every wave waited for its previous client's
+// stores to complete before issuing the next client's.  Measured r04: the
+// broadcast of the cfg2 round 156 us with cptr32, 127-134 us in a lab kernel
+// whose pointers are scalar loads (tools/writelab.hip).
+typedef float* f32m;
+typedef const int64_t* i64p;
+__device__ __forceinline__ float* sptr32(KArgs& a, int i) {
+  return a.n <= kInline ? const_cast<float*>(a.c32[i]) : ((const FA_CONST f32m*)a.tab32)[i];
+}
+__device__ __forceinline__ int64_t* sptr64(KArgs& a, int i) {
+  return const_cast<int64_t*>(a.n <= kInline ? a.c64[i] : ((const FA_CONST i64p*)a.tab64)[i]);
+}
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // The weights of clients b0..b0+nb-1, read once per batch BEFORE its data
@@ -412,8 +430,7 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
     const f4 r = sum_only ? s : div4s(s, fn);
     st_out<POL>(a.out32, start, vi[u], r);
     if (!CHAIN && (a.flags & FA_F_BCAST)) {
-      for (int i = 0; i < n; ++i)
-        stg4<(POL & 2) != 0>(const_cast<float*>(vptr32<TAB>(a, i)) + start, vi[u], r);
+      for (int i = 0; i < n; ++i) stg4<(POL & 2) != 0>(sptr32(a, i) + start, vi[u], r);
     }
   }
 }

@@ -208,7 +208,7 @@ class ProximalTerm:
         return (getattr(self.client_model, "_fa_arena", None) is self.ca and self.ca.valid()
                 and getattr(self.global_model, "_fa_arena", None) is self.ga and self.ga.valid())
 
-    def __call__(self, flat_grads: bool = True) -> torch.Tensor:
+    def __call__(self, flat_grads: bool = False) -> torch.Tensor:
         if flat_grads:
             _, anchor, _ = self._flat_state()
             return _ProxFlat.apply(self, anchor)
@@ -216,18 +216,29 @@ class ProximalTerm:
 
 
 def proximal_term(client_model: torch.nn.Module, global_model: torch.nn.Module,
-                  flat_grads: bool = True) -> torch.Tensor:
+                  flat_grads: bool = False) -> torch.Tensor:
     """Σ_k ||w_k − w_t,k||₂ over zip(client.parameters(), global.parameters()),
     differentiable w.r.t. both (train_fedprox.py:113-115).  The bound term is
     cached on the client module (no global registry).
 
-    ``flat_grads=True`` (default): ``loss.backward()`` reaches ONE graph node,
-    whose backward adds the gradients into both models' ``.grad`` (made views
-    of a flat gradient bucket per model, rebound after ``zero_grad(
-    set_to_none=True)``), as autograd's accumulation would — for training
-    steps (train_fedprox.py:117-127).  ``torch.autograd.grad`` w.r.t. the
-    parameters, double backward and per-parameter gradient hooks need the
-    per-parameter node: ``flat_grads=False``."""
+    ``flat_grads=False`` (default): an ordinary autograd node whose inputs are
+    the parameters, so every autograd use works as with the reference's loop —
+    ``loss.backward()``, ``torch.autograd.grad(loss, params)``,
+    ``backward(inputs=...)``, per-parameter hooks and DDP reducer hooks.
+
+    ``flat_grads=True`` (opt-in, for a plain ``loss.backward()`` training
+    step, train_fedprox.py:117-127): ONE graph node whose only input is a
+    private anchor tensor; its backward adds the gradients into both models'
+    ``.grad``, made views of one flat gradient bucket per model (rebound after
+    ``zero_grad(set_to_none=True)``), in one launch — autograd's
+    per-parameter AccumulateGrad work skipped.  Because the parameters are
+    not inputs of that node, autograd prunes it from
+    ``torch.autograd.grad(loss, params)`` and ``backward(inputs=params)``
+    (the proximal gradient is then silently missing), parameter hooks never
+    see its share of ``.grad``, double backward raises, and with gradient
+    accumulation the fp32 sum is (g + prox) + task rather than
+    g + (task + prox) (equal to rounding).  Use it only where the step is
+    ``loss.backward()`` followed by the optimizer."""
     cache = client_model.__dict__.setdefault("_fa_prox", {})
     t = cache.get(id(global_model))
     if t is None or t.global_model is not global_model or not t.valid():

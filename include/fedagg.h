@@ -119,6 +119,14 @@ extern "C" {
                                                with the default batch only (by
                                                default the launch shape follows
                                                the round count, below)          */
+#define FA_PLAN_TUNE_BCAST_R03 0x20000000u /* tuning: FA_F_BCAST through the r02/r03
+                                               kernels (each client's pointer behind
+                                               a vmcnt(0) wait; groups of <= 10,
+                                               2048-float parts) */
+#define FA_PLAN_TUNE_BCAST_U2 0x40000000u /* tuning: the r04 broadcast with
+                                              2048-float parts (default 1024) */
+#define FA_PLAN_TUNE_BCAST_G24 0x80000000u /* tuning: the r04 broadcast in client
+                                               groups of <= 24 (default <= 10) */
 /* tuning: packed scalar tiles of 64 >> c columns (c = 0..3; default 64) */
 #define FA_PLAN_TUNE_PACK(c) (((unsigned)(c) & 3u) << 26)
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
@@ -341,6 +349,17 @@ int fa_prox_grad_ex(const fa_norm_plan *plan, const float *a, const float *b,
 
 /* Streaming copy (bandwidth ceiling calibration for the roofline). */
 int fa_copy_f32(const float *src, float *dst, int64_t numel, void *stream);
+/* Tuning (experiments only; calling thread): the store policy of the round
+ * broadcast's flat kernel — 0 global nt (default), 1 sc1, 2 sc1 nt,
+ * 3 sc0 sc1, 4 plain.  Returns the previous policy, or FA_E_INVAL. */
+int fa_tune_bcast_store(int policy);
+/* Write-only streaming probe (write-bandwidth ceiling, r04): the round
+ * broadcast's launch shape — one workgroup per (1024-float part, group of
+ * <= 10 destinations) — storing non-zero hashed values (a function of the
+ * element index and `seed`) into n <= 256 destination buckets of numel
+ * floats (the last numel % 4 are not written); nothing is read. */
+int fa_write_probe_f32(float *const *dst, int n, int64_t numel, unsigned seed,
+                       void *stream);
 /* Read-only streaming probe (read-bandwidth ceiling): grid > 0 — a
  * grid-stride loop, out[grid] partial sums (accumulated: zero out first);
  * grid == 0 — one 2048-float tile per workgroup, the reduce's own load shape,

@@ -666,6 +666,39 @@ def test_proximal_term_flat_grads_in_a_training_loop(set_to_none):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
 
 
+def test_proximal_term_default_works_with_autograd_grad():
+    """the default form is an ordinary autograd node over the
+    parameters, so torch.autograd.grad(loss, params) and
+    backward(inputs=params) see the proximal gradient; the opt-in one-node
+    form is pruned from them (documented: its node has no parameter inputs),
+    which this test pins so the caveat cannot silently change."""
+    from feddct_amd.prox import proximal_term
+    c, g = _prox_models(4)
+    c_ref, g_ref = _prox_models(4)
+    x = torch.randn(4, 7, device=DEV)
+    pt = sum((w - w_t).norm(2) for w, w_t in zip(c_ref.parameters(), g_ref.parameters()))
+    want = torch.autograd.grad(c_ref[3](x).square().sum() + 0.5 * pt, list(c_ref.parameters()))
+    got = torch.autograd.grad(c[3](x).square().sum() + 0.5 * proximal_term(c, g),
+                              list(c.parameters()))
+    for a, b in zip(got, want):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+    # backward(inputs=...) on the default form: the global side untouched
+    loss = c[3](x).square().sum() + 0.5 * proximal_term(c, g)
+    loss.backward(inputs=list(c.parameters()))
+    for a, b in zip(c.parameters(), want):
+        torch.testing.assert_close(a.grad, b, rtol=1e-5, atol=1e-7)
+    assert all(p.grad is None for p in g.parameters())
+    # the one-node form is pruned by autograd.grad: only the task gradient
+    task = torch.autograd.grad(c_ref[3](x).square().sum(), list(c_ref.parameters()),
+                               allow_unused=True)
+    flat = torch.autograd.grad(c[3](x).square().sum() + 0.5 * proximal_term(c, g, flat_grads=True),
+                               list(c.parameters()), allow_unused=True)
+    for a, b in zip(flat, task):
+        assert (a is None) == (b is None)
+        if a is not None:
+            torch.testing.assert_close(a, b)
+
+
 def test_proximal_term_tracks_training_and_aggregation():
     """Across an optimizer step and a server round the bound term stays
     current (params are arena views)."""
