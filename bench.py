@@ -445,6 +445,85 @@ def host_inclusive(layout, clients, reducer_dev, out32, out64, reps=3):
     return res
 
 
+def round_block(layout, clients, out32, out64, plan, extra, k=40):
+    """The whole server_aggregate round (train_fedavg.py:145-149: the mean,
+    the global's load, the broadcast into every client slot) on its measured
+    roofline: FA_F_BCAST = the reduce launch + the
+    broadcast launch.  Algorithmic bytes: reduce N*B read + B written,
+    broadcast B read + N*B written, 2*(N+1)*B in all.  Also each launch's
+    time inside the round (the round as two calls with events between them),
+    and this box's write ceiling: a write-only probe of non-zero hashed
+    register values in the broadcast's own launch shape over the client
+    buckets themselves (same placement), best of three passes — so it
+    overwrites the clients and runs after every measurement that needs their
+    values.  Ceiling fractions: the round's reads (N+1)*B at the read
+    ceiling plus its writes (N+1)*B at the write ceiling, over the round."""
+    n = len(clients)
+    B = layout.state_bytes()
+    red_bytes = layout.algorithmic_bytes(n)
+    bc_bytes = (n + 1) * B
+    bred = Reducer(layout, clients, out32, out64, flags=_lib.FA_F_BCAST, plan=plan)
+    t_round, _ = timed_launches(bred, k, 5)
+    # each launch inside the round
+    red = Reducer(layout, clients, out32, out64, plan=plan)
+    bco = Reducer(layout, clients, out32, out64, flags=_lib.FA_F_BCAST_ONLY, plan=plan)
+    for _ in range(3):
+        red()
+        bco()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * k + 1)]
+    ev[0].record()
+    for i in range(k):
+        red()
+        ev[2 * i + 1].record()
+        bco()
+        ev[2 * i + 2].record()
+    ev[-1].synchronize()
+    tr = sorted(ev[2 * i].elapsed_time(ev[2 * i + 1]) * 1e-3 for i in range(k))[k // 2]
+    tb = sorted(ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) * 1e-3 for i in range(k))[k // 2]
+    t_alone, _ = timed_launches(bco, k, 5)
+    # the write ceiling over the client buckets (their values are gone after)
+    dst = _lib.ptr_array([c[0].data_ptr() for c in clients])
+    numel = clients[0][0].numel()
+    seed = [0]
+
+    def write_probe():
+        seed[0] += 1
+        _lib.check(_lib.lib.fa_write_probe_f32(dst, n, numel, seed[0],
+                                               torch.cuda.current_stream().cuda_stream))
+    tw = min(timed_launches(write_probe, k, 3)[0] for _ in range(3))
+    wceil = n * numel * 4 / tw / 1e9
+    rceil = extra.get("read_ceiling_GBps")
+    out = {
+        "us": round(t_round * 1e6, 1),
+        "algorithmic_bytes": red_bytes + bc_bytes,
+        "GBps": round((red_bytes + bc_bytes) / t_round / 1e9, 1),
+        "frac": round((red_bytes + bc_bytes) / t_round / 1e9 / HBM_PEAK_GBS, 4),
+        "reduce_in_round_us": round(tr * 1e6, 1),
+        "bcast_in_round_us": round(tb * 1e6, 1),
+        "bcast_alone_us": round(t_alone * 1e6, 1),
+        "bcast_bytes": bc_bytes,
+        "bcast_in_round_frac": round(bc_bytes / tb / 1e9 / HBM_PEAK_GBS, 4),
+        "bcast_alone_frac": round(bc_bytes / t_alone / 1e9 / HBM_PEAK_GBS, 4),
+        "write_ceiling_GBps": round(wceil, 1),
+        "write_ceiling_probe": (f"fa_write_probe_f32: {n} x {numel} floats of hashed register "
+                                "values into the client buckets, the broadcast's launch shape "
+                                "(1024-float parts, groups of <= 10), best of 3 passes"),
+    }
+    if rceil:
+        # the time the round's bytes take at this box's read and write ceilings
+        t_ceil = (n + 1) * B / (rceil * 1e9) + (n + 1) * B / (wceil * 1e9)
+        tb_ceil = B / (rceil * 1e9) + n * B / (wceil * 1e9)
+        out["vs_box_ceilings"] = {
+            "round": round(t_ceil / t_round, 4),
+            "bcast_in_round": round(tb_ceil / tb, 4),
+            "bcast_alone": round(tb_ceil / t_alone, 4),
+            "round_vs_copy": round((red_bytes + bc_bytes) / t_round / 1e9
+                                   / extra["copy_ceiling_GBps"], 4),
+            "note": "ceiling time = reads at read_ceiling_GBps + writes at write_ceiling_GBps"}
+    extra["write_ceiling_GBps"] = out["write_ceiling_GBps"]
+    return out
+
+
 def separate_allocations_ab(layout, clients, reducer, out32, out64, rounds=3, k=50):
     """The headline's reduce over its slab-carved buckets (slab.py, the
     product's storage) against the same values in 20 + 1 separate
@@ -522,6 +601,33 @@ def other_configs(dev, steps=100, warmup=20):
             out["bit_exact_vs_reference_digest" if not any(
                 d.startswith("weighted/") for d in digests.values())
                 else "bit_exact_vs_weighted_definition_digest"] = bool(ok)
+        # the whole round: reduce + broadcast over the
+        # same rotated sets, as the product launches it (two launches), and
+        # the single-pass form (FA_F_BCAST inside the reduce) beside it
+        rb_bytes = sum(r[2].algorithmic_bytes(r[3]) + (r[3] + 1) * r[2].state_bytes()
+                       for r in sets[0])
+        for key, pflags in (("round", 0), ("round_fused", _lib.FA_PLAN_TUNE_FUSED_BCAST)):
+            rsets = []
+            for reds in sets:
+                rr = []
+                for names, prefixes, lay, n, red, o32, o64 in reds:
+                    plan = red.plan if pflags == 0 else _lib.Plan(
+                        lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
+                        flags=_lib.FA_PLAN_GAPS_ARE_PADDING | pflags)
+                    rr.append(Reducer(lay, red._keep[0], o32, o64,
+                                      weights=None if red.w is None else list(red.w),
+                                      flags=_lib.FA_F_BCAST, plan=plan))
+                rsets.append(rr)
+            kr = [0]
+
+            def rstep(rsets=rsets, kr=kr):
+                for r in rsets[kr[0] % rot]:
+                    r()
+                kr[0] += 1
+            tr, _ = timed_launches(rstep, steps, warmup)
+            out[f"{key}_us"] = round(tr * 1e6, 1)
+            out[f"{key}_frac"] = round(rb_bytes / tr / 1e9 / HBM_PEAK_GBS, 4)
+        out["round_algorithmic_bytes"] = rb_bytes
         res[name] = out
 
     run("cfg3_feddct_c10_n5", [(("wrnsl16_8_sf4_c10_main", "wrnsl16_8_sf4_c10_proxy"), 5, None)], 2,
@@ -916,15 +1022,37 @@ def dropin_timing(layout, clients, dev, reps=20):
         ts.append(time.perf_counter() - t0)
     ts.sort()
     t = ts[len(ts) // 2]
-    return {"server_aggregate_ms": round(t * 1e3, 3),
-            "note": "median wall incl. Python shim, arena checks, reduce + broadcast launches, sync"}
+    out = {"server_aggregate_ms": round(t * 1e3, 3),
+           "note": "median wall incl. Python shim, arena checks, reduce + broadcast launches, "
+                   "sync; gpu_round_us: the same round's two launches back to back"}
+    out.update(_bound_round_gpu(t))
+    return out
 
 
-def _feddct_modules(dev, n=5, cpu=False):
+def _bound_round_gpu(wall_s, reps=30):
+    """GPU time of the last drop-in round (the engine's bound round: its plan,
+    pointer arrays and buckets), its two launches timed back to back, and the
+    drop-in's wall time beyond it (host work before the launch + the sync)."""
+    from feddct_amd.aggregate import engine
+    e = engine()
+    rb = e._round
+    if rb is None:
+        return {"gpu_round_us": None}
+    ga = rb.arenas[0]()
+
+    def launch():
+        e._launch(rb.plan, rb.a32, rb.a64, rb.n, None, ga.f32.data_ptr(), ga.i64.data_ptr(),
+                  _lib.FA_F_BCAST, rb.dev)
+    tg, _ = timed_launches(launch, reps, 3)
+    return {"gpu_round_us": round(tg * 1e6, 1),
+            "host_share_us": round((wall_s - tg) * 1e6, 1)}
+
+
+def _feddct_modules(dev, n=5, cpu=False, classes=10):
     """BASELINE config 3's slots as nn.Modules: n main-client + n proxy
-    modules (wrnsl16_8 sf4 C10 state_dicts) holding the synthetic states,
-    plus the two global models."""
-    names = ("wrnsl16_8_sf4_c10_main", "wrnsl16_8_sf4_c10_proxy")
+    modules (wrnsl16_8 sf4 C10 state_dicts; config 5: C100, n = 24) holding
+    the synthetic states, plus the two global models."""
+    names = (f"wrnsl16_8_sf4_c{classes}_main", f"wrnsl16_8_sf4_c{classes}_proxy")
     out = []
     for nm in names:
         man = load_manifest(nm)
@@ -943,14 +1071,16 @@ def _feddct_modules(dev, n=5, cpu=False):
     return out
 
 
-def dropin_feddct_timing(dev, reps=20):
+def dropin_feddct_timing(dev, reps=20, n=5, classes=10):
     """The FedDCT drop-in ``server_aggregate(g_main, g_proxy, mains, proxies)``
-    (train_feddct.py:34-56) on BASELINE config 3's shape, end to end: the
-    result is checked against the reference's digests, then timed."""
+    (train_feddct.py:34-56) on BASELINE config 3's shape (config 5's with
+    n=24, classes=100), end to end: the result is checked against the
+    reference's digests, then timed."""
     from feddct_amd.feddct import server_aggregate
     with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
         dig = json.load(f)
-    (nm_m, lay_m, g_m, mains), (nm_p, lay_p, g_p, proxies) = _feddct_modules(dev)
+    (nm_m, lay_m, g_m, mains), (nm_p, lay_p, g_p, proxies) = _feddct_modules(
+        dev, n=n, classes=classes)
     server_aggregate(g_m, g_p, mains, proxies)
     torch.cuda.synchronize()
     import hashlib
@@ -960,7 +1090,7 @@ def dropin_feddct_timing(dev, reps=20):
         for k, v in g.state_dict().items():
             h.update(k.encode())
             h.update(v.detach().cpu().numpy().tobytes())
-        ok &= h.hexdigest() == dig[f"feddct/{nm}/n5"]
+        ok &= h.hexdigest() == dig[f"feddct/{nm}/n{n}"]
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -968,9 +1098,12 @@ def dropin_feddct_timing(dev, reps=20):
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     ts.sort()
-    return {"server_aggregate_ms": round(ts[len(ts) // 2] * 1e3, 3),
-            "bit_exact_vs_reference_digest": bool(ok),
-            "note": "cfg3 shape: 5 slots x (main + proxy), median wall incl. sync"}
+    out = {"server_aggregate_ms": round(ts[len(ts) // 2] * 1e3, 3),
+           "bit_exact_vs_reference_digest": bool(ok),
+           "note": f"cfg{3 if n == 5 else 5} shape: {n} slots x (main + proxy), median wall "
+                   "incl. sync; gpu_round_us: the same round's two launches back to back"}
+    out.update(_bound_round_gpu(ts[len(ts) // 2]))
+    return out
 
 
 
@@ -1406,15 +1539,18 @@ def main():
             # the round with its broadcast (FA_F_BCAST: reduce launch + broadcast
             # launch over the same tiles), N*B read + (N+1)*B written — after
             # every measurement that needs the clients' own values
-            bred = Reducer(layout, clients, torch.zeros_like(out32), torch.zeros_like(out64),
-                           flags=_lib.FA_F_BCAST, plan=reducer.plan)
-            tb, _ = timed_launches(bred, max(10, args.steps // 2), 3)
-            extra["round_with_broadcast_us"] = round(tb * 1e6, 1)
+            extra["round"] = round_block(layout, clients, out32, out64, reducer.plan,
+                                         extra, max(20, args.steps // 2))
+            extra["round_with_broadcast_us"] = extra["round"]["us"]
             extra["dropin"] = dropin_timing(layout, clients, dev)
             try:
                 extra["dropin_feddct_cfg3"] = dropin_feddct_timing(dev)
             except Exception as e:  # noqa: BLE001
                 extra["dropin_feddct_cfg3"] = {"error": repr(e)}
+            try:
+                extra["dropin_feddct_cfg5"] = dropin_feddct_timing(dev, n=24, classes=100)
+            except Exception as e:  # noqa: BLE001
+                extra["dropin_feddct_cfg5"] = {"error": repr(e)}
             extra["other_configs"] = other_configs(dev)
             try:
                 extra["next_rows"] = next_rows(dev)

@@ -17,7 +17,9 @@ def server_aggregate(global_model, client_models):
     return _sa(global_model, client_models)
 
 
-def set_summation_order(order: str) -> None:
-    """"torch_cpu" (default) or "torch_gpu": see aggregate.set_summation_order."""
+def set_summation_order(order: str, strict: bool = False) -> None:
+    """"torch_cpu" (default) or "torch_gpu" (torch-ROCm's GPU mean on this
+    device, not the published NVIDIA runs' order): see
+    aggregate.set_summation_order."""
     from .aggregate import set_summation_order as _s
-    _s(order)
+    _s(order, strict)

@@ -35,7 +35,10 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
-from . import _lib
+from array import array
+
+from . import _lib, slab
+from . import arena as _arena
 from .arena import ModuleArena, get_arena
 from .layout import BucketLayout
 
@@ -51,6 +54,89 @@ def _require_gpu():
                            "no CPU fallback")
 
 
+class _RoundBinding:
+    """The last device-resident round's bound state (r04 fast path): the
+    global and client modules, their arenas, plan, pointer arrays, and ONE
+    flattened validity check over every bound tensor.  A repeat call on the
+    same modules re-checks only (a) that no module anywhere registered a
+    parameter, buffer or submodule since (arena._STRUCT_GEN), (b) that each
+    module still carries the same arena, and (c) in one C call
+    (_fa_shim.valid_tagged): every parameter/buffer dict's PEP 509 version
+    tag — unchanged tag, unchanged slots — and every bound tensor's data
+    pointer (a `.data` swap).  Anything else takes the full path, which
+    re-binds what changed and records a new binding."""
+
+    __slots__ = ("gref", "crefs", "arenas", "gen", "dicts", "tags", "tensors", "ptrs",
+                 "written", "packed", "plan", "a32", "a64", "n", "dev", "order", "weighted",
+                 "__weakref__")
+
+    def __init__(self, engine, global_model, client_models, ga, cas, plan, a32, a64, order,
+                 weighted):
+        from . import _fa_shim
+        # modules and arenas held weakly: the binding must not keep a dropped
+        # round's modules or buckets alive; when any of them goes, so does
+        # the binding (its tensor tuples hold the bound parameters)
+        eng, me = weakref.ref(engine), weakref.ref(self)
+
+        def dropped(_r):
+            e = eng()
+            if e is not None and me() is not None and e._round is me():
+                e._round = None
+        self.gref = weakref.ref(global_model, dropped)
+        self.crefs = tuple(weakref.ref(m, dropped) for m in client_models)
+        arenas = (ga, *cas)
+        self.arenas = tuple(weakref.ref(a, dropped) for a in arenas)
+        self.gen = _arena._STRUCT_GEN[0]
+        dicts, seen = [], set()
+        tensors, ptrs = [], array("Q")
+        for a in arenas:
+            for d, _, t, p in a._checks:
+                if id(d) not in seen:
+                    seen.add(id(d))
+                    dicts.append(d)
+                tensors.append(t)
+                ptrs.append(p)
+            for d, _, _, _ in a._packed:
+                if id(d) not in seen:
+                    seen.add(id(d))
+                    dicts.append(d)
+        self.dicts = tuple(dicts)
+        self.tags = _fa_shim.dict_tags(self.dicts)   # None: no tags (CPython >= 3.12)
+        self.tensors = tuple(tensors)
+        self.ptrs = ptrs.tobytes()
+        self.written = tuple(t for a in arenas for t in a._written)
+        self.packed = tuple(i for i, a in enumerate(arenas) if a._packed)
+        self.plan, self.a32, self.a64 = plan, a32, a64
+        self.n = len(cas)
+        self.dev = cas[0].device
+        self.order = order
+        self.weighted = weighted
+
+    def same_modules(self, global_model, client_models, order, weighted) -> bool:
+        """The cheap half of the check: the same modules, arenas, order and
+        weighting, and no tensor/module registration anywhere since."""
+        if (self.tags is None or self.order != order or self.weighted != weighted
+                or _arena._STRUCT_GEN[0] != self.gen or self.gref() is not global_model
+                or len(client_models) != self.n):
+            return False
+        if global_model.__dict__.get("_fa_arena") is not self.arenas[0]():
+            return False
+        for r, m, a in zip(self.crefs, client_models, self.arenas[1:]):
+            if r() is not m or m.__dict__.get("_fa_arena") is not a():
+                return False
+        return True
+
+    def views_intact(self) -> bool:
+        """The per-tensor half (one C call): every parameter/buffer dict's
+        version tag and every bound tensor's data pointer unchanged."""
+        from . import _fa_shim
+        return _fa_shim.valid_tagged(self.dicts, self.tags, self.tensors, self.ptrs)
+
+    def matches(self, global_model, client_models, order, weighted) -> bool:
+        return (self.same_modules(global_model, client_models, order, weighted)
+                and self.views_intact())
+
+
 class Engine:
     """Plan/staging caches for one process (one GPU per process)."""
 
@@ -62,9 +148,16 @@ class Engine:
         # torch-GPU-order plans are cut per client count: a small LRU, so a
         # loop whose participation varies does not grow device plans forever
         self._gpu_plans: "OrderedDict[tuple, Optional[_lib.Plan]]" = OrderedDict()
-        self._warned_gpu_order = False
+        # rounds the torch-GPU order could not restate, per (layout, N): a
+        # warning for each new pair, and a count callers can query
+        # (gpu_order_fallbacks) — ADVICE r03: warning once per Engine hid
+        # every later layout / N from a caller who set the order for parity
+        self.gpu_order_fallbacks: Dict[tuple, int] = {}
+        self.strict_gpu_order = False
+        self._fallback_round = False
         self._layouts: Dict[tuple, BucketLayout] = {}
         self._pipes: Dict[tuple, object] = {}
+        self._round: Optional[_RoundBinding] = None
 
     # ------------------------------------------------------------ caches --
     GPU_PLAN_CACHE = 8
@@ -110,17 +203,63 @@ class Engine:
         return self._layouts.setdefault(lay.signature, lay)
 
     # ------------------------------------------------------------- core --
+    def try_bound_round(self, global_model: torch.nn.Module,
+                        client_models: Sequence[torch.nn.Module],
+                        weights: Optional[Sequence[float]] = None) -> bool:
+        """The repeat call's fast path (r04): when these exact modules made
+        the last device-resident round (_RoundBinding.same_modules), the
+        reduce is launched at once and the per-tensor check
+        (_RoundBinding.views_intact) runs on the host while the GPU reduces;
+        the broadcast is launched only after the check has passed, then the
+        version counters are bumped while the GPU broadcasts.  The reduce
+        reads the client buckets and writes only the global's bucket, whose
+        value the round replaces anyway, so a failed check loses nothing:
+        False, and the caller takes the full path (re-bind, whole round).
+        Measured r04 (tools/shim_profile.py): the check is 13 us for the
+        cfg2 shape's 2,058 tensors and 64 us for cfg5's 9,800 — now hidden
+        behind the reduce instead of before the launch."""
+        rb = self._round
+        if rb is None or not rb.same_modules(global_model, client_models, self.order,
+                                             weights is not None):
+            return False
+        if torch.cuda.current_device() != rb.dev.index:
+            return False
+        arenas = [r() for r in rb.arenas]
+        for i in rb.packed:
+            arenas[i].pack()
+        ga = arenas[0]
+        stream = ctypes.c_void_p(torch.cuda.current_stream(rb.dev).cuda_stream)
+        o32, o64 = ga.f32.data_ptr(), ga.i64.data_ptr()
+        fa_reduce = _lib.lib.fa_reduce
+        _lib.check(fa_reduce(rb.plan.handle, rb.a32, rb.a64, rb.n,
+                             self._weights_arg(weights, rb.n), o32, o64, 0, stream), "fa_reduce")
+        if not rb.views_intact():
+            self._round = None
+            return False
+        _lib.check(fa_reduce(rb.plan.handle, rb.a32, rb.a64, rb.n, None, o32, o64,
+                             _lib.FA_F_BCAST_ONLY, stream), "fa_reduce")
+        if rb.packed:
+            ga.unpack()
+            for c in arenas[1:]:
+                c.unpack(ga)
+        from . import _fa_shim
+        _fa_shim.bump_versions(rb.written)
+        return True
+
     def reduce_modules(self, global_model: torch.nn.Module,
                        client_models: Sequence[torch.nn.Module],
                        weights: Optional[Sequence[float]] = None,
                        broadcast: bool = True) -> None:
+        if broadcast and self.try_bound_round(global_model, client_models, weights):
+            return
         n = len(client_models)
         if n == 0:
             raise RuntimeError("stack expects a non-empty TensorList")
         _require_gpu()
         layout = self.layout_of(global_model)
-        ga = get_arena(global_model, layout)
-        cas = [get_arena(c, layout) for c in client_models]
+        with slab.expecting(n + 1):   # a new slab sized for this round's buckets
+            ga = get_arena(global_model, layout)
+            cas = [get_arena(c, layout) for c in client_models]
         # torch.stack (train_fedavg.py:145) needs the clients on one device;
         # the global may live elsewhere (load_state_dict at :147 copies across)
         dev = cas[0].device
@@ -138,7 +277,14 @@ class Engine:
             c.pack()
         if dev.type == "cuda":
             if ga.device == dev:
-                self._reduce_device(layout, ga.f32, ga.i64, cas, weights, fuse_bcast)
+                self._fallback_round = False
+                plan = self._reduce_device(layout, ga.f32, ga.i64, cas, weights, fuse_bcast)
+                # (a round the torch-GPU order could not restate is never bound:
+                # each such call takes this path, is counted and can be refused)
+                if fuse_bcast and _arena._fa_shim is not None and not self._fallback_round:
+                    a32, a64 = self._ptr_arrays(cas)
+                    self._round = _RoundBinding(self, global_model, client_models, ga, cas,
+                                                plan, a32, a64, self.order, weights is not None)
             else:
                 o32, o64 = self._stage(layout, dev)
                 self._reduce_device(layout, o32, o64, cas, weights, fuse_bcast)
@@ -214,17 +360,23 @@ class Engine:
             order = "torch_cpu"   # (the GPU order is torch's unweighted mean, N >= 2)
         plan = self.plan(layout, dev, n, order)
         if plan is None:   # torch would split a key across blocks at this N
-            if not self._warned_gpu_order:
-                warnings.warn(f"feddct_amd: torch-GPU summation order is not restated for "
-                              f"N={n} on this layout (torch splits a key across blocks); "
-                              "this round uses torch's CPU order", RuntimeWarning,
-                              stacklevel=3)
-                self._warned_gpu_order = True
+            msg = (f"feddct_amd: torch-GPU summation order is not restated for N={n} on "
+                   f"this layout (torch splits a key across blocks)")
+            if self.strict_gpu_order:
+                raise RuntimeError(msg + "; strict mode (set_summation_order(..., strict=True))")
+            key = (layout.signature, n)
+            seen = self.gpu_order_fallbacks.get(key, 0)
+            self.gpu_order_fallbacks[key] = seen + 1
+            if seen == 0:
+                warnings.warn(msg + "; rounds of this layout at this N use torch's CPU order",
+                              RuntimeWarning, stacklevel=3)
             plan = self.plan(layout, dev, n, "torch_cpu")
+            self._fallback_round = True
         flags = _lib.FA_F_BCAST if fuse else 0
         a32, a64 = self._ptr_arrays(cas)
         self._launch(plan, a32, a64, n, self._weights_arg(weights, n), out32.data_ptr(),
                      out64.data_ptr(), flags, dev)
+        return plan
 
     def _reduce_host(self, layout, ga: ModuleArena, cas: List[ModuleArena], weights, fuse):
         """Host-resident state (the reference's CPU configuration): the
@@ -301,6 +453,9 @@ def server_aggregate_split(global_model_a, global_model_b, models_a, models_b):
         try:
             g = _pair(global_model_a, global_model_b)
             pairs = [_pair(a, b) for a, b in zip(models_a, models_b)]
+            # a bound round exists only for pairs without extra keys
+            if e.try_bound_round(g, pairs):
+                return
             layout = e.layout_of(g)
             arenas = [get_arena(p, layout) for p in pairs]
             if not any(a.extra_keys for a in arenas):
@@ -336,20 +491,26 @@ def aggregate_weighted(global_model, client_models, weights=None, sizes=None,
         engine().reduce_modules(global_model, list(client_models), w, broadcast)
 
 
-def set_summation_order(order: str) -> None:
+def set_summation_order(order: str, strict: bool = False) -> None:
     """Which torch order device-resident rounds reproduce bit for bit:
     ``"torch_cpu"`` (default: torch's CPU stack(...).mean(0), the reference's
     BASELINE config 1 and its device-independent definition) or
-    ``"torch_gpu"`` (torch-ROCm's own GPU reduction — what the reference's
-    training runs computed, their models being on the GPU,
-    train_fedavg.py:244-250; unweighted rounds of N >= 2 clients; a round
-    torch would split across thread blocks warns once and takes the CPU
-    order).
+    ``"torch_gpu"`` (torch-ROCm's GPU reduction on THIS device: what the
+    unchanged reference script computes when its models sit on this MI355X,
+    train_fedavg.py:244-250 — restated from the torch-ROCm 2.x headers and
+    pinned against torch's own `cuda` mean on this GPU.  It is NOT the order
+    of the reference's published runs, which ran torch 1.10/1.11 on NVIDIA
+    GPUs with another block configuration; parity with those runs is
+    unpinned.  Unweighted rounds of N >= 2 clients; a round torch would
+    split across thread blocks takes the CPU order, with a RuntimeWarning
+    for each new (layout, N) and a count in ``engine().gpu_order_fallbacks``
+    — or, with ``strict=True``, raises instead.  See INTEGRATION.md).
     Host-resident modules always take the CPU order, which is what the
     reference computes for them."""
     if order not in ORDERS:
         raise ValueError(f"order must be one of {sorted(ORDERS)}, not {order!r}")
     engine().order = order
+    engine().strict_gpu_order = bool(strict)
 
 
 def summation_order() -> str:

@@ -1146,11 +1146,14 @@ int round_batch(int dev, int n, int vec_u, bool w, unsigned pflags, int ntiles) 
 // instead was slower, see above).  Same process, weighted, split vs plain
 // (profiles/r03_exp_round_quant_tail_split*.jsonl): r = 10 137.9 vs 143.8
 // us, r = 85 139.5 vs 144.0, r = 135 141.5 vs 144.8, r = 285 144.8 vs 146.3,
-// r = 335 145.4 vs 147.6 — a gain at every r up to 0.44 slots, so it is
-// applied for 0 < r <= slots / kTailDiv.
-constexpr int64_t kTailDiv = 2;
+// r = 335 145.4 vs 147.6 — a gain at every r measured, up to 0.44 slots,
+// so it is applied for 0 < r <= 0.44 slots (r03 applied it up to
+// slots / 2, past the measured range).  A tile too small to halve (< 2 *
+// kMinTile / 2 elements: ragged ends of runs) is left whole, so such a table
+// may end up a few tiles short of exactly k rounds; the bits never change.
+constexpr int64_t kTailMaxPct = 44;
 std::vector<Tile> split_tail(const std::vector<Tile>& tiles, int64_t r, int slots) {
-  if (r <= 0 || r * kTailDiv > slots) return {};
+  if (r <= 0 || r * 100 > kTailMaxPct * (int64_t)slots) return {};
   std::vector<Tile> vec;
   for (const Tile& x : tiles)
     if (x.kind == K_F32_VEC) vec.push_back(x);

@@ -834,6 +834,10 @@ struct fa_round_plan {
   std::list<Graph> graphs;
   hipStream_t gs = nullptr;     // capture stream
   bool graph_failed = false;    // capture refused once: this plan runs uncaptured
+  // one rank (r04): every form is the plain single-GPU reduction of all the
+  // slots, one fa_reduce call on this plan (no chunks, planes, copies or
+  // empty exchanges)
+  fa_plan* single = nullptr;
 };
 
 namespace {
@@ -843,6 +847,7 @@ void free_round(fa_round_plan* p) {
   DeviceGuard dg;
   if (p->device >= 0) (void)hipSetDevice(p->device);
   for (fa_plan* c : p->chunk) fa_plan_destroy(c);
+  fa_plan_destroy(p->single);
   fa_plan_destroy(p->stripe);
   fa_plan_destroy(p->plan64);
   fa_plan_destroy(p->plan_t32);
@@ -928,6 +933,17 @@ int make_round(fa_comm* comm, int mode, const fa_seg* seg32, int nseg32, int64_t
     free_round(p);
     return code;
   };
+  if (g.nranks == 1) {
+    // One rank (r04): the round IS the single-GPU
+    // reduction — every form's own kernels (chunked chain segments, block
+    // sums and their fold, stripe copies, partial sums) and its empty
+    // exchanges cost 1.2-2.1x the plain launch on one rank
+    // (profiles/r03_native_round_cost_nographs.jsonl), for the same bits.
+    rc = fa_plan_create(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, 0, flags, &p->single);
+    if (rc) return fail(rc);
+    *out = p;
+    return FA_OK;
+  }
   if ((rc = build_round(p, nchunks, &vec, &cut, &tails, &tidx))) return fail(rc);
   // tile plans
   if (mode == FA_MODE_SHARDED) {
@@ -1551,6 +1567,15 @@ int run_round(fa_round_plan* const* plans, int nlocal, const fa_shard_io* io, in
       return set_err(FA_E_INVAL, "%s: result buckets required on rank %d", who, g.rank);
     if (p->g.n_total != plans[0]->g.n_total || p->range.size() != plans[0]->range.size())
       return set_err(FA_E_INVAL, "%s: plans of different layouts", who);
+    if (p->single) {
+      // one rank: the plain reduction (fa_reduce's own checks apply)
+      if (nlocal != 1) return set_err(FA_E_INVAL, "%s: a one-rank plan drives one GPU", who);
+      DeviceGuard dg1;
+      const hipError_t he = hipSetDevice(p->device);
+      if (he != hipSuccess) return set_err(FA_E_HIP, "%s: %s", who, hipGetErrorString(he));
+      return fa_reduce(p->single, io[d].c32, io[d].c64, g.n_total, io[d].weights, io[d].out32,
+                       io[d].out64, 0, io[d].stream);
+    }
     Local L;
     L.p = p;
     L.io = &io[d];

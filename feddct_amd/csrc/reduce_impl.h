@@ -580,7 +580,7 @@ __device__ __forceinline__ void tile_scalar_packed(KArgs& a, int k) {
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t* ents = a.sidx + (int64_t)k * kPackCols;
-  if (n > kStageFloats) {  // (N > 8192) direct loads, one column per lane of wave 0
+  if (n > kStageFloats) {  // (N > 4096) direct loads, one column per lane of wave 0
     if (wv == 0) {
       const int64_t ent = ents[lane];
       if (ent >= 0)

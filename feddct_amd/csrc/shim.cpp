@@ -55,6 +55,81 @@ PyObject* valid_views(PyObject*, PyObject* args) {
   Py_RETURN_TRUE;
 }
 
+// The round fast path's check (r04): a dict's version tag (PEP 509; CPython
+// < 3.12 keeps it in every dict) changes with every store into the dict, so
+// an unchanged tag proves that each parameter / buffer slot still holds the
+// tensor bound to it, and only the `.data` swap (which leaves the dict alone)
+// remains to be checked, one data pointer per tensor — no dict lookups.
+// dict_tags(dicts) -> bytes of uint64 tags, or None where tags are not
+// available (the caller then keeps the lookup check).
+// valid_tagged(dicts, tags, tensors, ptrs) -> bool: every dict's tag
+// unchanged and every tensor's data pointer the bound one.
+#if PY_VERSION_HEX < 0x030C0000
+#define FA_DICT_TAGS 1
+#endif
+
+PyObject* dict_tags(PyObject*, PyObject* args) {
+  PyObject* dicts;
+  if (!PyArg_ParseTuple(args, "O!", &PyTuple_Type, &dicts)) return nullptr;
+#ifdef FA_DICT_TAGS
+  const Py_ssize_t n = PyTuple_GET_SIZE(dicts);
+  PyObject* out = PyBytes_FromStringAndSize(nullptr, n * (Py_ssize_t)sizeof(uint64_t));
+  if (!out) return nullptr;
+  char* p = PyBytes_AS_STRING(out);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* d = PyTuple_GET_ITEM(dicts, i);
+    if (!PyDict_Check(d)) {
+      Py_DECREF(out);
+      PyErr_SetString(PyExc_TypeError, "dict_tags: expected dicts");
+      return nullptr;
+    }
+    const uint64_t tag = ((PyDictObject*)d)->ma_version_tag;
+    std::memcpy(p + i * sizeof(uint64_t), &tag, sizeof tag);
+  }
+  return out;
+#else
+  (void)dicts;
+  Py_RETURN_NONE;
+#endif
+}
+
+PyObject* valid_tagged(PyObject*, PyObject* args) {
+  PyObject *dicts, *tags, *tensors, *ptrs;
+  if (!PyArg_ParseTuple(args, "O!SO!S", &PyTuple_Type, &dicts, &tags, &PyTuple_Type, &tensors,
+                        &ptrs))
+    return nullptr;
+#ifdef FA_DICT_TAGS
+  const Py_ssize_t nd = PyTuple_GET_SIZE(dicts), n = PyTuple_GET_SIZE(tensors);
+  if (PyBytes_GET_SIZE(tags) != nd * (Py_ssize_t)sizeof(uint64_t) ||
+      PyBytes_GET_SIZE(ptrs) != n * (Py_ssize_t)sizeof(uint64_t)) {
+    PyErr_SetString(PyExc_ValueError, "valid_tagged: length mismatch");
+    return nullptr;
+  }
+  const char* tp = PyBytes_AS_STRING(tags);
+  for (Py_ssize_t i = 0; i < nd; ++i) {
+    PyObject* d = PyTuple_GET_ITEM(dicts, i);
+    uint64_t want;
+    std::memcpy(&want, tp + i * sizeof(uint64_t), sizeof want);
+    if (!PyDict_Check(d) || ((PyDictObject*)d)->ma_version_tag != want) Py_RETURN_FALSE;
+  }
+  const char* p = PyBytes_AS_STRING(ptrs);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* t = PyTuple_GET_ITEM(tensors, i);
+    if (!THPVariable_Check(t)) Py_RETURN_FALSE;
+    uint64_t want;
+    std::memcpy(&want, p + i * sizeof(uint64_t), sizeof want);
+    if ((uint64_t)(uintptr_t)THPVariable_Unpack(t).data_ptr() != want) Py_RETURN_FALSE;
+  }
+  Py_RETURN_TRUE;
+#else
+  (void)dicts;
+  (void)tags;
+  (void)tensors;
+  (void)ptrs;
+  Py_RETURN_FALSE;
+#endif
+}
+
 // bump_versions(tensors) -> None: torch.autograd.graph.increment_version
 // for every tensor of the tuple.
 PyObject* bump_versions(PyObject*, PyObject* args) {
@@ -134,6 +209,8 @@ PyMethodDef kMethods[] = {
     {"grad_state", grad_state, METH_VARARGS, "is every .grad its bucket view / None"},
     {"bind_grads", bind_grads, METH_VARARGS, ".grad = bucket view for every parameter"},
     {"valid_views", valid_views, METH_VARARGS, "arena validity check (see shim.cpp)"},
+    {"dict_tags", dict_tags, METH_VARARGS, "PEP 509 version tags of dicts (None: unavailable)"},
+    {"valid_tagged", valid_tagged, METH_VARARGS, "tag + data-pointer validity check"},
     {"bump_versions", bump_versions, METH_VARARGS, "autograd version bump of every tensor"},
     {nullptr, nullptr, 0, nullptr}};
 

@@ -20,6 +20,18 @@ is.  Buckets are never recycled within a slab: the reference creates its
 client models once and keeps them for every round (train_fedavg.py:367-380),
 so the carve is append-only.  Set FA_SLAB=0 to allocate every bucket on its
 own (the r02 behaviour).
+
+Sizing (r04): a new slab holds as many buckets of the requested
+size as the caller says it expects (``expecting(count)``: the engine binds a
+round's N clients + the global under ``expecting(N + 1)``), else
+SLAB_BUCKETS; always within MIN_SLAB..MAX_SLAB.
+
+Limits of carved buckets: a bucket's storage is a slice of the
+slab's, so its data pointer is not one the caching allocator handed out —
+``Tensor.record_stream`` on a bucket is a silent no-op (a bucket used on a
+side stream must be kept alive by the caller until that stream is done), and
+CUDA/HIP IPC sharing of buckets (``torch.multiprocessing``) is not
+supported.  Callers that need either set FA_SLAB=0 (plain allocations).
 """
 from __future__ import annotations
 
@@ -35,14 +47,32 @@ SLAB_BUCKETS = 24                 # buckets of the requested size per new slab
 
 _lock = threading.Lock()
 _current: dict = {}               # device -> [slab tensor (uint8), bytes handed out]
+_expect = threading.local()       # .count: buckets the caller expects to carve
 
 
 def enabled() -> bool:
     return os.environ.get("FA_SLAB", "1") != "0"
 
 
+class expecting:
+    """Context: the buckets carved inside are ``count`` of a kind, so a new
+    slab started there is sized for ``count`` of them (not SLAB_BUCKETS)."""
+
+    def __init__(self, count: int):
+        self.count = max(1, int(count))
+
+    def __enter__(self):
+        self.prev = getattr(_expect, "count", None)
+        _expect.count = self.count
+        return self
+
+    def __exit__(self, *exc):
+        _expect.count = self.prev
+
+
 def _slab_bytes(need: int) -> int:
-    size = min(max(SLAB_BUCKETS * need, MIN_SLAB), MAX_SLAB)
+    count = getattr(_expect, "count", None) or SLAB_BUCKETS
+    size = min(max(count * need, MIN_SLAB), MAX_SLAB)
     return max(size, need)
 
 

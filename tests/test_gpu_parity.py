@@ -446,6 +446,78 @@ def test_shim_second_round_and_rebind():
         assert bits_equal(clients[2].state_dict()[k].cpu().numpy(), want), k
 
 
+@pytest.mark.parametrize("change", ["none", "inplace", "data_swap", "new_param", "dict_store",
+                                    "new_buffer", "other_clients", "weighted"])
+def test_bound_round_fast_path_sees_every_change(change):
+    """r04: a repeat server_aggregate on the same modules takes the bound
+    round (Engine.try_bound_round); anything that changes what is bound must
+    send it down the full path (re-bind), and every round equals the
+    reference's arithmetic on the modules' values at call time."""
+    import gc
+    from feddct_amd import aggregate as A
+    from feddct_amd.fedavg import server_aggregate
+    man = {"keys": [{"key": "w", "shape": [1000], "dtype": "float32"},
+                    {"key": "b", "shape": [7], "dtype": "float32"},
+                    {"key": "n", "shape": [], "dtype": "int64"}]}
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(5)]
+    g = StateModule(man).to(DEV)
+    clients = _modules(man, states)
+    server_aggregate(g, clients)
+    e = A.engine()
+    assert e._round is not None
+    calls = []
+    orig = e.try_bound_round
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        calls.append(r)
+        return r
+    e.try_bound_round = spy
+    try:
+        with torch.no_grad():
+            for i, c in enumerate(clients):
+                c.w.mul_(float(i + 2))
+        want_fast = change in ("none", "inplace")
+        if change == "data_swap":
+            clients[1].w.data = clients[1].w.data.clone() + 1
+        elif change == "new_param":
+            clients[3].b = torch.nn.Parameter(clients[3].b.detach().clone() - 2)
+        elif change == "dict_store":
+            clients[0]._parameters["b"] = torch.nn.Parameter(clients[0].b.detach().clone() * 3)
+        elif change == "new_buffer":
+            clients[2].register_buffer("extra_nonpersistent", torch.zeros(2, device=DEV),
+                                       persistent=False)
+        elif change == "other_clients":
+            clients = clients[:4]
+        weights = None
+        if change == "weighted":
+            weights = [1.0, 2.0, 3.0, 4.0, 5.0]
+        snap = [[(k, v.detach().cpu().numpy().copy()) for k, v in c.state_dict().items()]
+                for c in clients]
+        if weights is None:
+            server_aggregate(g, clients)
+        else:
+            A.aggregate_weighted(g, clients, sizes=weights)
+        torch.cuda.synchronize()
+        assert calls and calls[0] == want_fast, (change, calls)
+        if weights is None:
+            for (k, want) in O.aggregate_state(snap):
+                assert bits_equal(g.state_dict()[k].cpu().numpy(), want), (change, k)
+                for c in clients:
+                    assert bits_equal(c.state_dict()[k].cpu().numpy(), want), (change, k)
+        # and the round after the change is bound again
+        calls.clear()
+        server_aggregate(g, clients) if weights is None else A.aggregate_weighted(
+            g, clients, sizes=weights)
+        assert calls == [True]
+    finally:
+        del e.try_bound_round
+    # the binding does not keep a dropped round alive
+    del g, clients, snap
+    gc.collect()
+    assert e._round is None
+
+
 def test_shim_errors_like_reference():
     from feddct_amd.fedavg import server_aggregate
     man = {"keys": [{"key": "w", "shape": [10], "dtype": "float32"}]}

@@ -284,6 +284,39 @@ def test_dropin_gpu_order_outside_restatement_warns_and_uses_cpu_order():
         assert g.state_dict()[k].cpu().numpy().tobytes() == np.asarray(want).tobytes(), k
 
 
+def test_dropin_gpu_order_fallback_is_counted_per_layout_and_n_and_strict_raises():
+    """every round outside the restatement is counted per
+    (layout, N) in engine().gpu_order_fallbacks, each new pair warns (a
+    repeat does not), and strict mode raises instead of falling back."""
+    import warnings
+    import feddct_amd
+    from feddct_amd import aggregate as A
+    from feddct_amd.fedavg import server_aggregate
+    from helpers import StateModule
+    e = A.engine()
+    for shape, n in (([4096], 600), ([2048], 600), ([4096], 700)):
+        man = {"keys": [{"key": "w", "shape": shape, "dtype": "float32"}]}
+        mods = [StateModule(man).load_numpy(synth.gen_state(man, i)).to(DEV) for i in range(n)]
+        g = StateModule(man).to(DEV)
+        feddct_amd.set_summation_order("torch_gpu")
+        try:
+            sig = A.engine().layout_of(g).signature
+            before = e.gpu_order_fallbacks.get((sig, n), 0)
+            with warnings.catch_warnings(record=True) as w:
+                warnings.simplefilter("always")
+                server_aggregate(g, mods)
+                server_aggregate(g, mods)
+            warned = sum("not restated" in str(x.message) for x in w)
+            assert warned == (1 if before == 0 else 0), (shape, n, warned)
+            assert e.gpu_order_fallbacks[(sig, n)] == before + 2
+            feddct_amd.set_summation_order("torch_gpu", strict=True)
+            with pytest.raises(RuntimeError, match="strict"):
+                server_aggregate(g, mods)
+        finally:
+            feddct_amd.set_summation_order("torch_cpu")
+    assert e.strict_gpu_order is False
+
+
 def test_dropin_gpu_order_sf2_proxy_layout_n48():
     """the drop-in at N = 48 on the wrnsl16_8 sf2 proxy
     layout (script/feddct_wrn168_split2_cifar100_96clients_96choose_650rounds

@@ -77,3 +77,23 @@ def test_slab_size_rule():
     assert slab._slab_bytes(n) == slab.SLAB_BUCKETS * n
     assert slab._slab_bytes(1 << 30) == slab.MAX_SLAB
     assert slab._slab_bytes(3 << 30) == 3 << 30
+
+
+def test_slab_sized_for_the_expected_bucket_count():
+    """a slab started inside expecting(k) holds k buckets of the
+    requested size (within MIN_SLAB..MAX_SLAB), not SLAB_BUCKETS."""
+    n = 44 << 20
+    with slab.expecting(21):
+        assert slab._slab_bytes(n) == 21 * n
+        with slab.expecting(3):
+            assert slab._slab_bytes(n) == 3 * n
+            assert slab._slab_bytes(1) == slab.MIN_SLAB
+        assert slab._slab_bytes(n) == 21 * n
+        assert slab._slab_bytes(1 << 30) == slab.MAX_SLAB
+    assert slab._slab_bytes(n) == slab.SLAB_BUCKETS * n
+    slab.release()
+    with slab.expecting(4):
+        a = slab.carve((20 << 20) // 4, torch.float32, "cpu", force=True)
+    base = a.untyped_storage()
+    assert a.numel() == 5 << 20
+    slab.release()
