@@ -748,6 +748,34 @@ def cfg5_sharded(dev, world, rank, group, steps, ncomm=None, chain_chunks=16):
     if rank == 0 and e1 is not None and e2 is not None:
         out["e1_torch_distributed"]["max_abs_err_vs_exact"] = float((e1[0] - e2[0]).abs().max())
         out["e1_torch_distributed"]["int64_bit_exact"] = bool(torch.equal(e1[1], e2[1]))
+    # the sharding decision: the same 24 slots
+    # all on ONE GPU (rank 0 generates every slot), one plain reduce launch —
+    # printed beside the fastest exact multi-GPU round of this run
+    one = None
+    if rank == 0:
+        try:
+            cl_all = make_clients(lay, list(zip(mans, prefixes)), range(n), dev)
+            a32, a64 = torch.zeros_like(o32), torch.zeros_like(o64)
+            t1, _ = timed_launches(Reducer(lay, cl_all, a32, a64), steps, 5)
+            one = {"ms": round(t1 * 1e3, 4), "GBps": round(nbytes / t1 / 1e9, 2),
+                   "bit_exact_vs_reference_digest": all(
+                       digest_of(lay, a32, a64, pf) == dig[f"feddct/{nm}/n24"]
+                       for nm, pf in zip(names, prefixes))}
+            del cl_all
+        except Exception as e:  # noqa: BLE001
+            one = {"error": repr(e)}
+    exact = {k: v["ms"] for k, v in out.items() if isinstance(v, dict) and "ms" in v
+             and v.get("bit_exact_vs_reference_digest")}
+    if one is not None:
+        out["one_gpu_all_slots"] = one
+        if exact:
+            best = min(exact, key=exact.get)
+            out["decision"] = {
+                "fastest_exact_multi_gpu": best, "multi_gpu_ms": exact[best],
+                "one_gpu_ms": one.get("ms"),
+                "rule": "slots already on one GPU: keep them there while N*B fits its HBM "
+                        "(one launch); slots trained on W GPUs: the exact sharded round, "
+                        "never a gather of (W-1)/W*N*B over xGMI (DESIGN §8)"}
     return out
 
 

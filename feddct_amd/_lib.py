@@ -50,7 +50,7 @@ FA_PLAN_TUNE_ISSUE_ALL = 0x100000
 FA_PLAN_TUNE_TGPU_NARROW = 0x200000
 FA_PLAN_TUNE_BCAST_TILES = 0x400000
 FA_PLAN_TUNE_BCAST_TABLE = 0x800000
-FA_PLAN_TUNE_BCAST_REVERSE = 0x1000000
+FA_PLAN_TUNE_ST_NT = 0x1000000
 FA_PLAN_TUNE_BCAST_XCD = 0x2000000
 FA_PLAN_TUNE_NO_BALANCE = 0x10000000
 FA_PLAN_TUNE_BCAST_R03 = 0x20000000

@@ -83,7 +83,7 @@ __global__ void div_trunc_i64_kernel(const float* __restrict__ x, float d,
 // same tile table: every tile's result range copied into every client bucket
 // (only segment elements are written, as the fused form).  A pure write
 // stream after a pure read stream: 4 % faster than writing the client buckets
-// from inside the reduce (tools/exp_bcast.py: 300.6 vs 313.2 us for the cfg2
+// from inside the reduce (tools/archive/exp_bcast.py: 300.6 vs 313.2 us for the cfg2
 // round), where the interleaved read and write streams pay bus turnarounds.
 __global__ __launch_bounds__(kBlock) void bcast_tiles_kernel(ReduceArgs args) {
   (void)args;
@@ -214,15 +214,14 @@ __global__ __launch_bounds__(kBlock) void bcast_group_kernel(ReduceArgs args, ui
 // without the tile table): bcast_group_kernel's shape — one workgroup per
 // (2048-float part, group of <= kBcastGroup clients), groups fastest — over
 // the flat bucket, so no workgroup waits on a tile-descriptor fetch; the
-// int64 bucket is one extra part.  cfg2 round (tools/exp_bcast.py, same
+// int64 bucket is one extra part.  cfg2 round (tools/archive/exp_bcast.py, same
 // box, profiles/r02_exp_bcast_flatgroups.jsonl): 308.7 us against 312.4 us
 // through the tile table (FA_PLAN_TUNE_BCAST_TABLE) and 331.7 us for r01's
 // form; one client per workgroup instead: 403-407 us.
 __global__ __launch_bounds__(kBlock) void bcast_flat_kernel(ReduceArgs args, uint32_t parts,
                                                             uint32_t groups, uint32_t gsize,
                                                             int64_t f32_numel,
-                                                            int64_t i64_numel, int reverse,
-                                                            int xcd) {
+                                                            int64_t i64_numel, int xcd) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const uint32_t nparts = parts + (i64_numel > 0 ? 1u : 0u);
@@ -231,9 +230,6 @@ __global__ __launch_bounds__(kBlock) void bcast_flat_kernel(ReduceArgs args, uin
   for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
     uint32_t p, g;
     if (!bcast_part(v, nparts, groups, xcd, &p, &g)) continue;
-    // tuning (FA_PLAN_TUNE_BCAST_REVERSE): the parts in reverse order, the
-    // reduce's last-written results first
-    if (reverse && p < parts) p = parts - 1 - p;
     const int c0 = (int)(g * gsize);
     const int c1 = min(a.n, c0 + (int)gsize);
     if (p < parts) {
@@ -559,7 +555,7 @@ __device__ __forceinline__ void tgpu_wide(KArgs& a, int64_t start, int count, fl
     f4 r = ((acc[0][u] + acc[1][u]) + acc[2][u]) + acc[3][u];
     if (!sum_only)
       r = f4{__fmul_rn(r.x, fac), __fmul_rn(r.y, fac), __fmul_rn(r.z, fac), __fmul_rn(r.w, fac)};
-    stg4<true>(a.out32 + start, vi[u], r);
+    st_out<5>(a.out32, start, vi[u], r);  // sc1: see reduce_impl.h st_out
     if (a.flags & FA_F_BCAST)
       for (int i = 0; i < n; ++i) stg4<true>(const_cast<float*>(cptr32(a, i)) + start, vi[u], r);
   }
@@ -650,7 +646,7 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
     f4 r = tgpu_outer4<S>(a, t.start, v, n);
     if (!sum_only)
       r = f4{__fmul_rn(r.x, fac), __fmul_rn(r.y, fac), __fmul_rn(r.z, fac), __fmul_rn(r.w, fac)};
-    stg4<true>(a.out32 + t.start, v, r);
+    st_out<5>(a.out32, t.start, v, r);
     if (a.flags & FA_F_BCAST)
       for (int i = 0; i < n; ++i) stg4<true>(const_cast<float*>(cptr32(a, i)) + t.start, v, r);
     return;
@@ -1064,7 +1060,7 @@ int pick_batch(int n, int vec_u, unsigned pflags) {
 // workgroups (CUs x workgroups per CU) runs ceil(T / slots) rounds, and a
 // part-filled round costs nearly a whole one while the launch is only one or
 // two rounds long — measured r03 on one fp32 tensor of T x 2048 floats
-// (tools/exp_batch_cross.py, profiles/r03_exp_batch_cross*.jsonl), N = 20,
+// (tools/archive/exp_batch_cross.py, profiles/r03_exp_batch_cross*.jsonl), N = 20,
 // 16-client kernel on 768 slots: 384 tiles 16.1 us, re-cut to 768 13.4 us;
 // 768 tiles 22.7 us; 1,024 tiles 33.5 us, on the 8-client kernel's 1,280
 // slots (one round) 28.3 us.  Past two rounds the tail is a small share and
@@ -1135,7 +1131,7 @@ int round_batch(int dev, int n, int vec_u, bool w, unsigned pflags, int ntiles) 
 }
 
 // A multi-round launch whose last round holds only r << slots tiles (r03
-// session 4, tools/exp_round_quant.py, profiles/r03_exp_round_quant.jsonl):
+// session 4, tools/archive/exp_round_quant.py, profiles/r03_exp_round_quant.jsonl):
 // those r tiles run alone, latency-bound, ~7-8 us after the last full round
 // at N = 20 — cfg2's layout plus 16 / 18 / 25 extra 2048-float tiles (r = 1
 // / 3 / 10 past 7 rounds of 768) reads 139.0 / 142.3 / 143.9 us against
@@ -1266,10 +1262,17 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
     return b4 ? launch_one<2, 4, false, false, 11>(a, ntiles, st)
               : launch_one<2, 8, false, false, 11>(a, ntiles, st);
   }
+  // cache policy (launch_u's pol): bit 0 nt loads, bit 1 nt result stores,
+  // bit 2 result stores through a buffer op with sc1.  r04 default: nt loads
+  // and sc1 result stores (pol 5) — see st_out; the tuning flags give the
+  // r01-r03 forms (nt stores: FA_PLAN_TUNE_ST_NT) and the older experiments.
   int nt = (pflags & FA_PLAN_TUNE_NO_NT) ? 0 : 3;
   if (pflags & FA_PLAN_TUNE_ST_PLAIN) nt &= ~2;
   if (pflags & FA_PLAN_TUNE_LD_PLAIN) nt &= ~1;
   if (pflags & FA_PLAN_TUNE_ST_SC1) nt |= 4;
+  if (!(pflags & (FA_PLAN_TUNE_ST_NT | FA_PLAN_TUNE_NO_NT | FA_PLAN_TUNE_ST_PLAIN |
+                  FA_PLAN_TUNE_LD_PLAIN | FA_PLAN_TUNE_ST_SC1)))
+    nt = 5;
   // weighted reductions take the mean's 16-client batches too since the
   // batch's weights are read once up front (r02 sweep, same box: weighted
   // U2xB16 140.5 us vs U2xB8 143.3 us, unweighted 143.0 us)
@@ -1492,7 +1495,7 @@ hipError_t upload_tables(fa_plan* p, const std::vector<Tile>& tiles,
     reqs.push_back(Req{u, slots, batch, host, dev, ns});
   };
   // the 16-client kernels' calls: the whole rule; the calls of N < 16 (the
-  // 8-client kernels): the tail split only (tools/exp_tail_small_n.py: N = 5
+  // 8-client kernels): the tail split only (tools/archive/exp_tail_small_n.py: N = 5
   // / 8 / 12, 1.1-2.9 us per launch; a one-round re-cut is no gain there)
   for (int deep = 0; deep < 2; ++deep)
     for (int w = 0; w < 2; ++w) {
@@ -1979,8 +1982,7 @@ hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, b
     const int64_t total = bcast_blocks((uint32_t)np, groups, xcd);
     const unsigned grid = (unsigned)std::min<int64_t>(total, 1ll << 30);
     hipLaunchKernelGGL(bcast_flat_kernel, dim3(grid), dim3(kBlock), 0, st, a, (uint32_t)parts,
-                       groups, gsize, f, i, (plan->flags & FA_PLAN_TUNE_BCAST_REVERSE) ? 1 : 0,
-                       xcd);
+                       groups, gsize, f, i, xcd);
   } else if (ntiles > 0) {
     // ntiles * groups < 2^32: n clients of ntiles 4-16 KB tiles would
     // outgrow any GPU's memory long before
@@ -2010,7 +2012,7 @@ Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) 
   Launch L{plan->d_tiles, plan->nt_dev, plan->ns_dev, plan->d_sidx, plan->vec_u, 0, 0};
   bool alt = false;
   // 1024-float tiles for unweighted N >= 64, and for the fused broadcast
-  // (tuning form) at any N (cfg2 round: 313 vs 318 us, tools/exp_bcast.py)
+  // (tuning form) at any N (cfg2 round: 313 vs 318 us, tools/archive/exp_bcast.py)
   if (plan->d_tiles_alt && !weighted &&
       (n >= 64 || ((flags & FA_F_BCAST) && (plan->flags & FA_PLAN_TUNE_FUSED_BCAST)))) {
     L.tiles = plan->d_tiles_alt;

@@ -47,7 +47,7 @@ struct NormChunk {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-// Cache policy (measured, tools/exp_prox_ab.py, profiles/r01_experiments.jsonl
+// Cache policy (measured, tools/archive/exp_prox_ab.py, profiles/r01_experiments.jsonl
 // "prox_ab"): the forward reads the two buckets with plain loads, so the
 // backward — which in a training step runs right after it (the proximal term
 // is next to the loss, the first node loss.backward() reaches) — finds them

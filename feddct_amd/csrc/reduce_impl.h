@@ -118,7 +118,7 @@ __device__ __forceinline__ float cw(KArgs& a, int i) {
 // launch), so a uniform index is one scalar load: 2-10 % faster at 300
 // clients than generic loads (2 % slower at 200, hence only from 256 on).
 // Otherwise the runtime-selecting accessor above.  Measured
-// (tools/exp_ab.py, same box, one process): compiled this way the inline
+// (tools/archive/exp_ab.py, same box, one process): compiled this way the inline
 // kernel issues each client's U loads behind a vmcnt(0) wait and runs
 // 141-146 us on the cfg2 workload; reading a.c32[i] directly lets the
 // compiler issue the whole batch's loads back to back, which is 4-6 %
@@ -228,6 +228,16 @@ __device__ __forceinline__ void st4(float* p, f4 v) {
 // Result store of a vector tile.  POL bit 2: through a buffer op with the
 // sc1 cache-policy bit (explicit aux bits: 2 = nt, 16 = sc1) instead of the
 // global nt store; the descriptor is based at the tile start (uniform).
+// r04 default (POL 5: sc1 without nt).  An sc1 store writes through and drops
+// the line from the XCD's L2; an nt store (r01-r03) keeps it there.  The
+// round's broadcast reads this result right after the reduce, and reading it
+// then was the round's back-to-back penalty: tools/roundlab.hip
+// (profiles/r04_roundlab_policy.jsonl, one box, 20 x 43.9 MB, hashed data):
+// the broadcast after a read pass whose result went out nt 168-172 us, after
+// one whose result went out sc1 (or sc0 sc1) 151-152 us, alone 149 us; the
+// read pass itself 136-138 us with sc1 result stores against 142 us nt.  The
+// r01 measurement that kept nt ("sc1 result stores 1-2 % slower") was of
+// sc1 + nt (aux 18, FA_PLAN_TUNE_ST_SC1), which keeps the penalty.
 template <int POL>
 __device__ __forceinline__ void st_out(float* out, int64_t start, uint32_t vidx, f4 v) {
   if constexpr ((POL & 4) != 0) {
@@ -521,7 +531,7 @@ __device__ __forceinline__ float inner_seq(const Src& src, int64_t e, int n) {
 // 16 KB (64 columns x 64 rows at once): the 16-client kernels are VGPR-bound
 // at 3 workgroups per CU (156-176 VGPRs), and the 8-client ones (91-126) at
 // 4-5, which a 32 KB stage capped at 4 (measured r03: tile counts of 1,280
-// ran as two rounds of 1,024, tools/exp_batch_cross.py).
+// ran as two rounds of 1,024, tools/archive/exp_batch_cross.py).
 constexpr int kStageFloats = 4096;
 struct SrcLdsCol {
   const float* stage;
@@ -686,10 +696,15 @@ template <int U, int B>
 hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, int pol, hipStream_t st) {
   // pol: bit 0 = non-temporal loads, bit 1 = non-temporal stores (default 3),
   // bit 2 = result stores with sc1 (buffer op)
-  if (deep) return w ? launch_one<U, B, true, true, 3>(a, ntiles, st)
-                     : launch_one<U, B, true, false, 3>(a, ntiles, st);
-  if (w) return pol == 3 ? launch_one<U, B, false, true, 3>(a, ntiles, st)
-                         : launch_one<U, B, false, true, 0>(a, ntiles, st);
+  if (deep) {
+    if (pol == 5) return w ? launch_one<U, B, true, true, 5>(a, ntiles, st)
+                           : launch_one<U, B, true, false, 5>(a, ntiles, st);
+    return w ? launch_one<U, B, true, true, 3>(a, ntiles, st)
+             : launch_one<U, B, true, false, 3>(a, ntiles, st);
+  }
+  if (w) return pol == 5   ? launch_one<U, B, false, true, 5>(a, ntiles, st)
+                : pol == 3 ? launch_one<U, B, false, true, 3>(a, ntiles, st)
+                           : launch_one<U, B, false, true, 0>(a, ntiles, st);
   switch (pol) {
     case 5: return launch_one<U, B, false, false, 5>(a, ntiles, st);
     case 7: return launch_one<U, B, false, false, 7>(a, ntiles, st);
@@ -709,14 +724,14 @@ int occupancy_u(bool deep, bool w) {
   hipError_t e;
   if (deep)
     e = w ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, true, true, 3>), kBlock, 0)
+                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, true, true, 5>), kBlock, 0)
           : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, true, false, 3>), kBlock, 0);
+                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, true, false, 5>), kBlock, 0);
   else
     e = w ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, false, true, 3>), kBlock, 0)
+                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, false, true, 5>), kBlock, 0)
           : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, false, false, 3>), kBlock,
+                &nb, reinterpret_cast<const void*>(reduce_kernel<U, B, false, false, 5>), kBlock,
                 0);
   return e == hipSuccess ? nb : 0;
 }

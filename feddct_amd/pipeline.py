@@ -38,7 +38,7 @@ from .partition import range_plans
 
 
 class HostPipeline:
-    # measured (tools/exp_pipeline.py, profiles/r03_exp_pipeline.jsonl):
+    # measured (tools/archive/exp_pipeline.py, profiles/r03_exp_pipeline.jsonl):
     # with the broadcast the CPU fan-out of a chunk must overlap the later
     # uploads, so the first chunk stays at half; without it only the copy
     # count and the tail matter

@@ -6,7 +6,7 @@ some MI355X boxes the headline reduce over them runs ~8 % slower than over
 the same buckets inside ONE allocation: 145.3 us against 134.2-134.8 us on
 one box, same process, same bits, whatever the stride between the buckets
 (256 B, 2 MiB, 2 MiB + 4 KiB, 2 MiB + 64 KiB + 256 B) —
-profiles/r03_exp_alloc.jsonl (tools/exp_alloc.py).  The placement of the
+profiles/r03_exp_alloc.jsonl (tools/archive/exp_alloc.py).  The placement of the
 buckets in memory, not their data or their alignment, is what the box-to-box
 spread of the headline came from (133 us on some boxes, 143-146 us on
 others).

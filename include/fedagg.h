@@ -93,7 +93,7 @@ extern "C" {
 #define FA_PLAN_TUNE_WAVE_CONTIG 32u /* tuning: each wave reads adjacent KiBs  */
 #define FA_PLAN_TUNE_ST_PLAIN 64u  /* tuning: plain (temporal) stores only     */
 #define FA_PLAN_TUNE_LD_PLAIN 128u /* tuning: plain (temporal) loads only      */
-#define FA_PLAN_TUNE_ST_SC1 0x10000u /* tuning: result stores with sc1         */
+#define FA_PLAN_TUNE_ST_SC1 0x10000u /* tuning: result stores with sc1 + nt     */
 #define FA_PLAN_TUNE_BATCH1 0x20000u /* tuning: 1 client per load batch         */
 #define FA_PLAN_TUNE_BATCH4 0x40000u /* tuning: 4 clients per load batch        */
 #define FA_PLAN_TUNE_FUSED_BCAST 0x80000u /* tuning: FA_F_BCAST inside the reduce */
@@ -104,8 +104,10 @@ extern "C" {
                                               table (client groups per tile) also
                                               on gap-padded plans, which copy
                                               their buckets flat by default    */
-#define FA_PLAN_TUNE_BCAST_REVERSE 0x1000000u /* tuning: the flat broadcast walks the
-                                                 bucket from its end            */
+#define FA_PLAN_TUNE_ST_NT 0x1000000u /* tuning: the reduce's result stores
+                                        non-temporal, as r01-r03 (default since r04:
+                                        sc1 write-through stores, see reduce_impl.h
+                                        st_out) */
 #define FA_PLAN_TUNE_BCAST_XCD 0x2000000u /* tuning: the broadcast's client groups
                                               of a part on one XCD (blocks b, b+8,
                                               ...: one source fetch) instead of on

@@ -56,7 +56,7 @@ def test_random_layouts_bit_exact(seed):
     # the others), fused into the reduce, one workgroup per tile (r01),
     # client groups per tile on every plan
     flags |= (0, _lib.FA_PLAN_TUNE_FUSED_BCAST, _lib.FA_PLAN_TUNE_BCAST_TILES,
-              _lib.FA_PLAN_TUNE_BCAST_TABLE, _lib.FA_PLAN_TUNE_BCAST_REVERSE)[seed % 5]
+              _lib.FA_PLAN_TUNE_BCAST_TABLE, _lib.FA_PLAN_TUNE_ST_NT)[seed % 5]
     plan = _lib.Plan(c["segs"], numel, c["segs64"], c["numel64"], tile_elems=c["tile"],
                      flags=flags)
     # adversarial-range values, exact small integers for the int64 keys

@@ -13,7 +13,7 @@ N = 20), one process, interleaved rounds, bits compared:
 plus this box's read-only rate over the same 20 x B bytes (read probe over
 the arena_256 allocation) and a copy of one bucket's worth x 20.
 
-    python tools/exp_alloc.py [ROUNDS] [one_tensor]  |  python tools/exp_alloc.py order
+    python tools/archive/exp_alloc.py [ROUNDS] [one_tensor]  |  python tools/archive/exp_alloc.py order
 """
 import json
 import sys
@@ -21,7 +21,7 @@ import os
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402

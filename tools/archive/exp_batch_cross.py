@@ -5,7 +5,7 @@ one (vector tiles re-cut to fill whole rounds) — on one fp32 tensor of
 T x 2048 elements, N clients, buffers rotated past the MALL, all variants
 interleaved in one process, bits compared.
 
-    python tools/exp_batch_cross.py [ROUNDS]
+    python tools/archive/exp_batch_cross.py [ROUNDS]
 """
 import json
 import math
@@ -14,7 +14,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402

@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402
@@ -43,8 +43,6 @@ def main():
                              plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_TILES)),
         "table": Reducer(lay, clients, o32, o64, flags=B,
                          plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_TABLE)),
-        "flat_reverse": Reducer(lay, clients, o32, o64, flags=B,
-                                plan=plan(0, _lib.FA_PLAN_TUNE_BCAST_REVERSE)),
         # the reduce's result stores temporal / sc1, so the broadcast that
         # follows may find its source in the caches
         "st_plain": Reducer(lay, clients, o32, o64, flags=B,

@@ -4,7 +4,7 @@ burst run faster than a long one (clock / power state), and how much of
 the spread between measurement scripts (20 vs 60 vs 200 launches) is
 that?  Each launch bracketed by its own pair of events.
 
-    python tools/exp_burst.py [BURST] [GAPS_MS,...]
+    python tools/archive/exp_burst.py [BURST] [GAPS_MS,...]
 """
 import json
 import os
@@ -13,7 +13,7 @@ import time
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402

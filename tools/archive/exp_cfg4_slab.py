@@ -8,7 +8,7 @@ Variants, one process, interleaved:
   cfg4_fresh_slab  - slab.release() first: all 20 buckets in one slab
   cfg2w_fresh_slab - the weighted headline's layout, fresh slab
 
-    python tools/exp_cfg4_slab.py [ROUNDS]
+    python tools/archive/exp_cfg4_slab.py [ROUNDS]
 """
 import json
 import os
@@ -16,7 +16,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import slab  # noqa: E402
 from feddct_amd.aggregate import client_weights  # noqa: E402

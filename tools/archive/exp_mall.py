@@ -4,7 +4,7 @@ back to back?  cfg2 (wrn16_8 C10, N = 20) with 1, 2 and 3 rotated client
 sets (footprint 0.92 / 1.84 / 2.77 GB), and the same bytes as one synthetic
 tensor of 5376 x 2048 floats, interleaved in one process, bits compared.
 
-    python tools/exp_mall.py [ROUNDS]
+    python tools/archive/exp_mall.py [ROUNDS]
 """
 import json
 import os
@@ -12,7 +12,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402

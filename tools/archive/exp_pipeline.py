@@ -4,7 +4,7 @@ tail after the last upload is the last chunk's reduce + download (+ its CPU
 fan-out with the broadcast).  cfg2 (20 wrn16_8 clients in pinned host
 memory), one process, interleaved; the serial round for reference.
 
-    python tools/exp_pipeline.py [REPS]
+    python tools/archive/exp_pipeline.py [REPS]
 """
 import json
 import os
@@ -13,7 +13,7 @@ import time
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd.layout import BucketLayout  # noqa: E402
 from feddct_amd.pipeline import HostPipeline  # noqa: E402

@@ -7,7 +7,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd.layout import BucketLayout  # noqa: E402
 from feddct_amd.workload import Reducer, load_manifest, make_clients  # noqa: E402

@@ -7,7 +7,7 @@ step jumps between k = 16 and k = 20 by more than the extra bytes, the
 quantization is the cause.  Each k runs the default plan (its tail split,
 fedagg.hip split_tail) and the plain table (FA_PLAN_TUNE_NO_BALANCE).
 
-    python tools/exp_round_quant.py [ROUNDS]
+    python tools/archive/exp_round_quant.py [ROUNDS]
 """
 import copy
 import ctypes
@@ -17,7 +17,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.aggregate import client_weights  # noqa: E402

@@ -5,7 +5,7 @@ tiles of 2048 (default), 4096 and 1024 floats — on the joint
 main + proxy bucket, rotated past the MALL, interleaved in one process.
 Every variant's output is checked against the default's bits.
 
-    python tools/exp_scalar.py [ROUNDS]
+    python tools/archive/exp_scalar.py [ROUNDS]
 """
 import json
 import os
@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402

@@ -6,7 +6,7 @@ per-tensor tiles, no scalar columns) at the same N; that flat tensor at 1/2,
 a float4 copy of the same bytes.  Buffers rotated past the MALL, every
 variant interleaved in one process.
 
-    python tools/exp_small.py [ROUNDS] [LAYOUT,...]
+    python tools/archive/exp_small.py [ROUNDS] [LAYOUT,...]
 """
 import json
 import math
@@ -16,7 +16,7 @@ import sys
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402

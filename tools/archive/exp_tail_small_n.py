@@ -4,7 +4,7 @@ N = 5 at 4.2 rounds of 1,280 slots)?  One fp32 tensor of T x 2048 floats,
 plain tile table vs the split table, both as explicit tile tables
 (fa_plan_create_from_tiles), one process, interleaved.
 
-    python tools/exp_tail_small_n.py [ROUNDS]
+    python tools/archive/exp_tail_small_n.py [ROUNDS]
 """
 import json
 import os
@@ -13,7 +13,7 @@ import sys
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402

@@ -4,7 +4,7 @@ bytes as cfg2's layout (82 fp32 keys incl. BN vectors, 16 int64) and as one
 5376 x 2048 tensor (only the 2048-element wide body), each in both orders,
 one process, interleaved, slab buckets.
 
-    python tools/exp_tgpu_gap.py [ROUNDS]
+    python tools/archive/exp_tgpu_gap.py [ROUNDS]
 """
 import json
 import os
@@ -12,7 +12,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402

@@ -5,7 +5,7 @@ workgroups per CU caps — on the FedDCT sweep layouts and cfg3, rotated past
 the MALL, interleaved in one process.  Every variant's output is checked
 against the default's bits.
 
-    python tools/exp_tune.py [ROUNDS] [LAYOUT,...]
+    python tools/archive/exp_tune.py [ROUNDS] [LAYOUT,...]
 """
 import json
 import os
@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402

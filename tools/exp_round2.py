@@ -9,6 +9,8 @@ A/B'd in ONE process, interleaved, HIP events, per layout:
                 groups of <= 10 clients, 1024-float parts) — the default
   round_u2 / round_g24 / round_u2g24 / round_xcd   r04 kernel, tuning flags
   round_r03     the r02/r03 broadcast kernels (FA_PLAN_TUNE_BCAST_R03)
+  reduce_stnt / round_stnt / round_stnt_r03   the reduce's result stores nt
+                (FA_PLAN_TUNE_ST_NT: r01-r03) instead of sc1 (r04 default)
   round_fused   FA_F_BCAST inside the reduce (FA_PLAN_TUNE_FUSED_BCAST):
                 one launch
 
@@ -53,8 +55,10 @@ VARIANTS = {
     "round_bsc1nt": (_lib.FA_F_BCAST, 0, 2),
     "round_bsc0sc1": (_lib.FA_F_BCAST, 0, 3),
     "round_bplain": (_lib.FA_F_BCAST, 0, 4),
-    "round_stsc1_bsc1": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_ST_SC1, 1),
-    "round_stsc1": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_ST_SC1, 0),
+    # r04: the reduce's result stores sc1 by default; _stnt: nt (r01-r03)
+    "reduce_stnt": (0, _lib.FA_PLAN_TUNE_ST_NT),
+    "round_stnt": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_ST_NT),
+    "round_stnt_r03": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_ST_NT | _lib.FA_PLAN_TUNE_BCAST_R03),
 }
 
 
@@ -112,7 +116,8 @@ def run_layout(tag, rounds, dev):
     for k, ts in times.items():
         ts = sorted(ts)
         med[k] = ts[len(ts) // 2]
-        nb = red_bytes if k == "reduce" else bc_bytes if k == "bcast" else red_bytes + bc_bytes
+        nb = (red_bytes if k.startswith("reduce") else bc_bytes if k == "bcast"
+              else red_bytes + bc_bytes)
         print(json.dumps({"exp": "round2", "layout": tag, "n": n, "variant": k,
                           "us_median": round(med[k], 2), "us_min": round(ts[0], 2),
                           "bytes": nb, "frac": round(nb / (med[k] * 1e-6) / 8e12, 4)}),
@@ -124,6 +129,8 @@ def run_layout(tag, rounds, dev):
     # each kernel's time inside the round: the round as two calls (reduce,
     # then the broadcast alone) with events between them, per broadcast form
     for pfl, nm in ((0, "r04"), (_lib.FA_PLAN_TUNE_BCAST_R03, "r03"),
+                    (_lib.FA_PLAN_TUNE_ST_NT, "stnt"),
+                    (_lib.FA_PLAN_TUNE_ST_NT | _lib.FA_PLAN_TUNE_BCAST_R03, "stnt_r03"),
                     (_lib.FA_PLAN_TUNE_BCAST_G24, "g24"), (_lib.FA_PLAN_TUNE_BCAST_U2, "u2")):
         if pfl not in plans:
             continue
