@@ -980,7 +980,17 @@ def next_rows(dev, steps=30):
                                          norms.data_ptr(), one.data_ptr(), 1.0, ga.data_ptr(),
                                          gb.data_ptr(), st))
     t_k, _ = timed_launches(kernels, steps * 4, 4)
+    # the same with the gradients stored sc1 (r04 A/B, fa_tune_prox_store)
+    _lib.lib.fa_tune_prox_store(1)
+    try:
+        t_k1, _ = timed_launches(kernels, steps * 4, 4)
+    finally:
+        _lib.lib.fa_tune_prox_store(0)
     del sets
+
+    def term_only():     # the term's own forward + backward (no zero_grad)
+        proximal_term(client, glob, flat_grads=True).backward()
+    t_term, _ = timed_launches(term_only, steps, 3)
     kbytes = 24 * P
     f3 = {"params": P, "step_us": round(t_ours * 1e6, 1),
           "reference_loop_step_us": round(t_ref * 1e6, 1),
@@ -988,8 +998,12 @@ def next_rows(dev, steps=30):
           "kernels_us": round(t_k * 1e6, 1),
           "kernels_GBps": round(kbytes / t_k / 1e9, 1),
           "kernels_roofline_frac": round(kbytes / t_k / 1e9 / HBM_PEAK_GBS, 4),
+          "kernels_sc1_grad_stores_us": round(t_k1 * 1e6, 1),
+          "term_fwd_bwd_us": round(t_term * 1e6, 1),
           "rel_err_vs_torch": float(abs(got.item() - want.item()) / abs(want.item())),
-          "note": "fwd+bwd per training step incl. autograd; reference = its loop on torch-ROCm"}
+          "note": "step = the client's zero_grad (as the reference's optimizer) + the term's "
+                  "fwd + bwd incl. autograd; term_fwd_bwd_us without the zero_grad; "
+                  "reference = its loop on torch-ROCm"}
     # f4: checkpoint save of the bound global model
     from feddct_amd.aggregate import server_aggregate
     server_aggregate(glob, [client])  # binds glob's arena (and client's)

@@ -66,6 +66,20 @@ __device__ __forceinline__ void st4(f4* p, f4 v) {
   if constexpr (kNtStore) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
+// The gradient stores' cache policy (r04 tuning, fa_tune_prox_store): 0 nt
+// (default), 1 sc1 — write-through, the line leaves the XCD's L2 (what the
+// reduce's result stores use since r04, reduce_impl.h st_out).
+template <int SP>
+__device__ __forceinline__ void st_grad(f4* base, int i, f4 v) {
+  if constexpr (SP == 0) {
+    st4(base + i, v);
+  } else {  // the descriptor on the uniform chunk base, the lane's offset in a VGPR
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, 16 * i, 0, 16);
+  }
+}
+thread_local int t_prox_store = 0;
 
 __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -191,7 +205,7 @@ constexpr size_t kFinLdsMax = 64 * 1024;  // the default dynamic-LDS limit
 // ACC: the gradients are added to what the buckets hold (grad += d, one
 // rounding — what autograd's AccumulateGrad does in place), for parameters
 // whose .grad are views of the buckets (prox.py's one-node backward).
-template <bool ACC, bool ACCB>
+template <bool ACC, bool ACCB, int SP = 0>
 __global__ __launch_bounds__(kBlk) void prox_grad(const NormChunk* __restrict__ chunks,
                                                   const float* __restrict__ a,
                                                   const float* __restrict__ b,
@@ -219,12 +233,12 @@ __global__ __launch_bounds__(kBlk) void prox_grad(const NormChunk* __restrict__ 
     const int v = threadIdx.x + u * kBlk;
     if (v < nv) {
       const f4 d = g * (xa[u] - xb[u]);
-      if constexpr (ACC) st4(qa + v, ld4<kNtLoadBwd>(qa + v) + d);
-      else st4(qa + v, d);
+      if constexpr (ACC) st_grad<SP>(qa, v, ld4<kNtLoadBwd>(qa + v) + d);
+      else st_grad<SP>(qa, v, d);
       if constexpr (ACCB) {
-        if (gb) st4(qb + v, ld4<kNtLoadBwd>(qb + v) - d);
+        if (gb) st_grad<SP>(qb, v, ld4<kNtLoadBwd>(qb + v) - d);
       } else {
-        if (gb) st4(qb + v, -d);
+        if (gb) st_grad<SP>(qb, v, -d);
       }
     }
   }
@@ -321,6 +335,13 @@ int fa_prox_norms(const fa_norm_plan* p, const float* a, const float* b, float* 
   return FA_OK;
 }
 
+int fa_tune_prox_store(int policy) {
+  if (policy < 0 || policy > 1) return fa::set_err(FA_E_INVAL, "fa_tune_prox_store: %d", policy);
+  const int old = t_prox_store;
+  t_prox_store = policy;
+  return old;
+}
+
 int fa_prox_grad(const fa_norm_plan* p, const float* a, const float* b, const float* norms,
                  const float* gout, float alpha, float* grad_a, float* grad_b, void* stream) {
   return fa_prox_grad_ex(p, a, b, norms, gout, alpha, grad_a, grad_b, 0, stream);
@@ -342,6 +363,9 @@ int fa_prox_grad_ex(const fa_norm_plan* p, const float* a, const float* b, const
   const bool acc_b = flags & (FA_PROX_ACCUMULATE | FA_PROX_ACCUMULATE_B);
   auto k = acc_a ? (acc_b ? prox_grad<true, true> : prox_grad<true, false>)
                  : (acc_b ? prox_grad<false, true> : prox_grad<false, false>);
+  if (t_prox_store == 1)
+    k = acc_a ? (acc_b ? prox_grad<true, true, 1> : prox_grad<true, false, 1>)
+              : (acc_b ? prox_grad<false, true, 1> : prox_grad<false, false, 1>);
   hipLaunchKernelGGL(k, dim3(p->nchunks), dim3(kBlk), 0, (hipStream_t)stream, p->d_chunks, a, b,
                      norms, gout, alpha, grad_a, grad_b);
   FA_HIP_TRY(hipGetLastError());

@@ -351,6 +351,9 @@ int fa_prox_grad_ex(const fa_norm_plan *plan, const float *a, const float *b,
 
 /* Streaming copy (bandwidth ceiling calibration for the roofline). */
 int fa_copy_f32(const float *src, float *dst, int64_t numel, void *stream);
+/* Tuning (experiments only; calling thread): the proximal-term gradient
+ * stores' policy — 0 nt (default), 1 sc1.  Returns the previous one. */
+int fa_tune_prox_store(int policy);
 /* Tuning (experiments only; calling thread): the store policy of the round
  * broadcast's flat kernel — 0 global nt (default), 1 sc1, 2 sc1 nt,
  * 3 sc0 sc1, 4 plain.  Returns the previous policy, or FA_E_INVAL. */
