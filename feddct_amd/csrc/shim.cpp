@@ -14,8 +14,14 @@
 #include <cstdint>
 #include <cstring>
 
+#include <torch/csrc/autograd/function.h>
+#include <torch/csrc/autograd/functions/utils.h>
 #include <torch/csrc/autograd/python_variable.h>
 #include <torch/csrc/autograd/variable.h>
+
+#include <memory>
+#include <stdexcept>
+#include <vector>
 
 namespace {
 
@@ -205,7 +211,202 @@ PyObject* bind_grads(PyObject*, PyObject* args) {
   Py_RETURN_NONE;
 }
 
+// ---------------------------------------------------------------------------
+// The FedProx proximal term's one-node form in C++ (r04; prox.py
+// flat_grads=True).  r03's Python autograd Function cost ~38 us per backward
+// for the node alone (the engine's device thread taking the GIL to run
+// Python; tools/prox_profile.py: a no-op Python node measured the same way)
+// plus ~14 us to apply.  Here the node is a C++ torch::autograd::Node: its
+// forward launches fa_prox_norms, its backward (run by the engine without
+// Python) binds / takes over the parameters' .grad views of the flat
+// gradient buckets and launches fa_prox_grad_ex once — the same semantics as
+// prox.py's ProximalTerm.accumulate_grads, which stays as the definition.
+// The library's entry points come in as addresses (ctypes), so this module
+// does not link libfedagg.so.
+typedef int (*prox_norms_fn)(const void*, const float*, const float*, float*, float*, void*);
+typedef int (*prox_grad_fn)(const void*, const float*, const float*, const float*, const float*,
+                            float, float*, float*, unsigned, void*);
+
+struct ProxSide {
+  std::vector<at::Tensor> params, views;  // leaf parameters and their .grad views
+  at::Tensor buf;                         // the flat gradient bucket (undefined: no side)
+  unsigned acc_flag = 0;                  // FA_PROX_ACCUMULATE_A / _B
+};
+
+struct ProxState {
+  prox_norms_fn norms_fn = nullptr;
+  prox_grad_fn grad_fn = nullptr;
+  const void* plan = nullptr;
+  const float* pa = nullptr;  // client bucket (device)
+  const float* pb = nullptr;  // global bucket (device)
+  at::Tensor norms;           // per-tensor norms, written by the forward
+  at::Tensor scratch;         // write target of the client side when it has no grads
+  ProxSide side[2];
+};
+
+// 0: every .grad is its view; 1: every .grad undefined; 2: anything else
+int side_state(const ProxSide& s) {
+  bool bound = true, none = true;
+  for (size_t i = 0; i < s.params.size(); ++i) {
+    const at::Tensor& g = s.params[i].grad();
+    if (g.defined()) none = false;
+    if (!g.defined() || g.unsafeGetTensorImpl() != s.views[i].unsafeGetTensorImpl()) bound = false;
+  }
+  return bound ? 0 : (none ? 1 : 2);
+}
+
+void bind_side(const ProxSide& s) {
+  for (size_t i = 0; i < s.params.size(); ++i) s.params[i].mutable_grad() = s.views[i];
+}
+
+struct ProxNode : public torch::autograd::Node {
+  std::shared_ptr<ProxState> st;
+  void* stream = nullptr;  // the forward's stream: the backward's too
+  torch::autograd::variable_list apply(torch::autograd::variable_list&& grads) override {
+    if (c10::GradMode::is_enabled())
+      throw std::runtime_error(
+          "feddct_amd.prox: the one-node proximal term has no double backward; use "
+          "proximal_term(..., flat_grads=False)");
+    ProxState& S = *st;
+    int state[2] = {-1, -1};
+    {
+      at::NoGradGuard ng;
+      for (int k = 0; k < 2; ++k) {
+        ProxSide& sd = S.side[k];
+        if (!sd.buf.defined()) continue;
+        int x = side_state(sd);
+        if (x == 2) {  // some .grad not bucket views: take them over, once
+          for (size_t i = 0; i < sd.params.size(); ++i) {
+            const at::Tensor& g = sd.params[i].grad();
+            if (!g.defined()) sd.views[i].zero_();
+            else if (g.unsafeGetTensorImpl() != sd.views[i].unsafeGetTensorImpl())
+              sd.views[i].copy_(g);
+          }
+          bind_side(sd);
+          x = 0;
+        }
+        state[k] = x;
+      }
+    }
+    if (state[0] < 0 && state[1] < 0) return {at::Tensor()};
+    at::Tensor gout = grads[0].to(at::kFloat).contiguous();
+    const unsigned flags = (state[0] == 0 ? S.side[0].acc_flag : 0u) |
+                           (state[1] == 0 ? S.side[1].acc_flag : 0u);
+    float* ga = S.side[0].buf.defined() ? S.side[0].buf.data_ptr<float>()
+                                        : S.scratch.data_ptr<float>();
+    float* gb = S.side[1].buf.defined() ? S.side[1].buf.data_ptr<float>() : nullptr;
+    const int rc = S.grad_fn(S.plan, S.pa, S.pb, S.norms.data_ptr<float>(),
+                             gout.data_ptr<float>(), 1.0f, ga, gb, flags, stream);
+    if (rc != 0) throw std::runtime_error("feddct_amd.prox: fa_prox_grad_ex failed");
+    for (int k = 0; k < 2; ++k)
+      if (state[k] == 1) bind_side(S.side[k]);
+    return {at::Tensor()};  // the anchor gets no gradient
+  }
+  std::string name() const override { return "FedAggProximalTermBackward"; }
+};
+
+void prox_capsule_free(PyObject* cap) {
+  delete static_cast<std::shared_ptr<ProxState>*>(
+      PyCapsule_GetPointer(cap, "feddct_amd.prox_state"));
+}
+
+bool tensor_list(PyObject* seq, std::vector<at::Tensor>* out) {
+  if (!PyTuple_Check(seq)) return false;
+  for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(seq); ++i) {
+    PyObject* t = PyTuple_GET_ITEM(seq, i);
+    if (!THPVariable_Check(t)) return false;
+    out->push_back(THPVariable_Unpack(t));
+  }
+  return true;
+}
+
+// prox_state(norms_fn, grad_fn, plan, pa, pb, norms, scratch,
+//            params_a, views_a, buf_a | None, flag_a,
+//            params_b, views_b, buf_b | None, flag_b) -> capsule
+PyObject* prox_state(PyObject*, PyObject* args) {
+  unsigned long long fn_n, fn_g, plan, pa, pb;
+  PyObject *norms, *scratch, *pa_t, *va_t, *ba, *pb_t, *vb_t, *bb;
+  unsigned int fa, fb;
+  if (!PyArg_ParseTuple(args, "KKKKKOOO!O!OIO!O!OI", &fn_n, &fn_g, &plan, &pa, &pb, &norms,
+                        &scratch, &PyTuple_Type, &pa_t, &PyTuple_Type, &va_t, &ba, &fa,
+                        &PyTuple_Type, &pb_t, &PyTuple_Type, &vb_t, &bb, &fb))
+    return nullptr;
+  if (!THPVariable_Check(norms) || !THPVariable_Check(scratch)) {
+    PyErr_SetString(PyExc_TypeError, "prox_state: norms / scratch must be tensors");
+    return nullptr;
+  }
+  auto st = std::make_shared<ProxState>();
+  st->norms_fn = reinterpret_cast<prox_norms_fn>(fn_n);
+  st->grad_fn = reinterpret_cast<prox_grad_fn>(fn_g);
+  st->plan = reinterpret_cast<const void*>(plan);
+  st->pa = reinterpret_cast<const float*>(pa);
+  st->pb = reinterpret_cast<const float*>(pb);
+  st->norms = THPVariable_Unpack(norms);
+  st->scratch = THPVariable_Unpack(scratch);
+  PyObject* pt[2] = {pa_t, pb_t};
+  PyObject* vt[2] = {va_t, vb_t};
+  PyObject* bt[2] = {ba, bb};
+  const unsigned fl[2] = {fa, fb};
+  for (int k = 0; k < 2; ++k) {
+    ProxSide& sd = st->side[k];
+    if (!tensor_list(pt[k], &sd.params) || !tensor_list(vt[k], &sd.views) ||
+        sd.params.size() != sd.views.size()) {
+      PyErr_SetString(PyExc_TypeError, "prox_state: params / views must be equal tuples of tensors");
+      return nullptr;
+    }
+    if (bt[k] != Py_None) {
+      if (!THPVariable_Check(bt[k])) {
+        PyErr_SetString(PyExc_TypeError, "prox_state: buffer must be a tensor or None");
+        return nullptr;
+      }
+      sd.buf = THPVariable_Unpack(bt[k]);
+    }
+    sd.acc_flag = fl[k];
+  }
+  return PyCapsule_New(new std::shared_ptr<ProxState>(st), "feddct_amd.prox_state",
+                       prox_capsule_free);
+}
+
+// prox_apply(state, anchor, stream) -> the term (0-dim fp32 tensor), whose
+// grad_fn is a ProxNode when the anchor requires grad and grad mode is on
+PyObject* prox_apply(PyObject*, PyObject* args) {
+  PyObject *cap, *anchor;
+  unsigned long long stream;
+  if (!PyArg_ParseTuple(args, "OOK", &cap, &anchor, &stream)) return nullptr;
+  auto* sp = static_cast<std::shared_ptr<ProxState>*>(
+      PyCapsule_GetPointer(cap, "feddct_amd.prox_state"));
+  if (!sp || !THPVariable_Check(anchor)) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "prox_apply: bad arguments");
+    return nullptr;
+  }
+  const std::shared_ptr<ProxState>& st = *sp;
+  const at::Tensor& a = THPVariable_Unpack(anchor);
+  at::Tensor total;
+  try {
+    at::NoGradGuard ng;
+    total = at::empty({}, st->norms.options());
+    if (st->norms_fn(st->plan, st->pa, st->pb, st->norms.data_ptr<float>(),
+                     total.data_ptr<float>(), reinterpret_cast<void*>(stream)) != 0) {
+      PyErr_SetString(PyExc_RuntimeError, "feddct_amd.prox: fa_prox_norms failed");
+      return nullptr;
+    }
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+  if (c10::GradMode::is_enabled() && a.requires_grad()) {
+    auto node = std::shared_ptr<ProxNode>(new ProxNode(), torch::autograd::deleteNode);
+    node->st = st;
+    node->stream = reinterpret_cast<void*>(stream);
+    node->set_next_edges(torch::autograd::collect_next_edges(a));
+    torch::autograd::set_history(total, node);
+  }
+  return THPVariable_Wrap(std::move(total));
+}
+
 PyMethodDef kMethods[] = {
+    {"prox_state", prox_state, METH_VARARGS, "the C++ one-node proximal term's bound state"},
+    {"prox_apply", prox_apply, METH_VARARGS, "the one-node proximal term (C++ autograd node)"},
     {"grad_state", grad_state, METH_VARARGS, "is every .grad its bucket view / None"},
     {"bind_grads", bind_grads, METH_VARARGS, ".grad = bucket view for every parameter"},
     {"valid_views", valid_views, METH_VARARGS, "arena validity check (see shim.cpp)"},

@@ -76,7 +76,9 @@ class _Prox(torch.autograd.Function):
 
 
 class _ProxFlat(torch.autograd.Function):
-    """The one-node form (r03): the parameters are not inputs of the graph
+    """The one-node form (r03; since r04 the definition behind the C++ node
+    csrc/shim.cpp ProxNode, which runs it without Python in the backward):
+    the parameters are not inputs of the graph
     node, so a backward is ONE node instead of this node plus an
     AccumulateGrad per parameter (200 for wrn16_8's client + global: ~0.6 ms
     of autograd bookkeeping per training step).  Its backward accumulates the
@@ -146,6 +148,24 @@ class ProximalTerm:
                           torch.empty(max(1, self.plan.nseg), dtype=torch.float32, device=dev))
         return self._flat
 
+    def _native(self):
+        """The C++ one-node form's bound state (csrc/shim.cpp ProxNode, r04):
+        the same buckets, views and flags as accumulate_grads, handed to a
+        C++ autograd node whose backward runs without Python."""
+        cap = getattr(self, "_cap", None)
+        if cap is None:
+            from . import _fa_shim
+            sides, _, norms = self._flat_state()
+            (pa, va, ba), (pb, vb, bb) = sides
+            addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+            cap = self._cap = _fa_shim.prox_state(
+                addr(_lib.lib.fa_prox_norms), addr(_lib.lib.fa_prox_grad_ex),
+                self.plan.handle.value, self.ca.ptr32, self.ga.ptr32, norms,
+                self._scratch(self.ca.device) if ba is None else norms, pa, va, ba,
+                _lib.FA_PROX_ACCUMULATE_A,
+                pb, vb, bb, _lib.FA_PROX_ACCUMULATE_B)
+        return cap
+
     def norms_forward(self) -> torch.Tensor:
         _, _, norms = self._flat_state()
         dev = self.ca.device
@@ -211,6 +231,11 @@ class ProximalTerm:
     def __call__(self, flat_grads: bool = False) -> torch.Tensor:
         if flat_grads:
             _, anchor, _ = self._flat_state()
+            from . import _fa_shim
+            if hasattr(_fa_shim, "prox_apply"):
+                dev = self.ca.device
+                return _fa_shim.prox_apply(self._native(), anchor,
+                                           torch.cuda.current_stream(dev).cuda_stream)
             return _ProxFlat.apply(self, anchor)
         return _Prox.apply(self, *self.params)
 

@@ -738,6 +738,34 @@ def test_proximal_term_flat_grads_in_a_training_loop(set_to_none):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
 
 
+def test_proximal_term_one_node_is_the_cpp_node():
+    """r04: flat_grads=True builds the C++ autograd node (shim.cpp ProxNode):
+    its backward equals the Python one-node definition, twice in a row
+    (accumulation), and a double backward raises."""
+    from feddct_amd.prox import proximal_term
+    c1, g1 = _prox_models(5)
+    c2, g2 = _prox_models(5)
+    t = proximal_term(c1, g1, flat_grads=True)
+    assert t.grad_fn is not None and "FedAggProximalTerm" in t.grad_fn.name()
+    for _ in range(2):
+        (0.3 * proximal_term(c1, g1, flat_grads=True)).backward()
+        term = c2.__dict__.setdefault("_fa_prox", {}).get(id(g2))
+        if term is None:
+            proximal_term(c2, g2)          # binds the term
+            term = c2.__dict__["_fa_prox"][id(g2)]
+        from feddct_amd.prox import _ProxFlat
+        _, anchor, _ = term._flat_state()
+        (0.3 * _ProxFlat.apply(term, anchor)).backward()
+    torch.cuda.synchronize()
+    for a, b in zip(list(c1.parameters()) + list(g1.parameters()),
+                    list(c2.parameters()) + list(g2.parameters())):
+        torch.testing.assert_close(a.grad, b.grad, rtol=0, atol=0)
+    x = proximal_term(c1, g1, flat_grads=True)
+    anchor = c1.__dict__["_fa_prox"][id(g1)]._flat_state()[1]
+    with pytest.raises(RuntimeError, match="double backward"):
+        torch.autograd.grad(x, [anchor], create_graph=True)
+
+
 def test_proximal_term_default_works_with_autograd_grad():
     """the default form is an ordinary autograd node over the
     parameters, so torch.autograd.grad(loss, params) and

@@ -51,6 +51,7 @@ VARIANTS = {
     # the broadcast's store policy (fa_tune_bcast_store): sc1 stores leave no
     # dirty lines in the XCDs' L2 at the launch's end; "_stsc1": the reduce's
     # result stores sc1 too
+    "round_g24_bsc1nt": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_BCAST_G24, 2),
     "round_bsc1": (_lib.FA_F_BCAST, 0, 1),
     "round_bsc1nt": (_lib.FA_F_BCAST, 0, 2),
     "round_bsc0sc1": (_lib.FA_F_BCAST, 0, 3),
