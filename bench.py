@@ -271,7 +271,7 @@ def pmc_traffic(n_gpus):
                           "passes (separate runs) of bench.py --kernel-only",
                 "profile_kernel_avg_us": round(d["avg_ns"] / 1e3, 2) if "avg_ns" in d else None,
                 "profile_date_utc": d.get("date_utc"), "profile_host": d.get("host"),
-                "profile_gpu": d.get("gpu"),
+                "profile_gpu": d.get("gpu"), "profile_tree": d.get("tree"),
                 "note": "measured in a separate profiler run (counters cannot be read from "
                         "inside the timed process), not in this run",
                 "traffic_over_algorithmic": round(d["hbm_bytes_per_launch"]

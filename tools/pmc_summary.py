@@ -68,6 +68,9 @@ def main():
         "date_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
         "host": os.uname().nodename,
         "gpu": (bench_line or {}).get("gpu"),
+        # the commit of the profiled tree (FA_PROFILE_TREE, set by the caller:
+        # the GPU box has no .git)
+        "tree": os.environ.get("FA_PROFILE_TREE"),
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1)

@@ -22,7 +22,8 @@ from pmc_kernels import per_kernel, rows  # noqa: E402
 
 B, N = 43888744, 20
 ALGO = {"reduce_kernel": N * B + B, "tgpu_kernel": N * B + B, "bcast_group_kernel": B + N * B,
-        "bcast_flat_kernel": B + N * B}
+        "bcast_flat_kernel": B + N * B, "bcast_flat2_kernel": B + N * B,
+        "bcast_group2_kernel": B + N * B}
 
 
 def main():
