@@ -507,7 +507,7 @@ def round_block(layout, clients, out32, out64, plan, extra, k=40):
         "write_ceiling_GBps": round(wceil, 1),
         "write_ceiling_probe": (f"fa_write_probe_f32: {n} x {numel} floats of hashed register "
                                 "values into the client buckets, the broadcast's launch shape "
-                                "(1024-float parts, groups of <= 10), best of 3 passes"),
+                                "(1024-float parts, groups of <= 24), best of 3 passes"),
     }
     if rceil:
         # the time the round's bytes take at this box's read and write ceilings

@@ -55,7 +55,7 @@ FA_PLAN_TUNE_BCAST_XCD = 0x2000000
 FA_PLAN_TUNE_NO_BALANCE = 0x10000000
 FA_PLAN_TUNE_BCAST_R03 = 0x20000000
 FA_PLAN_TUNE_BCAST_U2 = 0x40000000
-FA_PLAN_TUNE_BCAST_G24 = 0x80000000
+FA_PLAN_TUNE_BCAST_G10 = 0x80000000
 FA_ORDER_TORCH_CPU = 0
 FA_ORDER_TORCH_GPU = 1
 

@@ -56,7 +56,7 @@ FA_K_UNITS(extern)
 namespace fa_k {
 thread_local size_t t_dyn_lds = 0;  // tuning: occupancy cap through dynamic LDS
 thread_local int t_grid_cap = 0;     // tuning: persistent grid size
-thread_local int t_bcast_store = 0;  // tuning: the r04 flat broadcast's store policy
+thread_local int t_bcast_store = 2;  // the r04 flat broadcast's store policy (default sc1 nt)
 }  // namespace fa_k
 
 namespace {
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kBlock) void bcast_group2_kernel(ReduceArgs args, u
         if (i == 0 || i < cnt) {
           float* d = sptr32(a, c0 + i) + t.start;
 #pragma unroll
-          for (int u = 0; u < 2; ++u) stg4<true>(d, threadIdx.x + u * kBlock, r[u]);
+          for (int u = 0; u < 2; ++u) st_bc<2>(d, threadIdx.x + u * kBlock, r[u]);
         }
       }
       return;
@@ -1910,16 +1910,21 @@ namespace {
 // FA_PLAN_TUNE_BCAST_TABLE); r01's one-workgroup-per-tile form with
 // FA_PLAN_TUNE_BCAST_TILES (CPU-order tables only: tiles_ok).
 // r04 default: bcast_flat2_kernel / bcast_group2_kernel (scalar pointer
-// loads), client groups of <= kBcastGroupMax = 10 (FA_PLAN_TUNE_BCAST_G24:
-// <= 24, one source fetch for N <= 24), U = 1 float4 per lane per part
-// (FA_PLAN_TUNE_BCAST_U2: 2); the r02/r03 kernels with
-// FA_PLAN_TUNE_BCAST_R03.  Groups of <= 10 against <= 24 inside the cfg2
-// round, same process, seven client placements (tools/exp_round2.py,
-// tools/exp_contig.py; profiles/r04_exp_round2*.jsonl, r04_exp_contig.jsonl):
-// 283.6-308.6 vs 289.2-318.9 us, every time faster, although the <= 24 form
-// is the faster one alone (146-148 us; the r03 kernels 156 us) and fetches
-// the source once; the r03 kernels 287.6-310.5 us.
-constexpr int kBcastGroupMax = 10;
+// loads), client groups of <= kBcastGroupMax = 24 (FA_PLAN_TUNE_BCAST_G10:
+// <= 10), U = 1 float4 per lane per part (FA_PLAN_TUNE_BCAST_U2: 2),
+// destination stores sc1 nt (fa_tune_bcast_store); the r02/r03 kernels with
+// FA_PLAN_TUNE_BCAST_R03.  Measured inside the round, same process, after
+// the reduce's result stores became sc1 (tools/exp_round2.py,
+// profiles/r04_exp_round2_bcast_forms.jsonl): groups of <= 24 vs <= 10 cfg2
+// 283.7 / 282.4 vs 284.9 / 285.0 us, cfg5 (24 slots: one group vs three)
+// 350.0 vs 363.5 us, the small layouts equal; and one source fetch instead
+// of one per group (PMC: broadcast traffic 1.0012 vs 1.0486 x algorithmic,
+// profiles/r04_round_pmc_round*.json).  (Before the sc1 result stores the
+// groups of <= 24 lost inside the round, 289-319 vs 284-309 us: the source
+// they read at once was the freshly written one)  sc1 nt vs nt
+// destination stores: r110 47.3 vs 47.9 us, cfg3 79.5 vs 79.8, cfg2 / cfg5 /
+// sf32 within 0.3 %.
+constexpr int kBcastGroupMax = 24;
 extern "C++" template <int G>
 void launch_bcast2(const fa_plan* plan, ReduceArgs& a, int ntiles, uint32_t groups,
                    uint32_t gsize, int xcd, hipStream_t st) {
@@ -1953,7 +1958,7 @@ hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, b
   a.flags |= FA_F_BCAST;
   if (n <= 0) return hipSuccess;
   if (!(plan->flags & FA_PLAN_TUNE_BCAST_R03) && !(tiles_ok && (plan->flags & FA_PLAN_TUNE_BCAST_TILES))) {
-    const int gmax = (plan->flags & FA_PLAN_TUNE_BCAST_G24) ? 24 : kBcastGroupMax;
+    const int gmax = (plan->flags & FA_PLAN_TUNE_BCAST_G10) ? 10 : kBcastGroupMax;
     const uint32_t groups = (uint32_t)((n + gmax - 1) / gmax);
     const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
     const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_XCD) ? 1 : 0;

@@ -127,8 +127,8 @@ extern "C" {
                                                2048-float parts) */
 #define FA_PLAN_TUNE_BCAST_U2 0x40000000u /* tuning: the r04 broadcast with
                                               2048-float parts (default 1024) */
-#define FA_PLAN_TUNE_BCAST_G24 0x80000000u /* tuning: the r04 broadcast in client
-                                               groups of <= 24 (default <= 10) */
+#define FA_PLAN_TUNE_BCAST_G10 0x80000000u /* tuning: the r04 broadcast in client
+                                               groups of <= 10 (default <= 24) */
 /* tuning: packed scalar tiles of 64 >> c columns (c = 0..3; default 64) */
 #define FA_PLAN_TUNE_PACK(c) (((unsigned)(c) & 3u) << 26)
 /* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
@@ -355,7 +355,7 @@ int fa_copy_f32(const float *src, float *dst, int64_t numel, void *stream);
  * stores' policy — 0 nt (default), 1 sc1.  Returns the previous one. */
 int fa_tune_prox_store(int policy);
 /* Tuning (experiments only; calling thread): the store policy of the round
- * broadcast's flat kernel — 0 global nt (default), 1 sc1, 2 sc1 nt,
+ * broadcast's flat kernel — 0 global nt, 1 sc1, 2 sc1 nt (default),
  * 3 sc0 sc1, 4 plain.  Returns the previous policy, or FA_E_INVAL. */
 int fa_tune_bcast_store(int policy);
 /* Write-only streaming probe (write-bandwidth ceiling, r04): the round

@@ -838,7 +838,7 @@ def test_checkpoint_from_device_bucket(tmp_path):
 
 
 @pytest.mark.parametrize("flags", ["xcd", "cap3", "batch8", "batch16", "plain", "persist",
-                                   "wavecontig"])
+                                   "wavecontig", "st_nt", "st_sc1nt"])
 def test_tuning_flags_keep_bits(lib, flags):
     from feddct_amd.workload import make_clients
     man = load_manifest("wrnsl16_8_sf4_c10_proxy")
@@ -850,7 +850,10 @@ def test_tuning_flags_keep_bits(lib, flags):
         "xcd": lib.FA_PLAN_TUNE_XCD, "cap3": lib.FA_PLAN_TUNE_BLOCKS_PER_CU(3),
         "batch8": lib.FA_PLAN_TUNE_BATCH8, "batch16": lib.FA_PLAN_TUNE_BATCH16,
         "plain": lib.FA_PLAN_TUNE_NO_NT, "persist": lib.FA_PLAN_TUNE_PERSIST(1),
-        "wavecontig": lib.FA_PLAN_TUNE_WAVE_CONTIG}[flags]
+        "wavecontig": lib.FA_PLAN_TUNE_WAVE_CONTIG,
+        # the reduce's result stores: r01-r03's nt, and sc1 + nt (the r04
+        # default is sc1 alone, reduce_impl.h st_out)
+        "st_nt": lib.FA_PLAN_TUNE_ST_NT, "st_sc1nt": lib.FA_PLAN_TUNE_ST_SC1}[flags]
     plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
                     4096 if flags == "wavecontig" else 1024, fl)
     from feddct_amd.workload import Reducer

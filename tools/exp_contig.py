@@ -84,14 +84,14 @@ def main():
     torch.cuda.synchronize()
     plans = {pf: _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
                            flags=_lib.FA_PLAN_GAPS_ARE_PADDING | pf)
-             for pf in (0, _lib.FA_PLAN_TUNE_BCAST_G24, _lib.FA_PLAN_TUNE_BCAST_R03)}
+             for pf in (0, _lib.FA_PLAN_TUNE_BCAST_G10, _lib.FA_PLAN_TUNE_BCAST_R03)}
     fns = {}
     for tag, (cl, o32, o64) in sets.items():
         fns[(tag, "reduce")] = Reducer(lay, cl, o32, o64, plan=plans[0])
         fns[(tag, "bcast")] = Reducer(lay, cl, o32, o64, flags=_lib.FA_F_BCAST_ONLY, plan=plans[0])
         fns[(tag, "round")] = Reducer(lay, cl, o32, o64, flags=_lib.FA_F_BCAST, plan=plans[0])
-        fns[(tag, "round_g24")] = Reducer(lay, cl, o32, o64, flags=_lib.FA_F_BCAST,
-                                          plan=plans[_lib.FA_PLAN_TUNE_BCAST_G24])
+        fns[(tag, "round_g10")] = Reducer(lay, cl, o32, o64, flags=_lib.FA_F_BCAST,
+                                          plan=plans[_lib.FA_PLAN_TUNE_BCAST_G10])
         fns[(tag, "round_r03")] = Reducer(lay, cl, o32, o64, flags=_lib.FA_F_BCAST,
                                           plan=plans[_lib.FA_PLAN_TUNE_BCAST_R03])
     times = {k: [] for k in fns}

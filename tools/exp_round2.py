@@ -38,22 +38,22 @@ LAYOUTS = {
     "r110": (("resnet110sl_sf4_c100_main", "resnet110sl_sf4_c100_proxy"), 25, 4),
 }
 P = _lib.FA_PLAN_GAPS_ARE_PADDING
+DEFAULT_STORE = 2   # the broadcast's default destination stores: sc1 nt
 VARIANTS = {
     "reduce": (0, 0),
     "bcast": (_lib.FA_F_BCAST_ONLY, 0),
     "round": (_lib.FA_F_BCAST, 0),
     "round_u2": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_BCAST_U2),
-    "round_g24": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_BCAST_G24),
-    "round_u2g24": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_BCAST_U2 | _lib.FA_PLAN_TUNE_BCAST_G24),
+    "round_g10": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_BCAST_G10),
+    "round_u2g10": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_BCAST_U2 | _lib.FA_PLAN_TUNE_BCAST_G10),
     "round_xcd": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_BCAST_XCD),
     "round_r03": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_BCAST_R03),
     "round_fused": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_FUSED_BCAST),
-    # the broadcast's store policy (fa_tune_bcast_store): sc1 stores leave no
-    # dirty lines in the XCDs' L2 at the launch's end; "_stsc1": the reduce's
-    # result stores sc1 too
-    "round_g24_bsc1nt": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_BCAST_G24, 2),
+    # the broadcast's store policy (fa_tune_bcast_store; default 2 = sc1 nt):
+    # sc1 stores leave no dirty lines in the XCDs' L2 at the launch's end
+    "round_g10_bnt": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_BCAST_G10, 0),
+    "round_bnt": (_lib.FA_F_BCAST, 0, 0),
     "round_bsc1": (_lib.FA_F_BCAST, 0, 1),
-    "round_bsc1nt": (_lib.FA_F_BCAST, 0, 2),
     "round_bsc0sc1": (_lib.FA_F_BCAST, 0, 3),
     "round_bplain": (_lib.FA_F_BCAST, 0, 4),
     # r04: the reduce's result stores sc1 by default; _stnt: nt (r01-r03)
@@ -84,7 +84,7 @@ def run_layout(tag, rounds, dev):
     plans = {}
     fns = {}
     for k, v in VARIANTS.items():
-        fl, pfl, sp = (v + (0,))[:3]
+        fl, pfl, sp = (v + (DEFAULT_STORE,))[:3]
         if pfl not in plans:
             plans[pfl] = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
                                    flags=P | pfl)
@@ -113,7 +113,7 @@ def run_layout(tag, rounds, dev):
     red_bytes = lay.algorithmic_bytes(n)
     bc_bytes = (n + 1) * B
     med = {}
-    _lib.lib.fa_tune_bcast_store(0)
+    _lib.lib.fa_tune_bcast_store(DEFAULT_STORE)
     for k, ts in times.items():
         ts = sorted(ts)
         med[k] = ts[len(ts) // 2]
@@ -132,7 +132,7 @@ def run_layout(tag, rounds, dev):
     for pfl, nm in ((0, "r04"), (_lib.FA_PLAN_TUNE_BCAST_R03, "r03"),
                     (_lib.FA_PLAN_TUNE_ST_NT, "stnt"),
                     (_lib.FA_PLAN_TUNE_ST_NT | _lib.FA_PLAN_TUNE_BCAST_R03, "stnt_r03"),
-                    (_lib.FA_PLAN_TUNE_BCAST_G24, "g24"), (_lib.FA_PLAN_TUNE_BCAST_U2, "u2")):
+                    (_lib.FA_PLAN_TUNE_BCAST_G10, "g10"), (_lib.FA_PLAN_TUNE_BCAST_U2, "u2")):
         if pfl not in plans:
             continue
         rr = [Reducer(lay, cl, o32, o64, plan=plans[pfl]) for cl, o32, o64 in sets]
