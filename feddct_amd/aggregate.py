@@ -68,7 +68,7 @@ class _RoundBinding:
 
     __slots__ = ("gref", "crefs", "arenas", "gen", "dicts", "tags", "tensors", "ptrs",
                  "written", "packed", "plan", "a32", "a64", "n", "dev", "order", "weighted",
-                 "__weakref__")
+                 "native", "__weakref__")
 
     def __init__(self, engine, global_model, client_models, ga, cas, plan, a32, a64, order,
                  weighted):
@@ -111,6 +111,15 @@ class _RoundBinding:
         self.dev = cas[0].device
         self.order = order
         self.weighted = weighted
+        # the whole repeat round in one C call (_fa_shim.bound_round) when no
+        # arena packs (a packed arena copies in and out around the launches)
+        self.native = None
+        if not self.packed and self.tags is not None:
+            self.native = _fa_shim.round_state(
+                ctypes.cast(_lib.lib.fa_reduce, ctypes.c_void_p).value, plan.handle.value,
+                ctypes.addressof(a32), ctypes.addressof(a64), self.n, ga.f32.data_ptr(),
+                ga.i64.data_ptr(), self.dev.index, self.dicts, self.tags, self.tensors,
+                self.ptrs, self.written)
 
     def same_modules(self, global_model, client_models, order, weighted) -> bool:
         """The cheap half of the check: the same modules, arenas, order and
@@ -221,6 +230,22 @@ class Engine:
         rb = self._round
         if rb is None or not rb.same_modules(global_model, client_models, self.order,
                                              weights is not None):
+            return False
+        if rb.native is not None:
+            from . import _fa_shim
+            w = None
+            if weights is not None:
+                w = np.asarray(weights, np.float32).reshape(-1)
+                if w.shape[0] != rb.n:
+                    raise ValueError(f"{w.shape[0]} weights for {rb.n} clients")
+                w = w.tobytes()
+            r = _fa_shim.bound_round(rb.native, w)
+            if r == 1:
+                return True
+            if r == 0:
+                self._round = None
+            elif r < 0:
+                _lib.check(r, "fa_reduce")
             return False
         if torch.cuda.current_device() != rb.dev.index:
             return False

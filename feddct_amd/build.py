@@ -15,7 +15,8 @@ HEADERS = [os.path.join(HERE, "csrc", "common.h"), os.path.join(HERE, "csrc", "r
            os.path.join(HERE, "..", "include", "fedagg.h")]
 DEPS = SRCS + HEADERS
 OUT = os.path.join(HERE, "libfedagg.so")
-HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.environ.get("HIPCC", os.path.join(ROCM, "bin", "hipcc"))
 # test infrastructure (build_loopback, below)
 LOOP_DIR = os.path.join(HERE, "..", "tests", "loopback")
 
@@ -53,14 +54,16 @@ def build_shim(force: bool = False) -> str:
     import torch
     from torch.utils.cpp_extension import include_paths
     out = shim_path()
-    if not force and not _stale(out, [SHIM_SRC]):
+    if not force and not _stale(out, [SHIM_SRC, os.path.join(HERE, "..", "include", "fedagg.h")]):
         return out
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall",
            f"-D_GLIBCXX_USE_CXX11_ABI={abi}", *("-I" + p for p in include_paths()),
-           "-I" + sysconfig.get_paths()["include"], SHIM_SRC, "-o", out + ".tmp",
-           "-L" + tlib, "-ltorch_python", "-lc10", "-ltorch_cpu", "-Wl,-rpath," + tlib]
+           "-I" + sysconfig.get_paths()["include"], "-I" + os.path.join(ROCM, "include"),
+           "-D__HIP_PLATFORM_AMD__=1", SHIM_SRC, "-o", out + ".tmp",
+           "-L" + tlib, "-ltorch_python", "-lc10", "-lc10_hip", "-ltorch_cpu",
+           "-Wl,-rpath," + tlib]
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
     return out

@@ -465,6 +465,7 @@ def test_bound_round_fast_path_sees_every_change(change):
     server_aggregate(g, clients)
     e = A.engine()
     assert e._round is not None
+    assert e._round.native is not None   # the one-call C++ form (shim bound_round)
     calls = []
     orig = e.try_bound_round
 
@@ -507,9 +508,23 @@ def test_bound_round_fast_path_sees_every_change(change):
                     assert bits_equal(c.state_dict()[k].cpu().numpy(), want), (change, k)
         # and the round after the change is bound again
         calls.clear()
+        snap = [[(k, v.detach().cpu().numpy().copy()) for k, v in c.state_dict().items()]
+                for c in clients]
         server_aggregate(g, clients) if weights is None else A.aggregate_weighted(
             g, clients, sizes=weights)
         assert calls == [True]
+        torch.cuda.synchronize()
+        if weights is not None:
+            # the bound weighted round equals the full path on fresh modules
+            fresh = _modules(man, snap)
+            g2 = StateModule(man).to(DEV)
+            A.aggregate_weighted(g2, fresh, sizes=weights)
+            torch.cuda.synchronize()
+            for k, v in g2.state_dict().items():
+                assert bits_equal(g.state_dict()[k].cpu().numpy(), v.cpu().numpy()), k
+                for c in clients:
+                    assert bits_equal(c.state_dict()[k].cpu().numpy(), v.cpu().numpy()), k
+            del fresh, g2
     finally:
         del e.try_bound_round
     # the binding does not keep a dropped round alive

@@ -6,8 +6,10 @@ of per-phase medians in microseconds: the binding's cheap check
 (same_modules: module and arena identities), the reduce launch call (ctypes
 fa_reduce), the per-tensor check that runs while the GPU reduces
 (views_intact: dict tags + data pointers in one C call), the broadcast
-launch call, the version bumps, the wall of a whole call with its sync, and the GPU time of the round
-alone (its two launches back to back).  Usage: shim_profile.py [REPS]"""
+launch call, the version bumps (these five: the r04 Python form of the fast
+path), native_call (the same sequence as one _fa_shim.bound_round call, the
+drop-in's form), the wall of a whole drop-in call with its sync, and the GPU
+time of the round alone (its two launches back to back).  Usage: shim_profile.py [REPS]"""
 import json
 import os
 import sys
@@ -55,12 +57,20 @@ def phases(call, reps):
         for k, a, b in (("same_modules", t0, t1), ("launch_reduce", t1, t2),
                         ("views_intact", t2, t3), ("launch_bcast", t3, t4), ("bump", t4, t5)):
             ph[k].append((b - a) * 1e6)
+    # the same round as one C call (the drop-in's path since r04 session 3)
+    ph["native_call"] = []
+    for _ in range(reps if rb.native is not None else 0):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        assert _fa_shim.bound_round(rb.native, None) == 1
+        ph["native_call"].append((time.perf_counter() - t0) * 1e6)
+        torch.cuda.synchronize()
     for _ in range(reps):
         t0 = time.perf_counter()
         call()
         torch.cuda.synchronize()
         ph["wall"].append((time.perf_counter() - t0) * 1e6)
-    out = {k: round(sorted(v)[len(v) // 2], 1) for k, v in ph.items()}
+    out = {k: round(sorted(v)[len(v) // 2], 1) for k, v in ph.items() if v}
     gpu = bench._bound_round_gpu(out["wall"] * 1e-6)
     out.update(gpu)
     out["bound_tensors"] = len(rb.tensors)
