@@ -980,12 +980,12 @@ def next_rows(dev, steps=30):
                                          norms.data_ptr(), one.data_ptr(), 1.0, ga.data_ptr(),
                                          gb.data_ptr(), st))
     t_k, _ = timed_launches(kernels, steps * 4, 4)
-    # the same with the gradients stored sc1 (r04 A/B, fa_tune_prox_store)
-    _lib.lib.fa_tune_prox_store(1)
+    # the same with two chunks per forward workgroup (r04 A/B, fa_tune_prox_cpw)
+    _lib.lib.fa_tune_prox_cpw(2)
     try:
         t_k1, _ = timed_launches(kernels, steps * 4, 4)
     finally:
-        _lib.lib.fa_tune_prox_store(0)
+        _lib.lib.fa_tune_prox_cpw(0)
     del sets
 
     def term_only():     # the term's own forward + backward (no zero_grad)
@@ -998,7 +998,7 @@ def next_rows(dev, steps=30):
           "kernels_us": round(t_k * 1e6, 1),
           "kernels_GBps": round(kbytes / t_k / 1e9, 1),
           "kernels_roofline_frac": round(kbytes / t_k / 1e9 / HBM_PEAK_GBS, 4),
-          "kernels_sc1_grad_stores_us": round(t_k1 * 1e6, 1),
+          "kernels_two_chunks_per_wg_us": round(t_k1 * 1e6, 1),
           "term_fwd_bwd_us": round(t_term * 1e6, 1),
           "rel_err_vs_torch": float(abs(got.item() - want.item()) / abs(want.item())),
           "note": "step = the client's zero_grad (as the reference's optimizer) + the term's "

@@ -12,8 +12,9 @@
 // the client's and the global's parameters are views of flat buckets
 // (arena.py), so the whole term is two launches forward and one backward:
 //
-//   prox_partials : one workgroup per chunk (<= 4096 floats of ONE tensor),
-//                   sum of (a-b)^2 with 16-B loads, wave + LDS reduction;
+//   prox_partials : per chunk (<= 4096 floats of ONE tensor; one chunk per
+//                   workgroup) the sum of (a-b)^2 with 16-B loads, wave +
+//                   LDS reduction;
 //   prox_finish   : one workgroup: per tensor the chunk partials in a fixed
 //                   order -> sqrt -> norms[k]; sum of norms -> total
 //                   (deterministic: no atomics);
@@ -80,23 +81,13 @@ __device__ __forceinline__ void st_grad(f4* base, int i, f4 v) {
   }
 }
 thread_local int t_prox_store = 0;
+thread_local int t_prox_cpw = 0;  // tuning: chunks per forward workgroup (0: the default)
 
 __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 
-__device__ __forceinline__ float block_sum(float v, float* lds) {
-  v = wave_sum(v);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  if (l == 0) lds[w] = v;
-  __syncthreads();
-  float r = 0.f;
-  if (threadIdx.x == 0)
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r += lds[i];
-  __syncthreads();
-  return r;  // valid in thread 0
-}
 
 // Every lane owns kVec float4 of the chunk (lane t: vectors t, t+256, ...);
 // all of them are loaded before any arithmetic, so a workgroup keeps its
@@ -105,90 +96,34 @@ __device__ __forceinline__ float block_sum(float v, float* lds) {
 // not a multiple of 4 finishes with scalar elements.
 constexpr int kVec = kChunk / (4 * kBlk);
 
-__global__ __launch_bounds__(kBlk) void prox_partials(const NormChunk* __restrict__ chunks,
-                                                      const float* __restrict__ a,
-                                                      const float* __restrict__ b,
-                                                      float* __restrict__ partials) {
-  __shared__ float lds[kBlk / 64];
-  const NormChunk c = chunks[blockIdx.x];
-  const int nv = c.count / 4;
-  const f4* pa = reinterpret_cast<const f4*>(a + c.start);
-  const f4* pb = reinterpret_cast<const f4*>(b + c.start);
-  f4 xa[kVec], xb[kVec];
-#pragma unroll
-  for (int u = 0; u < kVec; ++u) {
-    const int v = threadIdx.x + u * kBlk;
-    const bool ok = v < nv;
-    xa[u] = ok ? ld4<kNtLoadFwd>(pa + v) : f4{0.f, 0.f, 0.f, 0.f};
-    xb[u] = ok ? ld4<kNtLoadFwd>(pb + v) : f4{0.f, 0.f, 0.f, 0.f};
-  }
-  float acc = 0.f;
-#pragma unroll
-  for (int u = 0; u < kVec; ++u) {
-    const f4 d = xa[u] - xb[u];
-    acc += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
-  }
-  for (int j = 4 * nv + threadIdx.x; j < c.count; j += kBlk) {
-    const float d = a[c.start + j] - b[c.start + j];
-    acc += d * d;
-  }
-  const float s = block_sum(acc, lds);
-  if (threadIdx.x == 0) partials[blockIdx.x] = s;
-}
-
-// One workgroup of 1024 threads.  Its latency is the point (the work is a
-// few thousand floats): the chunk partials and the tensor boundaries come in
-// with ONE round of independent loads into LDS (when they fit, else they are
-// read from global memory in the same order); then wave w sums tensors w,
-// w+16, ... (lane l: partials l, l+64, ... of the tensor, then a shuffle
-// tree) -> norms[k], and the norms are summed the same way -> total.  Fixed
-// order throughout: deterministic, no atomics.
+// The finish: per tensor the chunk partials in a fixed order -> sqrt ->
+// norms[k]; the norms summed the same way -> total.  Its latency is the point
+// (the work is a few thousand floats): the chunk partials and the tensor
+// boundaries come in with ONE round of independent loads into LDS (when they
+// fit, else they are read from global memory in the same order); then wave w
+// sums tensors w, w+W, ... (lane l: partials l, l+64, ... of the tensor, then
+// a shuffle tree) -> norms[k], and wave 0 sums the norms.  The order depends
+// on neither the wave count nor which workgroup runs it: deterministic, no
+// atomics in the arithmetic.
 constexpr int kFinBlk = 1024;
-constexpr int kFinWaves = kFinBlk / 64;
 constexpr int kFinLoads = 8;
 
-template <bool LDS>
-__global__ __launch_bounds__(kFinBlk) void prox_finish(const int* __restrict__ seg_first,
-                                                       int nseg, int nchunks,
-                                                       const float* __restrict__ partials,
-                                                       float* __restrict__ norms,
-                                                       float* __restrict__ total) {
-  // [nchunks partials][nseg + 1 boundaries][nseg norms]
-  extern __shared__ float dyn[];
+// per tensor k (wave w: k = w, w + W, ...): sqrt of its partials' sum ->
+// norms[k] (and NL[k] when NL is in LDS); then wave 0 sums NL -> total
+template <int BLK, bool NL_LDS>
+__device__ __forceinline__ void finish_compute(const float* P, const int* F, float* NL, int nseg,
+                                               float* __restrict__ norms,
+                                               float* __restrict__ total) {
+  constexpr int kWaves = BLK / 64;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const float* P = partials;
-  const int* F = seg_first;
-  float* NL = norms;  // where the norms are summed from
-  if constexpr (LDS) {
-    float* sp = dyn;
-    int* sf = reinterpret_cast<int*>(dyn + nchunks);
-    for (int base = 0; base < nchunks; base += kFinBlk * kFinLoads) {
-      float x[kFinLoads];
-#pragma unroll
-      for (int i = 0; i < kFinLoads; ++i) {
-        const int j = base + threadIdx.x + i * kFinBlk;
-        x[i] = j < nchunks ? partials[j] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < kFinLoads; ++i) {
-        const int j = base + threadIdx.x + i * kFinBlk;
-        if (j < nchunks) sp[j] = x[i];
-      }
-    }
-    for (int j = threadIdx.x; j <= nseg; j += kFinBlk) sf[j] = seg_first[j];
-    __syncthreads();
-    P = sp;
-    F = sf;
-    NL = reinterpret_cast<float*>(sf + nseg + 1);
-  }
-  for (int k = wave; k < nseg; k += kFinWaves) {
+  for (int k = wave; k < nseg; k += kWaves) {
     float sq = 0.f;
     for (int i = F[k] + lane; i < F[k + 1]; i += 64) sq += P[i];
     sq = wave_sum(sq);
     if (lane == 0) {
       const float n = sqrtf(sq);
       norms[k] = n;
-      if constexpr (LDS) NL[k] = n;
+      if constexpr (NL_LDS) NL[k] = n;
     }
   }
   __syncthreads();  // NL[] written by this workgroup's waves
@@ -200,7 +135,119 @@ __global__ __launch_bounds__(kFinBlk) void prox_finish(const int* __restrict__ s
     if (lane == 0) *total = t;
   }
 }
+
+template <int BLK, bool LDS>
+__device__ __forceinline__ void finish_body(float* dyn, const int* __restrict__ seg_first,
+                                            int nseg, int nchunks,
+                                            const float* __restrict__ partials,
+                                            float* __restrict__ norms, float* __restrict__ total) {
+  // LDS: [nchunks partials][nseg + 1 boundaries][nseg norms]
+  if constexpr (LDS) {
+    float* sp = dyn;
+    int* sf = reinterpret_cast<int*>(dyn + nchunks);
+    // the boundaries' loads issued with the first batch of partials: one
+    // round trip for both when they fit (r04)
+    const int f0 = threadIdx.x <= nseg ? seg_first[threadIdx.x] : 0;
+    for (int base = 0; base < nchunks; base += BLK * kFinLoads) {
+      float x[kFinLoads];
+#pragma unroll
+      for (int i = 0; i < kFinLoads; ++i) {
+        const int j = base + threadIdx.x + i * BLK;
+        x[i] = j < nchunks ? partials[j] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < kFinLoads; ++i) {
+        const int j = base + threadIdx.x + i * BLK;
+        if (j < nchunks) sp[j] = x[i];
+      }
+    }
+    if (threadIdx.x <= nseg) sf[threadIdx.x] = f0;
+    for (int j = threadIdx.x + BLK; j <= nseg; j += BLK) sf[j] = seg_first[j];
+    __syncthreads();
+    finish_compute<BLK, true>(sp, sf, reinterpret_cast<float*>(sf + nseg + 1), nseg, norms,
+                              total);
+  } else {
+    finish_compute<BLK, false>(partials, seg_first, norms, nseg, norms, total);
+  }
+}
+
+// The finish: one workgroup of kFinBlk threads, the partials staged in LDS
+// when they fit (else read from global memory in the same order)
+template <bool LDS>
+__global__ __launch_bounds__(kFinBlk) void prox_finish(const int* __restrict__ seg_first,
+                                                       int nseg, int nchunks,
+                                                       const float* __restrict__ partials,
+                                                       float* __restrict__ norms,
+                                                       float* __restrict__ total) {
+  extern __shared__ float dyn[];
+  finish_body<kFinBlk, LDS>(dyn, seg_first, nseg, nchunks, partials, norms, total);
+}
+
+// r04: each workgroup sums CPW consecutive chunks (each chunk's partial its
+// own, so the partials — and the norms — are the same bits for every CPW),
+// all CPW x 2 x 16 KiB loads in flight before any arithmetic.  CPW = 2 puts
+// the 2,688-chunk grid of the wrn16_8 layout in one round of resident
+// workgroups, and is slower (16.4 vs 14.7 us): default 1, the knob
+// (fa_tune_prox_cpw) for other layouts.  Tried and dropped (r04): the forward as
+// ONE launch whose last workgroup runs the finish — a returning atomic per
+// workgroup on one counter 46 us, sharded over 8 words 24 us, partials
+// tagged with a launch epoch and polled by an extra workgroup 22.6 us, an
+// agent-scope fence per workgroup 137 us — against 15 + 4.8 us for the two
+// launches.
+template <int CPW>
+__global__ __launch_bounds__(kBlk) void prox_partials(const NormChunk* __restrict__ chunks,
+                                                      int nchunks, const float* __restrict__ a,
+                                                      const float* __restrict__ b,
+                                                      float* __restrict__ partials) {
+  __shared__ float lds[CPW][kBlk / 64];
+  const int c0 = blockIdx.x * CPW;
+  NormChunk c[CPW];
+  f4 xa[CPW][kVec], xb[CPW][kVec];
+#pragma unroll
+  for (int k = 0; k < CPW; ++k) {
+    c[k] = c0 + k < nchunks ? chunks[c0 + k] : NormChunk{0, 0, 0};
+    const int nv = c[k].count / 4;
+    const f4* pa = reinterpret_cast<const f4*>(a + c[k].start);
+    const f4* pb = reinterpret_cast<const f4*>(b + c[k].start);
+#pragma unroll
+    for (int u = 0; u < kVec; ++u) {
+      const int v = threadIdx.x + u * kBlk;
+      const bool ok = v < nv;
+      xa[k][u] = ok ? ld4<kNtLoadFwd>(pa + v) : f4{0.f, 0.f, 0.f, 0.f};
+      xb[k][u] = ok ? ld4<kNtLoadFwd>(pb + v) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  float acc[CPW];
+#pragma unroll
+  for (int k = 0; k < CPW; ++k) {
+    acc[k] = 0.f;
+#pragma unroll
+    for (int u = 0; u < kVec; ++u) {
+      const f4 d = xa[k][u] - xb[k][u];
+      acc[k] += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
+    }
+    for (int j = 4 * (c[k].count / 4) + threadIdx.x; j < c[k].count; j += kBlk) {
+      const float d = a[c[k].start + j] - b[c[k].start + j];
+      acc[k] += d * d;
+    }
+  }
+  // the block sums, as block_sum: wave sums, then thread 0 adds the waves'
+#pragma unroll
+  for (int k = 0; k < CPW; ++k) acc[k] = wave_sum(acc[k]);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0)
+#pragma unroll
+    for (int k = 0; k < CPW; ++k) lds[k][w] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < CPW && c0 + (int)threadIdx.x < nchunks) {
+    float r = 0.f;
+    for (int i = 0; i < kBlk / 64; ++i) r += lds[threadIdx.x][i];
+    partials[c0 + threadIdx.x] = r;
+  }
+}
+
 constexpr size_t kFinLdsMax = 64 * 1024;  // the default dynamic-LDS limit
+constexpr int kCpwDefault = 1;  // chunks per forward workgroup (2: 16.4 vs 14.7 us, r04)
 
 // ACC: the gradients are added to what the buckets hold (grad += d, one
 // rounding — what autograd's AccumulateGrad does in place), for parameters
@@ -320,8 +367,18 @@ int fa_prox_norms(const fa_norm_plan* p, const float* a, const float* b, float* 
     return fa::set_err(FA_E_ALIGN, "fa_prox_norms: buckets must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
   if (p->nchunks > 0) {
-    hipLaunchKernelGGL(prox_partials, dim3(p->nchunks), dim3(kBlk), 0, st, p->d_chunks, a, b,
-                       p->d_partials);
+    const int cpw = t_prox_cpw > 0 ? t_prox_cpw : kCpwDefault;
+    const unsigned grid = (unsigned)((p->nchunks + cpw - 1) / cpw);
+    switch (cpw) {
+      case 1: hipLaunchKernelGGL(prox_partials<1>, dim3(grid), dim3(kBlk), 0, st, p->d_chunks,
+                                 p->nchunks, a, b, p->d_partials); break;
+      case 3: hipLaunchKernelGGL(prox_partials<3>, dim3(grid), dim3(kBlk), 0, st, p->d_chunks,
+                                 p->nchunks, a, b, p->d_partials); break;
+      case 4: hipLaunchKernelGGL(prox_partials<4>, dim3(grid), dim3(kBlk), 0, st, p->d_chunks,
+                                 p->nchunks, a, b, p->d_partials); break;
+      default: hipLaunchKernelGGL(prox_partials<2>, dim3(grid), dim3(kBlk), 0, st, p->d_chunks,
+                                  p->nchunks, a, b, p->d_partials); break;
+    }
     FA_HIP_TRY(hipGetLastError());
   }
   const size_t lds = (size_t)(p->nchunks + 2 * p->nseg + 1) * 4;
@@ -333,6 +390,13 @@ int fa_prox_norms(const fa_norm_plan* p, const float* a, const float* b, float* 
                        p->nseg, p->nchunks, p->d_partials, norms, total);
   FA_HIP_TRY(hipGetLastError());
   return FA_OK;
+}
+
+int fa_tune_prox_cpw(int cpw) {
+  if (cpw < 0 || cpw > 4) return fa::set_err(FA_E_INVAL, "fa_tune_prox_cpw: %d", cpw);
+  const int old = t_prox_cpw;
+  t_prox_cpw = cpw;
+  return old;
 }
 
 int fa_tune_prox_store(int policy) {

@@ -354,6 +354,10 @@ int fa_copy_f32(const float *src, float *dst, int64_t numel, void *stream);
 /* Tuning (experiments only; calling thread): the proximal-term gradient
  * stores' policy — 0 nt (default), 1 sc1.  Returns the previous one. */
 int fa_tune_prox_store(int policy);
+/* Tuning (experiments only; calling thread): chunks of 4096 floats per
+ * workgroup of fa_prox_norms' partial-sum launch, 1..4 (0: the default, 2);
+ * the result bits do not depend on it.  Returns the previous setting. */
+int fa_tune_prox_cpw(int cpw);
 /* Tuning (experiments only; calling thread): the store policy of the round
  * broadcast's flat kernel — 0 global nt, 1 sc1, 2 sc1 nt (default),
  * 3 sc0 sc1, 4 plain.  Returns the previous policy, or FA_E_INVAL. */

@@ -111,3 +111,35 @@ def test_interleaved_plans():
         torch.testing.assert_close(n0, want, rtol=1e-5, atol=0)
         for n, t in outs[k][1:]:
             assert torch.equal(n, n0) and torch.equal(t, t0)
+
+
+@pytest.mark.parametrize("cpw", [2, 3, 4])
+def test_prox_chunks_per_workgroup_same_bits(big, cpw):
+    """r04: the forward's chunks-per-workgroup setting (default 1) changes
+    the launch shape, not the partials: norms and total are the same bits,
+    launch after launch."""
+    from feddct_amd import _lib
+    segs, numel, a, b = big
+    ref, _, _ = _run(segs, numel, a, b)
+    old = _lib.lib.fa_tune_prox_cpw(cpw)
+    try:
+        outs, _, _ = _run(segs, numel, a, b, reps=2)
+    finally:
+        _lib.lib.fa_tune_prox_cpw(old)
+    for n, t in outs:
+        assert torch.equal(n, ref[0][0]) and torch.equal(t, ref[0][1])
+
+
+def test_prox_many_chunks():
+    """4,200 chunks (more partials than the finish stages in one load batch):
+    still torch's norms, repeated launches identical."""
+    numel = 4200 * 4096
+    cut = np.linspace(0, numel, 9).astype(np.int64) // 64 * 64
+    segs = np.stack([cut[:-1], cut[1:] - cut[:-1]], 1)
+    g = torch.Generator(device=DEV).manual_seed(13)
+    a = torch.randn(numel, device=DEV, generator=g)
+    b = torch.randn(numel, device=DEV, generator=g)
+    want = torch.stack([(a[o:o + m] - b[o:o + m]).norm(2) for o, m in segs])
+    outs, _, _ = _run(segs, numel, a, b, reps=2)
+    torch.testing.assert_close(outs[0][0], want, rtol=1e-5, atol=0)
+    assert torch.equal(outs[1][0], outs[0][0])
