@@ -281,4 +281,5 @@ def get_arena(module: torch.nn.Module, layout: BucketLayout) -> ModuleArena:
         return a
     a = ModuleArena(module, layout)
     object.__setattr__(module, "_fa_arena", a)
+    _bump()   # a (re)bound arena ends any round bound over the old one
     return a

@@ -533,6 +533,63 @@ def test_bound_round_fast_path_sees_every_change(change):
     assert e._round is None
 
 
+@pytest.mark.parametrize("change", ["none", "inplace", "swap_order", "other_object",
+                                    "new_param"])
+def test_split_bound_round_fast_path(change):
+    """r04: a repeat FedDCT / SplitFed call (server_aggregate_split) on the
+    very objects of the last joint round takes the bound round without its
+    pair lookups (_RoundBinding.split_ids, one identity check in C); any other
+    objects, order or registration take the full path, and every round equals
+    the reference's arithmetic on both halves."""
+    from feddct_amd import aggregate as A
+    from feddct_amd.feddct import server_aggregate
+    mm = {"keys": [{"key": "w", "shape": [1000], "dtype": "float32"},
+                   {"key": "b", "shape": [7], "dtype": "float32"},
+                   {"key": "n", "shape": [], "dtype": "int64"}]}
+    pm = {"keys": [{"key": "v", "shape": [300], "dtype": "float32"},
+                   {"key": "m", "shape": [], "dtype": "int64"}]}
+    n = 5
+    ms = _modules(mm, [synth.gen_state(mm, i, synth.MODE_ADVERSARIAL) for i in range(n)])
+    ps = _modules(pm, [synth.gen_state(pm, 100 + i, synth.MODE_ADVERSARIAL) for i in range(n)])
+    gm, gp = StateModule(mm).to(DEV), StateModule(pm).to(DEV)
+    server_aggregate(gm, gp, ms, ps)
+    e = A.engine()
+    assert e._round is not None and e._round.split_ids is not None
+    calls = []
+    orig = e._run_bound
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        calls.append(r)
+        return r
+    e._run_bound = spy
+    try:
+        with torch.no_grad():
+            for i, c in enumerate(ms):
+                c.w.mul_(float(i + 2))
+        if change == "swap_order":
+            ms, ps = [ms[1], ms[0]] + ms[2:], [ps[1], ps[0]] + ps[2:]
+        elif change == "other_object":
+            ms = ms[:4] + _modules(mm, [synth.gen_state(mm, 50, synth.MODE_ADVERSARIAL)])
+        elif change == "new_param":
+            ms[3].b = torch.nn.Parameter(ms[3].b.detach().clone() - 2)
+        snaps = [[[(k, v.detach().cpu().numpy().copy()) for k, v in c.state_dict().items()]
+                  for c in cl] for cl in (ms, ps)]
+        server_aggregate(gm, gp, ms, ps)
+        torch.cuda.synchronize()
+        assert (bool(calls) and calls[0]) == (change in ("none", "inplace")), (change, calls)
+        for g, cl, snap in ((gm, ms, snaps[0]), (gp, ps, snaps[1])):
+            for k, want in O.aggregate_state(snap):
+                assert bits_equal(g.state_dict()[k].cpu().numpy(), want), (change, k)
+                for c in cl:
+                    assert bits_equal(c.state_dict()[k].cpu().numpy(), want), (change, k)
+        calls.clear()
+        server_aggregate(gm, gp, ms, ps)
+        assert calls == [True]
+    finally:
+        del e._run_bound
+
+
 def test_shim_errors_like_reference():
     from feddct_amd.fedavg import server_aggregate
     man = {"keys": [{"key": "w", "shape": [10], "dtype": "float32"}]}
