@@ -520,6 +520,25 @@ def round_block(layout, clients, out32, out64, plan, extra, k=40):
             "round_vs_copy": round((red_bytes + bc_bytes) / t_round / 1e9
                                    / extra["copy_ceiling_GBps"], 4),
             "note": "ceiling time = reads at read_ceiling_GBps + writes at write_ceiling_GBps"}
+    # the round's PMC traffic per launch, from its committed profiler run
+    # (tools/gpu_round_pmc.sh -> profiles/round_pmc.json; separate passes, as
+    # roofline.traffic)
+    path = os.path.join(ROOT, "profiles", "round_pmc.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        kt = {}
+        for k in d.get("kernels", []):
+            tot = k["fetch_bytes_x2"] + k["write_bytes"]
+            kind = "reduce" if "reduce_kernel" in k["kernel"] else "bcast"
+            kt[kind] = {"hbm_bytes": int(tot), "over_algorithmic":
+                        round(tot / k["algorithmic_bytes"], 4), "kernel": k["kernel"][:60]}
+        out["traffic_pmc"] = {**kt, "source": "profiles/round_pmc.json: rocprofv3 --pmc "
+                              "FETCH_SIZE (x2, gfx950) / WRITE_SIZE passes of "
+                              "tools/round_prof.py round (separate runs)",
+                              "profile_tree": d.get("tree")}
+    except Exception:
+        pass
     extra["write_ceiling_GBps"] = out["write_ceiling_GBps"]
     return out
 
