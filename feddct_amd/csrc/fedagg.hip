@@ -538,7 +538,7 @@ __device__ __forceinline__ void tgpu_wide(KArgs& a, int64_t start, int count, fl
     for (int b = 0; b < B; ++b) {
       if (b < nb) {
         const float* p = cptr32(a, b0 + b) + start;
-#pragma unroll
+  #pragma unroll
         for (int u = 0; u < U; ++u)
           x[b][u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
       }
@@ -1637,6 +1637,70 @@ int fa_torch_gpu_config(int n, int64_t m, int* stride) {
   return 1;
 }
 
+namespace {
+// Resident workgroups of tgpu_kernel<0> (the S = 1 group's launch) on `dev`,
+// queried once per process (0: unknown).
+int tgpu_slots(int dev) {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int occ = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tgpu_kernel<0>, kBlock, 0) !=
+      hipSuccess)
+    occ = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 0;
+  return cache[dev] = occ > 0 && cus > 0 ? occ * cus : 0;
+}
+
+// The S = 1 group's tail round (r04; the default plan's split_tail, §4.3 of
+// DESIGN.md): its scalar and inner tiles first; and when its T tiles spill
+// 0 < r <= 0.44 slots past k - 1 full rounds, the last slots - r wide tiles
+// are halved (64-element lines), so the table fills exactly k rounds with a
+// last round of half tiles instead of r tiles running alone.  cfg2 at N = 20: ~5,400 tiles on
+// 768 slots = 7.03 rounds.  Per-column arithmetic: the bits never change.
+void tgpu_split_tail(std::vector<Tile>* t, std::vector<float>* fac, int lo[6], int slots) {
+  const int64_t T = lo[1] - lo[0];
+  const int64_t k = slots > 0 ? (T + slots - 1) / slots : 0;
+  const int64_t r = T - (k - 1) * slots;
+  // m: the wide tiles to halve (0: none; the group is still reordered so
+  // its scalar and inner tiles — the int64 keys' one-wave latency chains —
+  // run in the first round, as the default plan places its scalar tiles)
+  const int64_t m = (k > 1 && r > 0 && r * 100 <= kTailMaxPct * (int64_t)slots) ? slots - r : 0;
+  std::vector<Tile> nw, wd;
+  std::vector<float> fnw, fwd;
+  for (int64_t i = lo[0]; i < lo[1]; ++i) {
+    const bool w = ((*t)[i].kind & 0xFF) == K_F32_TGPU_W;
+    (w ? wd : nw).push_back((*t)[i]);
+    (w ? fwd : fnw).push_back((*fac)[i]);
+  }
+  std::vector<Tile> g = nw;
+  std::vector<float> f = fnw;
+  const size_t first = (int64_t)wd.size() < m ? wd.size() : wd.size() - (size_t)m;
+  for (size_t j = 0; j < wd.size(); ++j) {
+    const Tile& x = wd[j];
+    const int64_t h = ((int64_t)x.count / 2) & ~(int64_t)63;
+    if (j < first || h < 64) {
+      g.push_back(x);
+      f.push_back(fwd[j]);
+      continue;
+    }
+    g.push_back(Tile{x.start, (int32_t)h, x.kind});
+    g.push_back(Tile{x.start + h, (int32_t)(x.count - h), x.kind});
+    f.push_back(fwd[j]);
+    f.push_back(fwd[j]);
+  }
+  const int add = (int)(g.size() - (size_t)T);
+  g.insert(g.end(), t->begin() + lo[1], t->end());
+  f.insert(f.end(), fac->begin() + lo[1], fac->end());
+  t->swap(g);
+  fac->swap(f);
+  for (int i = 1; i < 6; ++i) lo[i] += add;
+}
+}  // namespace
+
 int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_seg* seg64,
                          int nseg64, int64_t i64_numel, int n, int order, unsigned flags,
                          fa_plan** out) {
@@ -1763,6 +1827,10 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
     int lo[6] = {0, 0, 0, 0, 0, 0};
     for (size_t i = 0; i < ord.size(); ++i) lo[grp[ord[i]] + 1]++;
     for (int g = 0; g < 5; ++g) lo[g + 1] += lo[g];
+    if (!(flags & FA_PLAN_TUNE_NO_BALANCE)) {
+      int dev = 0;
+      if (hipGetDevice(&dev) == hipSuccess) tgpu_split_tail(&t, &fac, lo, tgpu_slots(dev));
+    }
     order_groups_tmp.assign(lo, lo + 6);
   }
   fa_plan* p = new fa_plan();

@@ -1,8 +1,9 @@
 """Launch time of the torch-GPU-order plan (FA_ORDER_TORCH_GPU) on the cfg2,
 cfg3 and cfg5 one-GPU workloads, with bit-exactness against torch's own
 cuda stack(...).mean(0) of every key (bench.torch_gpu_order_mode).  Each
-workload is timed with the default tiles and with FA_PLAN_TUNE_TGPU_NARROW
-(the r02 1024-element form), alternating, ``reps`` times each.
+workload is timed with the default tiles, without the S = 1 group's tail
+split (FA_PLAN_TUNE_NO_BALANCE, r04) and with FA_PLAN_TUNE_TGPU_NARROW (the
+r02 1024-element form), alternating, ``reps`` times each.
 
     python tools/tgpu_speed.py [reps]
 """
@@ -20,6 +21,7 @@ from feddct_amd.layout import BucketLayout  # noqa: E402
 from feddct_amd.workload import joint_manifest, load_manifest, make_clients  # noqa: E402
 
 FORMS = {"wide": _lib.FA_PLAN_GAPS_ARE_PADDING,
+         "wide_no_tail_split": _lib.FA_PLAN_GAPS_ARE_PADDING | _lib.FA_PLAN_TUNE_NO_BALANCE,
          "narrow": _lib.FA_PLAN_GAPS_ARE_PADDING | _lib.FA_PLAN_TUNE_TGPU_NARROW}
 
 
@@ -34,7 +36,10 @@ def measure(name, lay, cl, reps):
     nb = lay.algorithmic_bytes(len(cl))
     for k in FORMS:
         best = min(res[k])
-        print(json.dumps({"workload": name, "form": k, "us": res[k], "best_us": best,
+        p = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
+                      order=_lib.FA_ORDER_TORCH_GPU, n=len(cl), flags=FORMS[k])
+        print(json.dumps({"workload": name, "form": k, "ntiles": p.info["ntiles"],
+                          "us": res[k], "best_us": best,
                           "GBps": round(nb / best / 1e3, 1),
                           "bit_exact_vs_torch_cuda_mean": exact[k]}), flush=True)
 
