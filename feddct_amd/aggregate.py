@@ -59,12 +59,14 @@ class _RoundBinding:
     global and client modules, their arenas, plan, pointer arrays, and ONE
     flattened validity check over every bound tensor.  A repeat call on the
     same modules re-checks only (a) that no module anywhere registered a
-    parameter, buffer or submodule since (arena._STRUCT_GEN), (b) that each
-    module still carries the same arena, and (c) in one C call
-    (_fa_shim.valid_tagged): every parameter/buffer dict's PEP 509 version
-    tag — unchanged tag, unchanged slots — and every bound tensor's data
-    pointer (a `.data` swap).  Anything else takes the full path, which
-    re-binds what changed and records a new binding."""
+    parameter, buffer or submodule, and no arena was (re)bound, since
+    (arena._STRUCT_GEN), (b) that the caller passed the very objects bound
+    (one C call by identity, _fa_shim.src_match), and (c) in one C call
+    (_fa_shim.valid_tagged, or inside _fa_shim.bound_round): every
+    parameter/buffer dict's PEP 509 version tag — unchanged tag, unchanged
+    slots — and every bound tensor's data pointer (a `.data` swap).
+    Anything else takes the full path, which re-binds what changed and
+    records a new binding."""
 
     __slots__ = ("gref", "crefs", "arenas", "gen", "dicts", "tags", "tensors", "ptrs",
                  "written", "packed", "plan", "a32", "a64", "n", "dev", "order", "weighted",
