@@ -56,6 +56,10 @@ VARIANTS = {
     "round_bsc1": (_lib.FA_F_BCAST, 0, 1),
     "round_bsc0sc1": (_lib.FA_F_BCAST, 0, 3),
     "round_bplain": (_lib.FA_F_BCAST, 0, 4),
+    # the whole batch's loads back to back (FA_PLAN_TUNE_ISSUE_ALL) instead
+    # of each client's behind the previous one's
+    "reduce_issue_all": (0, _lib.FA_PLAN_TUNE_ISSUE_ALL),
+    "round_issue_all": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_ISSUE_ALL),
     # r04: the reduce's result stores sc1 by default; _stnt: nt (r01-r03)
     "reduce_stnt": (0, _lib.FA_PLAN_TUNE_ST_NT),
     "round_stnt": (_lib.FA_F_BCAST, _lib.FA_PLAN_TUNE_ST_NT),
@@ -83,7 +87,10 @@ def run_layout(tag, rounds, dev):
         tag = tag + ":" + where
     plans = {}
     fns = {}
+    sel = [x for x in os.environ.get("VARIANTS", "").split(",") if x]
     for k, v in VARIANTS.items():
+        if sel and k not in sel:
+            continue
         fl, pfl, sp = (v + (DEFAULT_STORE,))[:3]
         if pfl not in plans:
             plans[pfl] = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
@@ -123,10 +130,14 @@ def run_layout(tag, rounds, dev):
                           "us_median": round(med[k], 2), "us_min": round(ts[0], 2),
                           "bytes": nb, "frac": round(nb / (med[k] * 1e-6) / 8e12, 4)}),
               flush=True)
-    print(json.dumps({"exp": "round2_summary", "layout": tag,
-                      "round_over_sum": round(med["round"] / (med["reduce"] + med["bcast"]), 4),
-                      "fused_over_round": round(med["round_fused"] / med["round"], 4)}),
-          flush=True)
+    if all(k in med for k in ("round", "reduce", "bcast", "round_fused")):
+        print(json.dumps({"exp": "round2_summary", "layout": tag,
+                          "round_over_sum": round(med["round"] / (med["reduce"] + med["bcast"]),
+                                                  4),
+                          "fused_over_round": round(med["round_fused"] / med["round"], 4)}),
+              flush=True)
+    if sel:
+        return
     # each kernel's time inside the round: the round as two calls (reduce,
     # then the broadcast alone) with events between them, per broadcast form
     for pfl, nm in ((0, "r04"), (_lib.FA_PLAN_TUNE_BCAST_R03, "r03"),

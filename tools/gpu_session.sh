@@ -14,7 +14,7 @@
 #   profile           kernel trace + FETCH/WRITE passes of the headline (gpu_profile.sh)
 #   round_pmc         the same for the round and the torch-GPU-order reduce
 #   prof=<tool>[:arg] kernel trace of python3 tools/<tool>.py <arg>
-#   run=<tool>[:arg]  python3 tools/<tool>.py <arg>     -> gpurun_out/<tool>.jsonl
+#   run=<tool>[:args] python3 tools/<tool>.py <args> (commas -> spaces) -> gpurun_out/<tool>.jsonl
 #   multi             bench.py's N>1 path over RCCL with one rank (multi_rehearsal.sh)
 #   n2                two-rank gloo rehearsal of bench.py --gpus 2 on one GPU
 set -o pipefail
@@ -40,7 +40,7 @@ step() {
               -o run -- python3 "tools/$t.py" $a > "gpurun_out/prof_$t.jsonl" \
               2> "gpurun_out/prof_$t.err" ;;
     run=*) local t="${arg%%:*}" a=""; [[ "$arg" == *:* ]] && a="${arg#*:}"
-           timeout -k 10 600 python3 "tools/$t.py" $a > "gpurun_out/$t.jsonl" \
+           timeout -k 10 600 python3 "tools/$t.py" ${a//,/ } > "gpurun_out/$t.jsonl" \
              2> "gpurun_out/$t.err" ;;
     multi) bash tools/multi_rehearsal.sh > gpurun_out/multi_rehearsal.log 2>&1 ;;
     n2) FA_BENCH_STACK_DUMP_S=150 timeout -k 10 500 python3 -m torch.distributed.run \
