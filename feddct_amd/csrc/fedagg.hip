@@ -270,7 +270,7 @@ __global__ __launch_bounds__(kBlock) void bcast_flat_kernel(ReduceArgs args, uin
 // template bound, the host's group size `gsize` <= G.  The int64 bucket is
 // one more part.
 // Store policy of the broadcast's destination stores (tuning,
-// fa_tune_bcast_store): 0 global nt (default), 1 sc1, 2 sc1 nt, 3 sc0 sc1
+// fa_tune_bcast_store): 0 global nt, 1 sc1, 2 sc1 nt (default), 3 sc0 sc1
 // (buffer stores with those cache-policy bits: sc1 writes through and drops
 // the line from the XCD's L2, so the launch ends with no dirty lines to write
 // back), 4 plain.
