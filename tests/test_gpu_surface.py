@@ -7,7 +7,6 @@ back in each client's own dtype.  Every case is compared bit for bit with
 the reference loop restated on CPU torch (oracle/torch_mirror.py)."""
 import copy
 
-import numpy as np
 import pytest
 import torch
 

@@ -15,7 +15,7 @@ import torch
 from conftest import load_manifest
 from feddct_amd import synth
 from feddct_amd.layout import BucketLayout
-from helpers import bits_equal, buckets_to_state, states_to_buckets
+from helpers import bits_equal, states_to_buckets
 from oracle import torch_gpu_order as G
 
 pytestmark = pytest.mark.gpu
