@@ -393,3 +393,46 @@ def test_dropin_with_gpu_order_matches_reference_loop_on_gpu(n):
                            else g.state_dict()[k],
                            v.view(torch.int32) if v.dtype == torch.float32 else v), k
         assert torch.equal(mods[-1].state_dict()[k], ref_c[-1].state_dict()[k]), k
+
+
+def test_order_switch_between_repeat_calls():
+    """r04: a repeat call on the same modules after set_summation_order()
+    changed the order must not take the bound round of the other order:
+    CPU order, GPU order, CPU order again — each round equals that order's
+    reference (the reference loop on host copies / on GPU modules)."""
+    import copy
+    import feddct_amd
+    from feddct_amd import aggregate as A
+    from feddct_amd.fedavg import server_aggregate
+    from helpers import StateModule
+    from oracle.torch_mirror import reference_loop
+    man = {"keys": [{"key": "w", "shape": [40, 33], "dtype": "float32"},
+                    {"key": "b", "shape": [17], "dtype": "float32"},
+                    {"key": "n", "shape": [], "dtype": "int64"}]}
+    n = 6
+    mods = [StateModule(man).load_numpy(synth.gen_state(man, i, synth.MODE_ADVERSARIAL)).to(DEV)
+            for i in range(n)]
+    g = StateModule(man).to(DEV)
+    try:
+        for step, order in enumerate(("torch_cpu", "torch_gpu", "torch_cpu", "torch_cpu")):
+            with torch.no_grad():   # new client values every round
+                for i, m in enumerate(mods):
+                    m.w.add_(float(step + i) * 0.125)
+            feddct_amd.set_summation_order(order)
+            if order == "torch_gpu":   # the reference loop on the GPU modules
+                ref_g, ref_c = StateModule(man).to(DEV), [copy.deepcopy(m) for m in mods]
+            else:                      # the reference loop on host copies (CPU order)
+                ref_g = StateModule(man)
+                ref_c = [copy.deepcopy(m).cpu() for m in mods]
+            reference_loop(ref_g, ref_c)
+            bound_before = A.engine()._round is not None
+            server_aggregate(g, mods)
+            torch.cuda.synchronize()
+            for k, v in ref_g.state_dict().items():
+                got = g.state_dict()[k].cpu()
+                want = v.cpu()
+                if want.dtype == torch.float32:
+                    got, want = got.view(torch.int32), want.view(torch.int32)
+                assert torch.equal(got, want), (step, order, k, bound_before)
+    finally:
+        feddct_amd.set_summation_order("torch_cpu")

@@ -39,3 +39,23 @@ def test_bind_grads_refuses_mismatched_views():
     ps, buf, _ = _params()
     with pytest.raises(ValueError):
         _fa_shim.bind_grads(ps, tuple(buf[:12] for _ in ps))
+
+
+def test_src_match_is_an_identity_check():
+    """_fa_shim.src_match (the bound round's module check, r04): the objects
+    passed — single objects, or lists / tuples taken item by item — are
+    exactly the ones whose ids were recorded, in order and in number."""
+    from array import array
+    from feddct_amd import _fa_shim
+    g, a, b, c = object(), object(), object(), object()
+    ids = array("Q", [id(g), id(a), id(b)]).tobytes()
+    assert _fa_shim.src_match(ids, g, [a, b])
+    assert _fa_shim.src_match(ids, g, (a, b))
+    assert _fa_shim.src_match(ids, g, a, b)
+    assert not _fa_shim.src_match(ids, g, [b, a])        # order
+    assert not _fa_shim.src_match(ids, g, [a, b, c])     # one more
+    assert not _fa_shim.src_match(ids, g, [a])           # one fewer
+    assert not _fa_shim.src_match(ids, c, [a, b])        # another object
+    assert _fa_shim.src_match(array("Q").tobytes())      # nothing recorded, nothing passed
+    with pytest.raises(TypeError):
+        _fa_shim.src_match("not bytes", g)
