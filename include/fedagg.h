@@ -355,7 +355,7 @@ int fa_copy_f32(const float *src, float *dst, int64_t numel, void *stream);
  * stores' policy — 0 nt (default), 1 sc1.  Returns the previous one. */
 int fa_tune_prox_store(int policy);
 /* Tuning (experiments only; calling thread): chunks of 4096 floats per
- * workgroup of fa_prox_norms' partial-sum launch, 1..4 (0: the default, 2);
+ * workgroup of fa_prox_norms' partial-sum launch, 1..4 (0: the default, 1);
  * the result bits do not depend on it.  Returns the previous setting. */
 int fa_tune_prox_cpw(int cpw);
 /* Tuning (experiments only; calling thread): the store policy of the round
