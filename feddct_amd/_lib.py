@@ -80,7 +80,7 @@ EXPORTS = [
     "fa_synth_fill_f32", "fa_synth_fill_i64", "fa_copy_f32",
     "fa_norm_plan_create", "fa_norm_plan_destroy", "fa_prox_norms", "fa_prox_grad",
     "fa_prox_grad_ex",
-    "fa_read_probe_f32", "fa_write_probe_f32", "fa_tune_bcast_store", "fa_tune_prox_store", "fa_tune_prox_cpw", "fa_chain_levels", "fa_reduce_chain", "fa_torch_gpu_config",
+    "fa_read_probe_f32", "fa_write_probe_f32", "fa_tune_bcast_store", "fa_tune_prox_store", "fa_tune_prox_cpw", "fa_tune_tgpu_batch", "fa_chain_levels", "fa_reduce_chain", "fa_torch_gpu_config",
     "fa_plan_create_order", "fa_table_bytes", "fa_reduce_tab",
     "fa_plan_balance_host", "fa_plan_launch_shape",
 ]
@@ -151,6 +151,7 @@ def _load():
         "fa_tune_bcast_store": (_I, [_I]),
         "fa_tune_prox_store": (_I, [_I]),
         "fa_tune_prox_cpw": (_I, [_I]),
+        "fa_tune_tgpu_batch": (_I, [_I]),
         "fa_chain_levels": (ctypes.c_uint, [_I, _I]),
         "fa_torch_gpu_config": (_I, [_I, _I64, ctypes.POINTER(_I)]),
         "fa_plan_create_order": (_I, [_P, _I, _I64, _P, _I, _I64, _I, _I, ctypes.c_uint,

@@ -56,6 +56,7 @@ FA_K_UNITS(extern)
 namespace fa_k {
 thread_local size_t t_dyn_lds = 0;  // tuning: occupancy cap through dynamic LDS
 thread_local int t_grid_cap = 0;     // tuning: persistent grid size
+thread_local int t_tgpu_batch = 0;  // tuning: rows per load batch of the S = 1 torch-GPU tiles (0: by N)
 thread_local int t_bcast_store = 2;  // the r04 flat broadcast's store policy (default sc1 nt)
 }  // namespace fa_k
 
@@ -623,7 +624,7 @@ __device__ __forceinline__ float tgpu_inner_vec(const Src& src, int64_t e, int n
 // budget of the parts' values to that S (a runtime switch over S = 1..16 in
 // one kernel needed 300 VGPRs and spilled).  Inner tiles (M == 1) ride in
 // the LS = 0 group; their own field is the lane count exponent.
-template <int LS>
+template <int LS, int WB = 16>
 __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   (void)args;
   constexpr int S = 1 << LS;
@@ -635,8 +636,8 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   const int n = a.n;
   if constexpr (LS == 0) {
     if (base == K_F32_TGPU_W) {
-      if (t.count == 8 * kBlock) tgpu_wide<2, 16, true>(a, t.start, t.count, fac, sum_only);
-      else tgpu_wide<2, 16, false>(a, t.start, t.count, fac, sum_only);
+      if (t.count == 8 * kBlock) tgpu_wide<2, WB, true>(a, t.start, t.count, fac, sum_only);
+      else tgpu_wide<2, WB, false>(a, t.start, t.count, fac, sum_only);
       return;
     }
   }
@@ -893,6 +894,7 @@ struct fa_plan {
   bool has64 = false;  // ... the int64 bucket
   int order = FA_ORDER_TORCH_CPU;
   int order_n = 0;        // FA_ORDER_TORCH_GPU: the client count it was cut for
+  int tgpu_batch = 16;    // ... rows per load batch of its S = 1 tiles (8 for N < 16)
   float* d_fac = nullptr; // ... and its per-tile mean factors
   int tg_lo[6] = {0, 0, 0, 0, 0, 0};  // ... tiles grouped by row split S = 1..16
   // cut from a segment list with FA_PLAN_GAPS_ARE_PADDING: every byte of
@@ -1640,20 +1642,30 @@ int fa_torch_gpu_config(int n, int64_t m, int* stride) {
 namespace {
 // Resident workgroups of tgpu_kernel<0> (the S = 1 group's launch) on `dev`,
 // queried once per process (0: unknown).
-int tgpu_slots(int dev) {
+int tgpu_slots(int dev, int batch) {
   static std::mutex mu;
   static std::map<int, int> cache;
   std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find(dev);
+  const int key = dev * 2 + (batch == 8);
+  auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   int occ = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tgpu_kernel<0>, kBlock, 0) !=
-      hipSuccess)
-    occ = 0;
+  const hipError_t e =
+      batch == 8 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tgpu_kernel<0, 8>, kBlock, 0)
+                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tgpu_kernel<0>, kBlock, 0);
+  if (e != hipSuccess) occ = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 0;
-  return cache[dev] = occ > 0 && cus > 0 ? occ * cus : 0;
+  return cache[key] = occ > 0 && cus > 0 ? occ * cus : 0;
 }
+
+// Rows per load batch of the S = 1 tiles for a plan cut for n clients: 8
+// below 16 clients (as the default reduce's 8-client kernel; the 8-row form
+// holds 102 VGPRs against 164, five workgroups per CU against three):
+// measured r04 (tools/tgpu_speed.py, profiles/r04_tgpu_batch.jsonl) cfg3
+// N = 5 40.8 vs 45.8 us, but cfg2 N = 20 146.7 vs 140.9, cfg5 N = 24 173.9
+// vs 167.3.
+int tgpu_batch_for(int n) { return n < 16 ? 8 : 16; }
 
 // The S = 1 group's tail round (r04; the default plan's split_tail, §4.3 of
 // DESIGN.md): its scalar and inner tiles first; and when its T tiles spill
@@ -1829,7 +1841,8 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
     for (int g = 0; g < 5; ++g) lo[g + 1] += lo[g];
     if (!(flags & FA_PLAN_TUNE_NO_BALANCE)) {
       int dev = 0;
-      if (hipGetDevice(&dev) == hipSuccess) tgpu_split_tail(&t, &fac, lo, tgpu_slots(dev));
+      if (hipGetDevice(&dev) == hipSuccess)
+        tgpu_split_tail(&t, &fac, lo, tgpu_slots(dev, tgpu_batch_for(n)));
     }
     order_groups_tmp.assign(lo, lo + 6);
   }
@@ -1844,6 +1857,7 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
   p->flat_bcast = flat_bcast_ok(flags, s32, f32_numel, s64, i64_numel);
   p->order = FA_ORDER_TORCH_GPU;
   p->order_n = n;
+  p->tgpu_batch = tgpu_batch_for(n);
   for (const Tile& x : t) (kind_is64(x.kind) ? p->has64 : p->has32) = true;
   hipError_t e = hipGetDevice(&p->device);
   if (e == hipSuccess && !t.empty()) {
@@ -2266,7 +2280,12 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
       a.tfac = plan->d_fac + lo;
       a.ntiles = cnt;
       switch (g) {
-        case 0: hipLaunchKernelGGL(tgpu_kernel<0>, dim3(cnt), dim3(kBlock), 0, st, a); break;
+        case 0:
+          if ((t_tgpu_batch ? t_tgpu_batch : plan->tgpu_batch) == 8)
+            hipLaunchKernelGGL((tgpu_kernel<0, 8>), dim3(cnt), dim3(kBlock), 0, st, a);
+          else
+            hipLaunchKernelGGL(tgpu_kernel<0>, dim3(cnt), dim3(kBlock), 0, st, a);
+          break;
         case 1: hipLaunchKernelGGL(tgpu_kernel<1>, dim3(cnt), dim3(kBlock), 0, st, a); break;
         case 2: hipLaunchKernelGGL(tgpu_kernel<2>, dim3(cnt), dim3(kBlock), 0, st, a); break;
         case 3: hipLaunchKernelGGL(tgpu_kernel<3>, dim3(cnt), dim3(kBlock), 0, st, a); break;
@@ -2478,6 +2497,14 @@ int fa_broadcast_f32(const float* src, float* const* dst, int n, int64_t numel, 
     HIP_TRY(hipGetLastError());
   }
   return FA_OK;
+}
+
+int fa_tune_tgpu_batch(int rows) {
+  if (rows != 0 && rows != 8 && rows != 16)
+    return set_err(FA_E_INVAL, "fa_tune_tgpu_batch: %d", rows);
+  const int old = t_tgpu_batch;
+  t_tgpu_batch = rows;
+  return old;
 }
 
 int fa_tune_bcast_store(int policy) {

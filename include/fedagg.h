@@ -358,6 +358,12 @@ int fa_tune_prox_store(int policy);
  * workgroup of fa_prox_norms' partial-sum launch, 1..4 (0: the default, 1);
  * the result bits do not depend on it.  Returns the previous setting. */
 int fa_tune_prox_cpw(int cpw);
+/* Tuning (experiments only; calling thread): rows per load batch of the
+ * torch-GPU order's S = 1 tiles, 8 or 16 (0: the default, 8 for plans cut
+ * for N < 16, else 16).  The bits do not depend on it.  Returns the
+ * previous setting. */
+int fa_tune_tgpu_batch(int rows);
+
 /* Tuning (experiments only; calling thread): the store policy of the round
  * broadcast's flat kernel — 0 global nt, 1 sc1, 2 sc1 nt (default),
  * 3 sc0 sc1, 4 plain.  Returns the previous policy, or FA_E_INVAL. */

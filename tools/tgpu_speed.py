@@ -21,6 +21,8 @@ from feddct_amd.layout import BucketLayout  # noqa: E402
 from feddct_amd.workload import joint_manifest, load_manifest, make_clients  # noqa: E402
 
 FORMS = {"wide": _lib.FA_PLAN_GAPS_ARE_PADDING,
+         "wide_b8": _lib.FA_PLAN_GAPS_ARE_PADDING,
+         "wide_b16": _lib.FA_PLAN_GAPS_ARE_PADDING,
          "wide_no_tail_split": _lib.FA_PLAN_GAPS_ARE_PADDING | _lib.FA_PLAN_TUNE_NO_BALANCE,
          "narrow": _lib.FA_PLAN_GAPS_ARE_PADDING | _lib.FA_PLAN_TUNE_TGPU_NARROW}
 
@@ -30,7 +32,9 @@ def measure(name, lay, cl, reps):
     exact = {k: True for k in FORMS}
     for _ in range(reps):
         for k, fl in FORMS.items():
+            _lib.lib.fa_tune_tgpu_batch({"wide_b8": 8, "wide_b16": 16}.get(k, 0))
             r = bench.torch_gpu_order_mode(lay, cl, steps=100, warmup=20, plan_flags=fl)
+            _lib.lib.fa_tune_tgpu_batch(0)
             res[k].append(r["us"])
             exact[k] &= r["bit_exact_vs_torch_cuda_mean"]
     nb = lay.algorithmic_bytes(len(cl))
