@@ -56,6 +56,11 @@ VARIANTS = {
     "round_bsc1": (_lib.FA_F_BCAST, 0, 1),
     "round_bsc0sc1": (_lib.FA_F_BCAST, 0, 3),
     "round_bplain": (_lib.FA_F_BCAST, 0, 4),
+    # clients per load batch forced (the default: 16 from N = 16, else 8)
+    "reduce_b1": (0, _lib.FA_PLAN_TUNE_BATCH1),
+    "reduce_b4": (0, _lib.FA_PLAN_TUNE_BATCH4),
+    "reduce_b8": (0, _lib.FA_PLAN_TUNE_BATCH8),
+    "reduce_b16": (0, _lib.FA_PLAN_TUNE_BATCH16),
     # the whole batch's loads back to back (FA_PLAN_TUNE_ISSUE_ALL) instead
     # of each client's behind the previous one's
     "reduce_issue_all": (0, _lib.FA_PLAN_TUNE_ISSUE_ALL),
