@@ -1,13 +1,17 @@
-"""Native multi-GPU round over RCCL (libfedagg_comm.so, include/fedagg_comm.h).
+"""Native multi-GPU rounds over RCCL (libfedagg_comm.so, include/fedagg_comm.h;
+SURVEY.md §8 b, e).
 
-The C-ABI form of feddct_amd.dist.ShardedAggregator (SURVEY.md §8 b, e1): one
-process per GPU, client slots sharded contiguously in slot order; per round
-the library sums the rank's clients in the exact torch order column chunk by
-column chunk and exchanges each chunk (ncclReduce to the server rank, or
-ncclAllReduce) on its own stream while the next chunk is summed; int64 keys
-are all-gathered and reduced exactly.  torch.distributed only carries the
-communicator's 128-byte id from rank 0 to the others; the data path is the
-library's own RCCL communicator.
+One process per GPU, client slots sharded contiguously in slot order.  The
+default entry, ``NativeAggregator`` (fa_multi_plan_create / fa_reduce_multi),
+is EXACT: bit-identical to one GPU reducing every slot, i.e. to the
+reference's single-process ``stack(...).mean(0)`` (train_feddct.py:42-50) —
+the blocked round when every 16-slot cascade block lies on at most two ranks,
+else the chained round (``multi_select`` names the choice without a GPU).
+The re-associated e1 round (partial sums + an RCCL sum) is opt-in
+(``exact=False``, or ``NativeShardedAggregator``): measured r04, max 22,938
+ULP from the exact result (``E1_ULP_R04``).  torch.distributed only carries
+the communicator's 128-byte id from rank 0 to the others; the data path is
+the library's own RCCL communicator.
 
 No fallback: loading raises if libfedagg_comm.so is missing.
 """
@@ -34,10 +38,21 @@ COMM_EXPORTS = ["fa_comm_unique_id", "fa_comm_init_rank", "fa_comm_init", "fa_co
                 "fa_stripe_plan_create", "fa_stripe_plan_destroy", "fa_reduce_striped",
                 "fa_chain_plan_create", "fa_chain_plan_destroy", "fa_reduce_chained",
                 "fa_block_plan_create", "fa_block_plan_destroy", "fa_reduce_blocked",
-                "fa_describe_round"]
+                "fa_describe_round", "fa_multi_select", "fa_multi_plan_create",
+                "fa_multi_plan_mode", "fa_multi_plan_destroy", "fa_reduce_multi",
+                "fa_mean_f32_multi_ex"]
 
 FA_XCHG_REDUCE, FA_XCHG_RS_GATHER = 0, 1
 FA_MODE_SHARDED, FA_MODE_STRIPED, FA_MODE_CHAINED, FA_MODE_BLOCKED = 0, 1, 2, 3
+MODE_NAMES = {FA_MODE_SHARDED: "e1", FA_MODE_STRIPED: "striped", FA_MODE_CHAINED: "chained",
+              FA_MODE_BLOCKED: "blocked"}
+FA_MULTI_EXACT, FA_MULTI_REASSOCIATE = 0, 1
+# The e1 round's distance from the exact result, measured r04 (2 ranks x 20
+# wrn16_8 clients, realistic synthetic state; bench.py N>1 'modes', file
+# profiles/r04_final_bench_n2_gloo_rehearsal.json): fp32 elements per ULP bin.
+E1_ULP_R04 = {"max_ulp": 22938, "histogram": {"0": 7072061, "1": 2990526, "2": 892989,
+                                              "3-4": 15239, "5-8": 642, "9-16": 342,
+                                              "17+": 355}}
 X = dict(SEND=1, RECV=2, REDUCE=3, ALLREDUCE=4, REDUCE_SCATTER=5, GATHER=6, ALLGATHER=7, BCAST=8,
          K_SUM=16, K_ZERO=17, K_DIV=18, K_COPY=19, K_STRIPE=20, K_CHAIN=21, K_STACK=22,
          K_TAILS=23, K_PART=24, K_CONT=25, K_BLOCK=26, K_FOLD=27)
@@ -95,6 +110,14 @@ def _load():
         "fa_describe_round": [_I, _I, _I, ctypes.POINTER(_I), _P, _I, _I64, _P, _I, _I64, _I, _I,
                               ctypes.c_uint, _I, _I, ctypes.POINTER(FaXfer), _I,
                               ctypes.POINTER(_I)],
+        "fa_multi_select": [_I, ctypes.POINTER(_I), ctypes.c_uint, ctypes.POINTER(_I)],
+        "fa_multi_plan_create": [_P, _P, _I, _I64, _P, _I, _I64, ctypes.POINTER(_I), _I,
+                                 ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(_P)],
+        "fa_multi_plan_mode": [_P, ctypes.POINTER(_I)],
+        "fa_multi_plan_destroy": [_P],
+        "fa_reduce_multi": [ctypes.POINTER(_P), _I, ctypes.POINTER(FaShardIO), _I],
+        "fa_mean_f32_multi_ex": [_P, _P, ctypes.POINTER(_I), _I64, _P, _P, _I, _I, ctypes.c_uint,
+                                 _P],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -111,6 +134,17 @@ def lib():
     if _clib is None:
         _clib = _load()
     return _clib
+
+
+def multi_select(counts: Sequence[int], exact: bool = True) -> str:
+    """The round form the default entry takes for these shard counts
+    (fa_multi_select, host only): "blocked", "chained", or "e1" when
+    ``exact=False``."""
+    c = (_I * len(counts))(*map(int, counts))
+    m = _I()
+    _lib.check(lib().fa_multi_select(len(counts), c, 0 if exact else FA_MULTI_REASSOCIATE,
+                                     ctypes.byref(m)), "fa_multi_select")
+    return MODE_NAMES[m.value]
 
 
 def unique_id() -> bytes:
@@ -234,7 +268,9 @@ class ShardPlan:
 
 
 class NativeShardedAggregator:
-    """The cross-GPU round of ``dist.ShardedAggregator`` through the C ABI:
+    """The e1 round of ``dist.ShardedAggregator`` through the C ABI (opt-in:
+    RE-ASSOCIATED, not within 1 ULP of the reference — max 22,938 ULP
+    measured r04, ``E1_ULP_R04``; the default entry is ``NativeAggregator``):
     ``step()`` is ONE fa_reduce_sharded call (kernels, chunked RCCL exchange,
     /N, int64 gather + exact reduce), stream-ordered on the current stream.
 
@@ -467,3 +503,89 @@ class NativeBlockedAggregator(NativeChainedAggregator):
         self.io.stream = s
         _lib.check(lib().fa_reduce_blocked(self._plans, 1, ctypes.byref(self.io), self.root),
                    "fa_reduce_blocked")
+
+
+class MultiPlan:
+    """This rank's plan of the default round (fa_multi_plan_create): the form
+    fa_multi_select picks for ``counts``; ``mode`` names it."""
+
+    def __init__(self, comm: Comm, layout: BucketLayout, counts: Sequence[int],
+                 nchunks: int = 0, exact: bool = True):
+        a32, n32, a64, n64 = _segs(layout)
+        c = (_I * len(counts))(*map(int, counts))
+        h = _P()
+        _lib.check(lib().fa_multi_plan_create(comm.handle, a32, n32, int(layout.f32_numel), a64,
+                                              n64, int(layout.i64_numel), c, int(nchunks),
+                                              _lib.FA_PLAN_GAPS_ARE_PADDING,
+                                              0 if exact else FA_MULTI_REASSOCIATE,
+                                              ctypes.byref(h)), "fa_multi_plan_create")
+        self.handle = h
+        self.comm = comm
+        m = _I()
+        _lib.check(lib().fa_multi_plan_mode(h, ctypes.byref(m)), "fa_multi_plan_mode")
+        self.mode = MODE_NAMES[m.value]
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                lib().fa_multi_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+class NativeAggregator(NativeShardedAggregator):
+    """THE default multi-GPU round (fa_reduce_multi): exact — bit-identical to
+    one GPU reducing all ``n_total`` slots in slot order, i.e. to the
+    reference's single-process mean (train_feddct.py:42-50).  The form is
+    picked from the shard counts (``self.mode``): "blocked" when every
+    16-slot cascade block lies on at most two ranks, else "chained".
+
+    ``exact=False`` opts into the re-associated e1 round (partial sums + an
+    RCCL sum, ``self.mode == "e1"``): faster on the wire but NOT within 1 ULP
+    of the reference — measured r04 (2 ranks x 20 wrn16_8 clients): max
+    22,938 ULP, 64.5 % of elements exact, 27.3 % off by 1 ULP, 8.1 % by 2,
+    0.14 % by 3-4, 1,339 elements by 5 or more (``E1_ULP_R04``).
+
+    ``counts``: slots per rank (default: ``shard_range``); ``final="reduce"``
+    puts the result on ``root`` (default: the last rank holding slots, where
+    the chained round ends), ``"allreduce"`` on every rank; ``weights``: this
+    rank's fp32 client weights (weighted rounds are exact too)."""
+
+    def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
+                 local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
+                 out64: torch.Tensor, comm: Comm, final: str = "reduce",
+                 root: Optional[int] = None, weights: Optional[Sequence[float]] = None,
+                 counts: Optional[Sequence[int]] = None, exact: bool = True, nchunks: int = 0):
+        if final not in ("reduce", "allreduce"):
+            raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
+        world, rank, _ = comm.info()
+        if counts is None:
+            counts = [b - a for a, b in (shard_range(n_total, world, r) for r in range(world))]
+        if len(counts) != world or len(local32) != counts[rank] or sum(counts) != n_total:
+            raise ValueError(f"rank {rank} holds {len(local32)} clients, shard is "
+                             f"{counts[rank] if rank < len(counts) else '?'}")
+        self.plan = MultiPlan(comm, layout, counts, nchunks, exact)
+        self.mode = self.plan.mode
+        if root is None:
+            root = max(r for r in range(world) if counts[r] > 0)
+        self.root = root if final == "reduce" else -1
+        self._a32 = _lib.ptr_array([t.data_ptr() for t in local32])
+        self._a64 = _lib.ptr_array([t.data_ptr() for t in local64])
+        self._w = (None if weights is None
+                   else (ctypes.c_float * max(1, len(weights)))(*map(float, weights)))
+        self._plans = (_P * 1)(self.plan.handle.value)
+        self.io = FaShardIO()
+        self.io.c32 = ctypes.cast(self._a32, _P)
+        self.io.c64 = ctypes.cast(self._a64, _P) if layout.i64_numel else None
+        self.io.weights = ctypes.cast(self._w, _P) if self._w is not None else None
+        self.io.out32 = out32.data_ptr()
+        self.io.out64 = out64.data_ptr() if layout.i64_numel else None
+        self._keep = (local32, local64, out32, out64)
+
+    def step(self, stream=None) -> None:
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self.io.stream = s
+        _lib.check(lib().fa_reduce_multi(self._plans, 1, ctypes.byref(self.io), self.root),
+                   "fa_reduce_multi")

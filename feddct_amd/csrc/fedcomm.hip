@@ -666,13 +666,49 @@ int rank_of_row(const Geo& g, int i) {
   return -1;
 }
 
+// The cascade's level step for n rows (fa_reduce's lp: 16 below 2^16 rows).
+int cascade_lp(int n) {
+  int c = 0;
+  while ((1ll << c) < n) ++c;
+  return std::max(4, c / 4);
+}
+
+// The blocked round's condition from the counts alone: the first cascade
+// block (slots [*a, *b)) whose slots lie on more than two of the ranks that
+// hold slots (ranks without slots in between do not count), or -1 when every
+// block fits.  block_geo and fa_multi_select share it.
+int first_wide_block(int nranks, const int* counts, int* a_out, int* b_out) {
+  int n = 0;
+  std::vector<int> first(nranks);
+  for (int r = 0; r < nranks; ++r) {
+    first[r] = n;
+    n += std::max(0, counts[r]);
+  }
+  const int Q = 1 << cascade_lp(n);
+  for (int i = 0, a = 0; a < n; ++i, a += Q) {
+    const int b = std::min(n, a + Q);
+    int on = 0;
+    for (int r = 0; r < nranks; ++r)
+      if (counts[r] > 0 && first[r] < b && first[r] + counts[r] > a) ++on;
+    if (on > 2) {
+      if (a_out) *a_out = a;
+      if (b_out) *b_out = b;
+      return i;
+    }
+  }
+  return -1;
+}
+
 int block_geo(const Geo& g, const std::vector<fa_tile_desc>& vec, BlockGeo* bg) {
   const int n = g.n_total;
-  int lp = 4;
+  const int lp = cascade_lp(n);
   {
-    int c = 0;
-    while ((1ll << c) < n) ++c;
-    lp = std::max(4, c / 4);
+    int a = 0, b = 0;
+    if (first_wide_block(g.nranks, g.counts.data(), &a, &b) >= 0)
+      return set_err(FA_E_RANGE,
+                     "blocked round: slots %d..%d (one cascade block) lie on more than two "
+                     "ranks; use the chained round",
+                     a, b - 1);
   }
   bg->lp = lp;
   const int Q = 1 << lp, mask = Q - 1;
@@ -684,18 +720,9 @@ int block_geo(const Geo& g, const std::vector<fa_tile_desc>& vec, BlockGeo* bg) 
   bg->nbsum = 0;
   for (int i = 0; i < bg->P; ++i) {
     const int a = i * Q, b = std::min(n, a + Q);
+    // (first_wide_block above: the holder is the next rank holding slots
+    // after the starter)
     const int r0 = rank_of_row(g, a), r1 = rank_of_row(g, b - 1);
-    if (r0 != r1) {
-      // the holder must be the next rank holding slots after the starter
-      int nxt = -1;
-      for (int r = r0 + 1; r < g.nranks && nxt < 0; ++r)
-        if (g.counts[r] > 0) nxt = r;
-      if (nxt != r1 || g.first[r1] + g.counts[r1] < b)
-        return set_err(FA_E_RANGE,
-                       "blocked round: slots %d..%d (one cascade block) lie on more than two "
-                       "ranks; use the chained round",
-                       a, b - 1);
-    }
     bg->s0.push_back(a);
     bg->s1.push_back(b);
     bg->starter.push_back(r0);
@@ -1708,26 +1735,90 @@ int fa_reduce_sharded(fa_shard_plan* const* plans, int nlocal, const fa_shard_io
                    "fa_reduce_sharded");
 }
 
+// ======================================================= default (r05) ====
+// The default multi-GPU entry: the exact round the counts allow (blocked if
+// every cascade block lies on at most two ranks, else chained); e1 only on
+// request (FA_MULTI_REASSOCIATE).
+int fa_multi_select(int nranks, const int* counts, unsigned mflags, int* mode) {
+  if (!mode) return set_err(FA_E_INVAL, "fa_multi_select: mode is NULL");
+  *mode = -1;
+  if (nranks < 1 || !counts) return set_err(FA_E_INVAL, "fa_multi_select: bad arguments");
+  if (mflags & ~(unsigned)FA_MULTI_REASSOCIATE)
+    return set_err(FA_E_INVAL, "fa_multi_select: unknown flags 0x%x", mflags);
+  int n = 0;
+  for (int r = 0; r < nranks; ++r) {
+    if (counts[r] < 0) return set_err(FA_E_INVAL, "fa_multi_select: counts[%d]=%d", r, counts[r]);
+    n += counts[r];
+  }
+  if (n < 1 || n > FA_MAX_CLIENTS)
+    return set_err(FA_E_RANGE, "fa_multi_select: %d clients in total", n);
+  if (mflags & FA_MULTI_REASSOCIATE) *mode = FA_MODE_SHARDED;
+  else *mode = first_wide_block(nranks, counts, nullptr, nullptr) < 0 ? FA_MODE_BLOCKED
+                                                                      : FA_MODE_CHAINED;
+  return FA_OK;
+}
+
+int fa_multi_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
+                         const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
+                         int nchunks, unsigned flags, unsigned mflags, fa_multi_plan** out) {
+  if (!out) return set_err(FA_E_INVAL, "fa_multi_plan_create: out is NULL");
+  *out = nullptr;
+  if (!comm) return set_err(FA_E_INVAL, "fa_multi_plan_create: NULL comm");
+  int mode = -1;
+  int rc = fa_multi_select(comm->nranks, counts, mflags, &mode);
+  if (rc) return rc;
+  if (nchunks == 0) nchunks = mode == FA_MODE_CHAINED ? 16 : 8;
+  if (mode == FA_MODE_BLOCKED) nchunks = 1;
+  return make_round(comm, mode, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, counts,
+                    nchunks, FA_XCHG_REDUCE, flags, "fa_multi_plan_create",
+                    (fa_round_plan**)out);
+}
+
+int fa_multi_plan_mode(const fa_multi_plan* plan, int* mode) {
+  if (!plan || !mode) return set_err(FA_E_INVAL, "fa_multi_plan_mode: NULL argument");
+  *mode = ((const fa_round_plan*)plan)->mode;
+  return FA_OK;
+}
+
+int fa_multi_plan_destroy(fa_multi_plan* p) {
+  free_round((fa_round_plan*)p);
+  return FA_OK;
+}
+
+int fa_reduce_multi(fa_multi_plan* const* plans, int nlocal, const fa_shard_io* io, int root) {
+  if (nlocal < 1 || !plans || !plans[0])
+    return set_err(FA_E_INVAL, "fa_reduce_multi: bad arguments");
+  return run_round((fa_round_plan* const*)plans, nlocal, io, root,
+                   ((const fa_round_plan*)plans[0])->mode, "fa_reduce_multi");
+}
+
 // Stateless form (SURVEY.md §8 b's fa_mean_f32_multi): fp32 segments only,
-// shard plans cached per (communicator, layout, counts); 8 chunks.
+// the default (exact) round; plans cached per (communicator, layout, counts).
 int fa_mean_f32_multi(fa_comm* comm, const float* const* clients, const int* counts,
                       int64_t numel, float* out, const fa_seg* segs, int nseg, int root,
                       void* stream) {
+  return fa_mean_f32_multi_ex(comm, clients, counts, numel, out, segs, nseg, root, 0u, stream);
+}
+
+int fa_mean_f32_multi_ex(fa_comm* comm, const float* const* clients, const int* counts,
+                         int64_t numel, float* out, const fa_seg* segs, int nseg, int root,
+                         unsigned mflags, void* stream) {
   if (!comm || !counts) return set_err(FA_E_INVAL, "fa_mean_f32_multi: NULL comm/counts");
   if (nseg < 0 || (nseg > 0 && !segs)) return set_err(FA_E_INVAL, "fa_mean_f32_multi: segs");
   std::string key((const char*)&comm, sizeof comm);
+  key.append((const char*)&mflags, sizeof mflags);
   key.append((const char*)&numel, sizeof numel);
   key.append((const char*)counts, sizeof(int) * comm->nranks);
   if (nseg > 0) key.append((const char*)segs, sizeof(fa_seg) * nseg);
-  fa_shard_plan* plan = nullptr;
+  fa_multi_plan* plan = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_multi_mu);
     auto it = g_multi.find(key);
     if (it != g_multi.end()) {
-      plan = (fa_shard_plan*)it->second;
+      plan = (fa_multi_plan*)it->second;
     } else {
-      const int rc = fa_shard_plan_create(comm, segs, nseg, numel, nullptr, 0, 0, counts, 8,
-                                          FA_PLAN_GAPS_ARE_PADDING, &plan);
+      const int rc = fa_multi_plan_create(comm, segs, nseg, numel, nullptr, 0, 0, counts, 0,
+                                          FA_PLAN_GAPS_ARE_PADDING, mflags, &plan);
       if (rc) return rc;
       g_multi[key] = (fa_round_plan*)plan;
     }
@@ -1736,7 +1827,7 @@ int fa_mean_f32_multi(fa_comm* comm, const float* const* clients, const int* cou
   io.c32 = clients;
   io.out32 = out;
   io.stream = stream;
-  return fa_reduce_sharded(&plan, 1, &io, root);
+  return fa_reduce_multi(&plan, 1, &io, root);
 }
 
 // ============================================================== e2 ========

@@ -1,23 +1,32 @@
 """Aggregation across the GPUs of one node (SURVEY.md §8 e) over
 torch.distributed (backend "nccl" = RCCL over xGMI), one process per GPU.
 Rank r holds a contiguous shard of the client slots, in slot order
-(``shard_range``).  Three round forms:
+(``shard_range``).
 
-* ``ShardedAggregator`` (e1, the north_star's partitioning): the HIP kernel
-  sums the rank's clients in the torch order without the /N
-  (FA_F_SUM_ONLY), chunk by column chunk; each chunk's partial bucket is
-  summed across ranks by an RCCL reduce to the server rank (``final=
-  "reduce"``) or an all-reduce (``"allreduce"``) while the kernel sums the
-  next chunk; then ``/ N_total``.  The cross-rank sum re-associates fp32:
-  NOT bit-identical to the single-process reference (bench.py reports the
-  ULP distance);
+THE DEFAULT ENTRY IS ``Aggregator`` (r05), and it is EXACT: its result is
+bit-identical to one GPU reducing every slot, i.e. to the reference's
+single-process ``stack(...).mean(0)`` (train_feddct.py:42-50).  Over RCCL it
+runs the native library's default round (comm.NativeAggregator: the blocked
+round when every 16-slot cascade block lies on at most two ranks, else the
+chained round — ``exact_form``); over any other transport (gloo rehearsals)
+the chained round orchestrated here.  The round forms:
+
 * ``ChainAggregator`` (exact client shards): the shards stay put and the
   cascade's accumulator state travels rank to rank in slot order, chunk by
   chunk (fa_reduce_chain); the scalar columns are all-gathered raw.
   Bit-identical;
 * ``StripedAggregator`` (e2, exact column stripes): every client's values
   for rank r's column stripe go to rank r, which reduces the stripe over all
-  clients.  Bit-identical.
+  clients.  Bit-identical;
+* ``ShardedAggregator`` (e1, OPT-IN: ``Aggregator(exact=False)``): the HIP
+  kernel sums the rank's clients in the torch order without the /N
+  (FA_F_SUM_ONLY), chunk by column chunk; each chunk's partial bucket is
+  summed across ranks by an RCCL reduce to the server rank (``final=
+  "reduce"``) or an all-reduce (``"allreduce"``) while the kernel sums the
+  next chunk; then ``/ N_total``.  The cross-rank sum re-associates fp32:
+  NOT within the north_star's 1 ULP — measured r04 (2 ranks x 20 wrn16_8
+  clients) max 22,938 ULP, histogram in comm.E1_ULP_R04; bench.py's N>1
+  line reports it beside the time.
 
 int64 keys (a few bytes) always travel raw — an all-gather of every rank's
 int64 buckets — and are reduced exactly over all N_total clients.
@@ -49,6 +58,29 @@ def shard_range(n_total: int, world: int, rank: int):
     base, rem = divmod(n_total, world)
     lo = rank * base + min(rank, rem)
     return lo, lo + base + (1 if rank < rem else 0)
+
+
+def cascade_lp(n: int) -> int:
+    """torch's cascade level step for n rows (16 below 2**16 rows)."""
+    return max(4, (int(n - 1).bit_length() if n > 1 else 0) // 4)
+
+
+def exact_form(counts: Sequence[int]) -> str:
+    """The exact round the default entry takes for these shard counts
+    (fedcomm.hip fa_multi_select): "blocked" when every cascade block of
+    2**lp slots lies on at most two of the ranks holding slots, else
+    "chained"."""
+    first, n = [], 0
+    for c in counts:
+        first.append(n)
+        n += max(0, int(c))
+    q = 1 << cascade_lp(n)
+    for a in range(0, n, q):
+        b = min(n, a + q)
+        on = sum(1 for r, c in enumerate(counts) if c > 0 and first[r] < b and first[r] + c > a)
+        if on > 2:
+            return "chained"
+    return "blocked"
 
 
 def partner(world: int, rank: int, t: int) -> int:
@@ -643,3 +675,82 @@ class ChainAggregator:
                 self.backend.tails([self.gather32[r] for r in self.rows], self.tidx, self.out32,
                                    weights is not None)
             self.backend.reduce_i64([self.gather64[r] for r in self.rows], self.out64)
+
+
+# --------------------------------------------------------------------------
+# The default entry (r05): exact.
+# --------------------------------------------------------------------------
+class Aggregator:
+    """THE multi-GPU round (SURVEY.md §8 e; BASELINE config 5): this rank's
+    client slots ``local32`` / ``local64`` (a contiguous shard, slot order)
+    reduced with every other rank's into ``out32`` / ``out64``.
+
+    ``exact=True`` (default): bit-identical to one GPU reducing all
+    ``n_total`` slots (the reference's train_feddct.py:42-50 order).  Over an
+    RCCL ("nccl") group the native library's default round
+    (comm.NativeAggregator: blocked or chained by ``exact_form(counts)``, ONE
+    C call per round on the library's own communicator); over any other
+    backend, or with an injected arithmetic ``backend`` (tests), the chained
+    round orchestrated over torch.distributed (``ChainAggregator``) — the
+    blocked round exists natively only.
+
+    ``exact=False``: the re-associated e1 round (``ShardedAggregator``):
+    unweighted only; NOT within 1 ULP (max 22,938 ULP measured r04,
+    comm.E1_ULP_R04).
+
+    ``final="reduce"`` puts the result on ``root`` (default: the last rank
+    holding slots, where the chained round ends); ``"allreduce"`` on every
+    rank.  ``weights``: this rank's fp32 client weights (exact rounds only).
+    ``self.form`` names what runs, e.g. "blocked/native"."""
+
+    def __init__(self, layout: BucketLayout, local32: List[torch.Tensor],
+                 local64: List[torch.Tensor], n_total: int, out32: torch.Tensor,
+                 out64: torch.Tensor, group=None, final: str = "reduce",
+                 root: Optional[int] = None, weights: Optional[Sequence[float]] = None,
+                 counts: Optional[Sequence[int]] = None, exact: bool = True,
+                 native: Optional[bool] = None, backend=None, nchunks: Optional[int] = None):
+        if final not in ("reduce", "allreduce"):
+            raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        if counts is None:
+            counts = [b - a for a, b in (shard_range(n_total, world, r) for r in range(world))]
+        counts = [int(c) for c in counts]
+        if len(counts) != world or sum(counts) != n_total or len(local32) != counts[rank]:
+            raise ValueError(f"rank {rank} holds {len(local32)} clients; counts {counts} "
+                             f"over {world} ranks must sum to {n_total}")
+        if root is None:
+            root = max(r for r in range(world) if counts[r] > 0)
+        self.local32, self.local64, self.weights = local32, local64, weights
+        self.counts = counts
+        if not exact:
+            if weights is not None:
+                raise ValueError("the re-associated e1 round is unweighted")
+            if counts != [b - a for a, b in (shard_range(n_total, world, r)
+                                             for r in range(world))]:
+                raise ValueError("the e1 round takes shard_range shards")
+            self._agg = ShardedAggregator(layout, local32, local64, n_total, out32, out64,
+                                          nchunks=nchunks or 8, backend=backend, group=group,
+                                          final=final, root=root)
+            self.form = "e1/torch.distributed"
+            self._step = self._agg.step
+            return
+        if native is None:
+            native = backend is None and "nccl" in str(dist.get_backend(group))
+        if native:
+            from .comm import Comm, NativeAggregator
+            self._comm = Comm.from_process_group(group)
+            self._agg = NativeAggregator(layout, local32, local64, n_total, out32, out64,
+                                         self._comm, final=final, root=root, weights=weights,
+                                         counts=counts, nchunks=nchunks or 0)
+            self.form = f"{self._agg.mode}/native"
+            self._step = self._agg.step
+        else:
+            self._agg = ChainAggregator(layout, n_total, out32, out64, group=group,
+                                        backend=backend, final=final, root=root,
+                                        nchunks=nchunks or 16, counts=counts)
+            self.form = "chained/torch.distributed"
+            self._step = lambda: self._agg.step(self.local32, self.local64, self.weights)
+
+    def step(self) -> None:
+        """One round, stream-ordered on the current stream."""
+        self._step()

@@ -5,9 +5,25 @@
  *
  * Reference: the round loops aggregate every client of a round into one
  * global model (train_fedavg.py:138-149, train_feddct.py:34-56); when the
- * clients' states do not fit one GPU, the client slots are sharded across the
- * GPUs of the node — rank r holds a contiguous run of slots, in slot order —
- * and a round is
+ * clients' states do not fit one GPU, or were trained on several, the client
+ * slots are sharded across the GPUs of the node — rank r holds a contiguous
+ * run of slots, in slot order.
+ *
+ * THE DEFAULT ENTRY IS EXACT (r05): fa_multi_plan_create / fa_reduce_multi
+ * (and the stateless fa_mean_f32_multi) run a round whose result is
+ * bit-identical to one GPU's fa_reduce over all slots, i.e. to the
+ * reference's single-process stack(...).mean(0) (train_feddct.py:42-50):
+ * the blocked round when every cascade block of 16 slots lies on at most two
+ * ranks, else the chained round (fa_multi_select names the choice, host
+ * only).  The re-associated e1 round (partial sums + an RCCL sum,
+ * fa_reduce_sharded below) is opt-in (FA_MULTI_REASSOCIATE, or its own
+ * plan type): it is NOT within the north_star's 1 ULP — measured r04 on
+ * 2 x 20 wrn16_8 clients (profiles/r04_final_bench_n2_gloo_rehearsal.json):
+ * max 22,938 ULP (near-cancelling sums), ULP histogram 0: 7,072,061,
+ * 1: 2,990,526, 2: 892,989, 3-4: 15,239, 5-8: 642, 9-16: 342, 17+: 355
+ * elements; within the forward error bound 2N * 2^-24 * sum|x_i| / N.
+ *
+ * The e1 round (fa_reduce_sharded) is
  *
  *   1. per rank, the torch-order sum of its own clients for every fp32 key
  *      (fa_reduce with FA_F_SUM_ONLY, over a column chunk at a time);
@@ -19,9 +35,7 @@
  *   int64 keys (num_batches_tracked) are all-gathered raw and reduced exactly
  *   over all N_total clients, so they match the single-GPU result bit for bit.
  *
- * The cross-rank sum re-associates fp32: the fp32 result is NOT bit-identical
- * to the single-process reference (the exact column-striped mode is
- * fa_reduce_striped, below).  With one rank it is bit-identical.
+ * With one rank every form is the single-GPU reduction (bit-identical).
  *
  * Process models:
  *   - one process per GPU (the product's): rank 0 calls fa_comm_unique_id,
@@ -99,7 +113,8 @@ typedef struct fa_shard_io {
   void *stream;                 /* hipStream_t of the caller                  */
 } fa_shard_io;
 
-/* One round across the ranks.  plans[d] / io[d]: the d-th GPU this process
+/* One e1 round across the ranks (re-associated: see the top of this file;
+ * the default entry is fa_reduce_multi).  plans[d] / io[d]: the d-th GPU this process
  * drives (nlocal = 1 in the one-process-per-GPU model).  root >= 0: the
  * global state lands on rank `root` only (the north_star's final reduce);
  * root < 0: on every rank (all-reduce).  Weighted: fp32 keys = sum over all
@@ -108,15 +123,44 @@ typedef struct fa_shard_io {
 int fa_reduce_sharded(fa_shard_plan *const *plans, int nlocal,
                       const fa_shard_io *io, int root);
 
-/* Stateless form of the sharded round for fp32 keys (SURVEY.md §8 b's
+/* ---- the default multi-GPU round (r05): exact ------------------------------
+ * fa_multi_select (host only, no communicator): the round form the default
+ * entry takes for these counts — FA_MODE_BLOCKED when every cascade block of
+ * 2^lp slots (16 below 65,536 slots) lies on at most two of the ranks holding
+ * slots, else FA_MODE_CHAINED; FA_MODE_SHARDED (e1) only with
+ * FA_MULTI_REASSOCIATE.  fa_multi_plan_create builds that form's plan
+ * (nchunks 0: 16 column chunks for the chained round, 8 for e1; the blocked
+ * round has none); fa_reduce_multi runs it (io / root as fa_reduce_sharded;
+ * weighted rounds: fp32 keys = sum over all clients of fp32(x_i * w_i) in the
+ * torch order, also exact).  fa_multi_plan_mode reports the form. */
+#define FA_MULTI_EXACT 0u          /* default: blocked or chained, bit-identical */
+#define FA_MULTI_REASSOCIATE 1u    /* opt-in: e1, NOT bit-identical (above)      */
+typedef struct fa_multi_plan fa_multi_plan;
+int fa_multi_select(int nranks, const int *counts, unsigned mflags, int *mode);
+int fa_multi_plan_create(fa_comm *comm, const fa_seg *seg32, int nseg32,
+                         int64_t f32_numel, const fa_seg *seg64, int nseg64,
+                         int64_t i64_numel, const int *counts, int nchunks,
+                         unsigned flags, unsigned mflags, fa_multi_plan **out);
+int fa_multi_plan_mode(const fa_multi_plan *plan, int *mode);
+int fa_multi_plan_destroy(fa_multi_plan *plan);
+int fa_reduce_multi(fa_multi_plan *const *plans, int nlocal,
+                    const fa_shard_io *io, int root);
+
+/* Stateless fp32 form of the default round (SURVEY.md §8 b's
  * fa_mean_f32_multi): `clients` = this rank's counts[rank] buckets of numel
  * floats laid out by segs (as fa_mean_f32; gaps are treated as padding);
- * out = the mean over all ranks' clients on `root` (root < 0: every rank).
- * The shard plan is cached per (comm, layout, counts) and released with the
+ * out = the mean over all ranks' clients on `root` (root < 0: every rank),
+ * bit-identical to fa_mean_f32 over all clients on one GPU (r05; r01-r04 this
+ * entry ran e1).  _ex takes FA_MULTI_* flags (FA_MULTI_REASSOCIATE: e1).  The
+ * plan is cached per (comm, flags, layout, counts) and released with the
  * communicator (fa_comm_destroy). */
 int fa_mean_f32_multi(fa_comm *comm, const float *const *clients,
                       const int *counts, int64_t numel, float *out,
                       const fa_seg *segs, int nseg, int root, void *stream);
+int fa_mean_f32_multi_ex(fa_comm *comm, const float *const *clients,
+                         const int *counts, int64_t numel, float *out,
+                         const fa_seg *segs, int nseg, int root,
+                         unsigned mflags, void *stream);
 
 /* ---- exact mode: column stripes ----------------------
  * Rank r owns a contiguous column stripe [lo_r, lo_{r+1}) of the bucket (cut

@@ -2,20 +2,31 @@
 // libfedagg_comm (chained, striped, sharded with either e1 exchange) run with
 // W ranks on one GPU over the loopback communicator (loopccl.hip), checked
 // against one GPU's fa_reduce over all clients:
-//   chained / striped / blocked: bit-identical (fp32 and int64);
-//   sharded (e1): int64 bit-identical, fp32 within the forward error bound of
-//   two N-term sums, 2N * 2^-24 * sum_i |w_i x_i| (any summation order).
+//   chained / striped / blocked / multi / mean_multi: bit-identical (fp32 and
+//   int64; mean_multi has no int64 keys);
+//   sharded / multi_e1 (e1): int64 bit-identical, fp32 within the forward
+//   error bound of two N-term sums, 2N * 2^-24 * sum_i |w_i x_i| (any
+//   summation order).
 // Usage: loop_round LAYOUT CASE...
-//   LAYOUT: "f32_numel i64_numel nseg32 nseg64" then one "offset numel" line
-//           per segment (fp32 first), as BucketLayout.segs32 / segs64.
+//   LAYOUT: "f32_numel i64_numel nseg32 nseg64 [P]" then one "offset numel"
+//           line per segment (fp32 first), as BucketLayout.segs32 / segs64;
+//           with P, fp32 lines are "offset numel key mu sigma" and int64
+//           lines "offset numel key": the digest generator's per-key
+//           parameters (feddct_amd/workload.py fill_client), so a result can
+//           be checked against tests/golden/digests.json (FA_LOOP_DUMP).
 //   CASE:   mode:W:counts:root:model:weighted:nchunks
 //           mode   chained | striped | blocked | sharded | sharded_rs
+//                  | multi (the default entry: fa_multi_plan_create /
+//                    fa_reduce_multi) | multi_e1 (FA_MULTI_REASSOCIATE)
+//                  | mean_multi (fa_mean_f32_multi: fp32 keys only)
 //           counts comma-separated client slots per rank (sum = N)
 //           root   result rank, or -1 for every rank
 //           model  threads (one thread + comm per rank: fa_comm_init_rank)
 //                  | single (one thread drives all ranks: fa_comm_init; only
 //                    for schedules whose p2p pairs share a step: sharded, blocked)
 // One JSON line per case; exit status 0 iff every case passed.
+// FA_LOOP_DUMP=path: the first result rank's out32 then out64, raw, of the
+// last case.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -36,6 +47,9 @@ namespace {
 struct Layout {
   int64_t f32_numel = 0, i64_numel = 0;
   std::vector<fa_seg> s32, s64;
+  bool params = false;                 // per-key generator parameters given
+  std::vector<int> key32, key64;
+  std::vector<float> mu, sigma;
 };
 
 struct Case {
@@ -47,15 +61,32 @@ struct Case {
 bool read_layout(const char* path, Layout* L) {
   FILE* f = fopen(path, "r");
   if (!f) return false;
+  char line[256];
   long long a, b;
   int n32, n64;
-  if (fscanf(f, "%lld %lld %d %d", &a, &b, &n32, &n64) != 4) return false;
+  char tag[8] = {0};
+  if (!fgets(line, sizeof line, f)) return false;
+  const int got = sscanf(line, "%lld %lld %d %d %7s", &a, &b, &n32, &n64, tag);
+  if (got < 4) return false;
+  L->params = got == 5 && tag[0] == 'P';
   L->f32_numel = a;
   L->i64_numel = b;
   for (int i = 0; i < n32 + n64; ++i) {
     long long o, m;
     if (fscanf(f, "%lld %lld", &o, &m) != 2) return false;
     (i < n32 ? L->s32 : L->s64).push_back(fa_seg{o, m});
+    if (!L->params) continue;
+    int k;
+    if (fscanf(f, "%d", &k) != 1) return false;
+    if (i < n32) {
+      float mu, sg;
+      if (fscanf(f, "%f %f", &mu, &sg) != 2) return false;
+      L->key32.push_back(k);
+      L->mu.push_back(mu);
+      L->sigma.push_back(sg);
+    } else {
+      L->key64.push_back(k);
+    }
   }
   fclose(f);
   return true;
@@ -101,6 +132,12 @@ struct Rank {
 int create_plan(const Case& c, const Layout& L, Rank& r) {
   const unsigned fl = FA_PLAN_GAPS_ARE_PADDING;
   const fa_seg* s64 = L.s64.empty() ? nullptr : L.s64.data();
+  if (c.mode == "mean_multi") return 0;  // stateless: cached in the communicator
+  if (c.mode == "multi" || c.mode == "multi_e1")
+    return fa_multi_plan_create(r.comm, L.s32.data(), (int)L.s32.size(), L.f32_numel, s64,
+                                (int)L.s64.size(), L.i64_numel, c.counts.data(), c.nchunks, fl,
+                                c.mode == "multi" ? FA_MULTI_EXACT : FA_MULTI_REASSOCIATE,
+                                (fa_multi_plan**)&r.plan);
   if (c.mode == "chained")
     return fa_chain_plan_create(r.comm, L.s32.data(), (int)L.s32.size(), L.f32_numel, s64,
                                 (int)L.s64.size(), L.i64_numel, c.counts.data(), c.nchunks, fl,
@@ -119,8 +156,16 @@ int create_plan(const Case& c, const Layout& L, Rank& r) {
                                  (fa_shard_plan**)&r.plan);
 }
 
-int run_round(const Case& c, std::vector<void*>& plans, std::vector<fa_shard_io>& io) {
+int run_round(const Case& c, const Layout& L, std::vector<Rank*>& ranks,
+              std::vector<void*>& plans, std::vector<fa_shard_io>& io) {
   const int nl = (int)plans.size();
+  if (c.mode == "mean_multi") {
+    if (nl != 1) return -1;  // one thread per rank only
+    return fa_mean_f32_multi(ranks[0]->comm, io[0].c32, c.counts.data(), L.f32_numel,
+                             io[0].out32, L.s32.data(), (int)L.s32.size(), c.root, io[0].stream);
+  }
+  if (c.mode == "multi" || c.mode == "multi_e1")
+    return fa_reduce_multi((fa_multi_plan* const*)plans.data(), nl, io.data(), c.root);
   if (c.mode == "chained")
     return fa_reduce_chained((fa_chain_plan* const*)plans.data(), nl, io.data(), c.root);
   if (c.mode == "striped")
@@ -132,6 +177,10 @@ int run_round(const Case& c, std::vector<void*>& plans, std::vector<fa_shard_io>
 
 void destroy_plan(const Case& c, void* p) {
   if (!p) return;
+  if (c.mode == "multi" || c.mode == "multi_e1") {
+    fa_multi_plan_destroy((fa_multi_plan*)p);
+    return;
+  }
   if (c.mode == "chained") fa_chain_plan_destroy((fa_chain_plan*)p);
   else if (c.mode == "striped") fa_stripe_plan_destroy((fa_stripe_plan*)p);
   else if (c.mode == "blocked") fa_block_plan_destroy((fa_block_plan*)p);
@@ -151,11 +200,12 @@ bool run_case(const Case& c, const Layout& L) {
     HIPC(hipMemset(c32[i], 0, F * 4));
     HIPC(hipMemset(c64[i], 0, I * 8));
     for (size_t k = 0; k < L.s32.size(); ++k)
-      fa_synth_fill_f32(c32[i] + L.s32[k].offset, L.s32[k].numel, (int)k, i, 0.f, 0.05f, 0,
-                        nullptr);
+      fa_synth_fill_f32(c32[i] + L.s32[k].offset, L.s32[k].numel,
+                        L.params ? L.key32[k] : (int)k, i, L.params ? L.mu[k] : 0.f,
+                        L.params ? L.sigma[k] : 0.05f, 0, nullptr);
     for (size_t k = 0; k < L.s64.size(); ++k)
-      fa_synth_fill_i64(c64[i] + L.s64[k].offset, L.s64[k].numel, (int)(1000 + k), i, 0,
-                        nullptr);
+      fa_synth_fill_i64(c64[i] + L.s64[k].offset, L.s64[k].numel,
+                        L.params ? L.key64[k] : (int)(1000 + k), i, 0, nullptr);
   }
   std::vector<float> w(n);
   double ws = 0;
@@ -234,7 +284,8 @@ bool run_case(const Case& c, const Layout& L) {
             k.io.stream = k.st;
             std::vector<void*> plans{k.plan};
             std::vector<fa_shard_io> io{k.io};
-            k.rc = run_round(c, plans, io);
+            std::vector<Rank*> rk{&k};
+            k.rc = run_round(c, L, rk, plans, io);
           }
           if (k.rc) k.err = fa_last_error();
           if (k.st) (void)hipStreamSynchronize(k.st);
@@ -251,6 +302,7 @@ bool run_case(const Case& c, const Layout& L) {
     } else {
       std::vector<void*> plans(W);
       std::vector<fa_shard_io> io(W);
+      std::vector<Rank*> rk(W);
       for (int r = 0; r < W && !failed; ++r) {
         R[r].comm = comms[r];
         R[r].rc = create_plan(c, L, R[r]);
@@ -258,13 +310,14 @@ bool run_case(const Case& c, const Layout& L) {
         R[r].io.stream = R[r].st;
         plans[r] = R[r].plan;
         io[r] = R[r].io;
+        rk[r] = &R[r];
         if (R[r].rc) {
           R[r].err = fa_last_error();
           failed = true;
         }
       }
       if (!failed) {
-        rc = run_round(c, plans, io);
+        rc = run_round(c, L, rk, plans, io);
         if (rc) {
           err = fa_last_error();
           failed = true;
@@ -284,7 +337,9 @@ bool run_case(const Case& c, const Layout& L) {
   std::vector<int64_t> ref_i(I), got_i(I);
   HIPC(hipMemcpy(ref.data(), ref32, F * 4, hipMemcpyDeviceToHost));
   HIPC(hipMemcpy(ref_i.data(), ref64, I * 8, hipMemcpyDeviceToHost));
-  const bool exact = c.mode == "chained" || c.mode == "striped" || c.mode == "blocked";
+  const bool exact = c.mode == "chained" || c.mode == "striped" || c.mode == "blocked" ||
+                     c.mode == "multi" || c.mode == "mean_multi";
+  const bool with64 = c.mode != "mean_multi";
   std::vector<double> bound;
   if (!exact && !failed) {
     // forward error bound: 2N * 2^-24 * sum |w_i x_i| (/N for the mean)
@@ -330,8 +385,17 @@ bool run_case(const Case& c, const Layout& L) {
                std::to_string(first) + ", " + std::to_string(last) + "], " +
                std::to_string(nan) + " unwritten; ";
     for (const fa_seg& s : L.s64)
-      for (int64_t e = s.offset; e < s.offset + s.numel; ++e)
+      for (int64_t e = s.offset; e < s.offset + s.numel && with64; ++e)
         if (got_i[e] != ref_i[e]) ++bad64;
+    const char* dump = getenv("FA_LOOP_DUMP");
+    if (dump && checked == 1) {
+      FILE* df = fopen(dump, "wb");
+      if (df) {
+        fwrite(got.data(), 4, (size_t)F, df);
+        fwrite(got_i.data(), 8, (size_t)I, df);
+        fclose(df);
+      }
+    }
   }
   const bool ok = !failed && bad32 == 0 && bad64 == 0 && checked > 0;
   if (err.empty()) err = where;

@@ -18,10 +18,12 @@ so their single-thread form is left to tests/schedsim.py.  Cases cover
 uneven counts, a rank without clients, every root (first, middle, last, all),
 weighted rounds, 1..13 column chunks, N >= 256 (the deep cascade's four state
 planes) and the layouts of BASELINE configs 3 and 5."""
+import hashlib
 import json
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 from conftest import load_manifest
@@ -34,19 +36,46 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DRIVER = os.path.join(ROOT, "tests", "loopback", "loop_round")
 
 
-def _write_layout(layout, path):
+def _write_layout(layout, path, params=None):
+    """``params``: {offset: (key_index, mu, sigma)} per fp32 segment and
+    {offset: key_index} per int64 one — the digest generator's inputs."""
     with open(path, "w") as f:
         f.write(f"{layout.f32_numel} {layout.i64_numel} {len(layout.segs32)} "
-                f"{len(layout.segs64)}\n")
-        for o, m in list(layout.segs32) + list(layout.segs64):
-            f.write(f"{int(o)} {int(m)}\n")
+                f"{len(layout.segs64)}{' P' if params else ''}\n")
+        for o, m in layout.segs32:
+            extra = ""
+            if params:
+                k, mu, sg = params[0][int(o)]
+                extra = f" {k} {float(np.float32(mu)):.9g} {float(np.float32(sg)):.9g}"
+            f.write(f"{int(o)} {int(m)}{extra}\n")
+        for o, m in layout.segs64:
+            extra = f" {params[1][int(o)]}" if params else ""
+            f.write(f"{int(o)} {int(m)}{extra}\n")
 
 
-def _run(layout, cases, tmp_path, timeout=240):
+def _digest_params(layout, parts):
+    """Per-segment generator parameters of a (joint) layout: key index = the
+    key's position in its own manifest (feddct_amd/workload.py fill_client)."""
+    from feddct_amd import synth
+    p32, p64 = {}, {}
+    for man, prefix in parts:
+        for j, e in enumerate(man["keys"]):
+            s = layout.by_key[prefix + e["key"]]
+            if s.kind == "i64":
+                p64[s.offset] = j
+            else:
+                mu, sg = synth.key_params(e["key"], tuple(e["shape"]), e["dtype"])
+                p32[s.offset] = (j, mu, sg)
+    return p32, p64
+
+
+def _run(layout, cases, tmp_path, timeout=240, params=None, dump=None):
     assert os.path.exists(DRIVER), "tests/loopback/loop_round is not built (run build())"
     lf = str(tmp_path / "layout.txt")
-    _write_layout(layout, lf)
+    _write_layout(layout, lf, params)
     env = dict(os.environ, FA_LOOP_TIMEOUT_S="30")
+    if dump:
+        env["FA_LOOP_DUMP"] = dump
     p = subprocess.run([DRIVER, lf, *cases], capture_output=True, text=True, timeout=timeout,
                        env=env)
     rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
@@ -103,6 +132,14 @@ def test_loopback_small_layout_all_modes(tmp_path):
         "blocked:8:20,20,20,20,20,20,20,20:-1:single:1:0",
         "blocked:6:12,9,30,0,14,8:4:threads:0:0",
         "blocked:3:100,156,44:-1:threads:0:0",            # N=300: the fold's level 2
+        # r05: the default entry picks the exact form from the counts
+        "multi:8:1,2,1,3,1,1,2,9:-1:threads:0:0",          # -> chained
+        "multi:3:7,0,13:-1:threads:1:0",                   # -> blocked
+        "multi:2:10,10:0:single:0:0",                      # -> blocked, one thread
+        "multi:4:65,65,65,65:3:threads:1:0",               # N=260 -> chained, 4 planes
+        "multi_e1:4:5,0,2,1:-1:threads:1:4",               # opt-in e1: error bound
+        "mean_multi:3:4,5,3:2:threads:0:0",                # stateless fp32 form
+        "mean_multi:8:3,3,3,3,3,3,3,3:-1:threads:0:0",
     ]
     _run(_small_layout(), cases, tmp_path)
 
@@ -143,3 +180,37 @@ def test_loopback_blocked_bench_shape(tmp_path):
              "blocked:8:20,20,20,20,20,20,20,20:0:threads:0:0",
              "blocked:8:20,20,20,20,20,20,20,20:-1:threads:0:0"]
     _run(lay, cases, tmp_path, timeout=300)
+
+
+def test_loopback_cfg5_default_entry_matches_reference_digest(tmp_path):
+    """the DEFAULT multi-GPU entry (fa_multi_plan_create /
+    fa_reduce_multi — no form named by the caller) on BASELINE config 5's
+    shape, 24 FedDCT slots (wrnsl16_8 sf4 C100, main + proxy in one bucket)
+    over 8 ranks of 3 slots, with the digest generator's inputs: the result
+    rank's main and proxy halves hash to the digests the REFERENCE's own
+    server_aggregate produced (tests/golden/digests.json, n24), and equal one
+    GPU's reduction bit for bit.  With 3 slots per rank a 16-slot cascade
+    block spans 6 ranks, so the entry must take the chained round."""
+    from feddct_amd import dist
+    mm, pm = load_manifest("wrnsl16_8_sf4_c100_main"), load_manifest("wrnsl16_8_sf4_c100_proxy")
+    lay = BucketLayout.from_manifest(joint_manifest([mm, pm]))
+    assert dist.exact_form([3] * 8) == "chained"
+    params = _digest_params(lay, [(mm, "0."), (pm, "1.")])
+    dump = str(tmp_path / "out.bin")
+    rows = _run(lay, ["multi:8:3,3,3,3,3,3,3,3:7:threads:0:0"], tmp_path, timeout=300,
+                params=params, dump=dump)
+    assert rows[0]["check"] == "bit-exact"
+    raw = open(dump, "rb").read()
+    f32 = np.frombuffer(raw[:4 * lay.f32_numel], np.float32)
+    i64 = np.frombuffer(raw[4 * lay.f32_numel:], np.int64)
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        want = json.load(f)
+    for prefix, name in (("0.", "main"), ("1.", "proxy")):
+        h = hashlib.sha256()
+        for s in lay.slots:
+            if not s.key.startswith(prefix):
+                continue
+            src = i64 if s.kind == "i64" else f32
+            h.update(s.key[len(prefix):].encode())
+            h.update(np.ascontiguousarray(src[s.offset:s.offset + s.numel]).tobytes())
+        assert h.hexdigest() == want[f"feddct/wrnsl16_8_sf4_c100_{name}/n24"], name
