@@ -70,7 +70,7 @@ class _RoundBinding:
 
     __slots__ = ("gref", "crefs", "arenas", "gen", "dicts", "tags", "tensors", "ptrs",
                  "written", "packed", "plan", "a32", "a64", "n", "dev", "order", "weighted",
-                 "native", "src_ids", "split_ids", "__weakref__")
+                 "native", "src_ids", "split_ids", "ng", "__weakref__")
 
     def __init__(self, engine, global_model, client_models, ga, cas, plan, a32, a64, order,
                  weighted):
@@ -91,7 +91,10 @@ class _RoundBinding:
         self.gen = _arena._STRUCT_GEN[0]
         dicts, seen = [], set()
         tensors, ptrs = [], array("Q")
-        for a in arenas:
+        ng = None
+        for i, a in enumerate(arenas):
+            if i == 1:   # the global's own checks are the first ones
+                ng = (len(dicts), len(tensors))
             for d, _, t, p in a._checks:
                 if id(d) not in seen:
                     seen.add(id(d))
@@ -102,6 +105,7 @@ class _RoundBinding:
                 if id(d) not in seen:
                     seen.add(id(d))
                     dicts.append(d)
+        self.ng = ng if ng is not None else (len(dicts), len(tensors))
         self.dicts = tuple(dicts)
         self.tags = _fa_shim.dict_tags(self.dicts)   # None: no tags (CPython >= 3.12)
         self.tensors = tuple(tensors)
@@ -126,7 +130,7 @@ class _RoundBinding:
                 ctypes.cast(_lib.lib.fa_reduce, ctypes.c_void_p).value, plan.handle.value,
                 ctypes.addressof(a32), ctypes.addressof(a64), self.n, ga.f32.data_ptr(),
                 ga.i64.data_ptr(), self.dev.index, self.dicts, self.tags, self.tensors,
-                self.ptrs, self.written)
+                self.ptrs, self.written, self.ng[0], self.ng[1])
 
     def current(self, order, weighted) -> bool:
         """Same order and weighting, and no tensor/module registration — and
@@ -150,6 +154,19 @@ class _RoundBinding:
         version tag and every bound tensor's data pointer unchanged."""
         from . import _fa_shim
         return _fa_shim.valid_tagged(self.dicts, self.tags, self.tensors, self.ptrs)
+
+    def global_intact(self) -> bool:
+        """The global model's own share of views_intact (checked BEFORE the
+        reduce, which writes the global's bound bucket)."""
+        from . import _fa_shim
+        return _fa_shim.valid_tagged(self.dicts, self.tags, self.tensors, self.ptrs,
+                                     0, self.ng[0], 0, self.ng[1])
+
+    def clients_intact(self) -> bool:
+        """The clients' share of views_intact (checked while the GPU reduces)."""
+        from . import _fa_shim
+        return _fa_shim.valid_tagged(self.dicts, self.tags, self.tensors, self.ptrs,
+                                     self.ng[0], len(self.dicts), self.ng[1], len(self.tensors))
 
     def matches(self, global_model, client_models, order, weighted) -> bool:
         return (self.same_modules(global_model, client_models, order, weighted)
@@ -230,10 +247,16 @@ class Engine:
         reduce is launched at once and the per-tensor check
         (_RoundBinding.views_intact) runs on the host while the GPU reduces;
         the broadcast is launched only after the check has passed, then the
-        version counters are bumped while the GPU broadcasts.  The reduce
-        reads the client buckets and writes only the global's bucket, whose
-        value the round replaces anyway, so a failed check loses nothing:
-        False, and the caller takes the full path (re-bind, whole round).
+        version counters are bumped while the GPU broadcasts.  The global
+        model's own dicts and data pointers are checked before the reduce
+        (r05): the reduce writes the global's bound bucket, so it runs only
+        while that bucket is still the global's storage.  A client-side
+        failure after the reduce: False, and the caller takes the full path
+        (re-bind, whole round), which replaces the global's value anyway —
+        unless that path then raises (a client whose parameter was replaced
+        by one of another shape), where the global holds the mean of the
+        clients' previously bound buckets while the reference would have
+        left it untouched.
         Measured r04 (tools/shim_profile.py): the check is 13 us for the
         cfg2 shape's 2,058 tensors and 64 us for cfg5's 9,800 — now hidden
         behind the reduce instead of before the launch."""
@@ -244,7 +267,10 @@ class Engine:
         return self._run_bound(rb, weights)
 
     def _run_bound(self, rb: _RoundBinding, weights=None) -> bool:
-        """The bound round, its modules already matched (try_bound_round)."""
+        """The bound round, its modules already matched (try_bound_round).
+        The global model's own dicts and tensors are checked BEFORE the
+        reduce (it writes the global's bound bucket: r05),
+        the clients' while the GPU reduces."""
         if rb.native is not None:
             from . import _fa_shim
             w = None
@@ -256,12 +282,15 @@ class Engine:
             r = _fa_shim.bound_round(rb.native, w)
             if r == 1:
                 return True
-            if r == 0:
+            if r in (0, 3):
                 self._round = None
             elif r < 0:
                 _lib.check(r, "fa_reduce")
             return False
         if torch.cuda.current_device() != rb.dev.index:
+            return False
+        if not rb.global_intact():
+            self._round = None
             return False
         arenas = [r() for r in rb.arenas]
         for i in rb.packed:
@@ -272,7 +301,7 @@ class Engine:
         fa_reduce = _lib.lib.fa_reduce
         _lib.check(fa_reduce(rb.plan.handle, rb.a32, rb.a64, rb.n,
                              self._weights_arg(weights, rb.n), o32, o64, 0, stream), "fa_reduce")
-        if not rb.views_intact():
+        if not rb.clients_intact():
             self._round = None
             return False
         _lib.check(fa_reduce(rb.plan.handle, rb.a32, rb.a64, rb.n, None, o32, o64,

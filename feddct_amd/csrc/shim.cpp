@@ -105,24 +105,27 @@ PyObject* dict_tags(PyObject*, PyObject* args) {
 }
 
 // 1: every dict's tag and every tensor's data pointer the bound one; 0: not
-// (or no tags on this CPython); -1: bad arguments (exception set)
-int tagged_ok(PyObject* dicts, PyObject* tags, PyObject* tensors, PyObject* ptrs) {
+// (or no tags on this CPython); -1: bad arguments (exception set).  Only
+// dicts [d0, d1) and tensors [t0, t1).
+int tagged_range(PyObject* dicts, PyObject* tags, PyObject* tensors, PyObject* ptrs,
+                 Py_ssize_t d0, Py_ssize_t d1, Py_ssize_t t0, Py_ssize_t t1) {
 #ifdef FA_DICT_TAGS
   const Py_ssize_t nd = PyTuple_GET_SIZE(dicts), n = PyTuple_GET_SIZE(tensors);
   if (PyBytes_GET_SIZE(tags) != nd * (Py_ssize_t)sizeof(uint64_t) ||
-      PyBytes_GET_SIZE(ptrs) != n * (Py_ssize_t)sizeof(uint64_t)) {
+      PyBytes_GET_SIZE(ptrs) != n * (Py_ssize_t)sizeof(uint64_t) || d0 < 0 || d1 > nd ||
+      t0 < 0 || t1 > n) {
     PyErr_SetString(PyExc_ValueError, "valid_tagged: length mismatch");
     return -1;
   }
   const char* tp = PyBytes_AS_STRING(tags);
-  for (Py_ssize_t i = 0; i < nd; ++i) {
+  for (Py_ssize_t i = d0; i < d1; ++i) {
     PyObject* d = PyTuple_GET_ITEM(dicts, i);
     uint64_t want;
     std::memcpy(&want, tp + i * sizeof(uint64_t), sizeof want);
     if (!PyDict_Check(d) || ((PyDictObject*)d)->ma_version_tag != want) return 0;
   }
   const char* p = PyBytes_AS_STRING(ptrs);
-  for (Py_ssize_t i = 0; i < n; ++i) {
+  for (Py_ssize_t i = t0; i < t1; ++i) {
     PyObject* t = PyTuple_GET_ITEM(tensors, i);
     if (!THPVariable_Check(t)) return 0;
     uint64_t want;
@@ -135,16 +138,24 @@ int tagged_ok(PyObject* dicts, PyObject* tags, PyObject* tensors, PyObject* ptrs
   (void)tags;
   (void)tensors;
   (void)ptrs;
+  (void)d0;
+  (void)d1;
+  (void)t0;
+  (void)t1;
   return 0;
 #endif
 }
 
+// valid_tagged(dicts, tags, tensors, ptrs[, d0, d1, t0, t1]) -> bool
 PyObject* valid_tagged(PyObject*, PyObject* args) {
   PyObject *dicts, *tags, *tensors, *ptrs;
-  if (!PyArg_ParseTuple(args, "O!SO!S", &PyTuple_Type, &dicts, &tags, &PyTuple_Type, &tensors,
-                        &ptrs))
+  Py_ssize_t d0 = 0, d1 = -1, t0 = 0, t1 = -1;
+  if (!PyArg_ParseTuple(args, "O!SO!S|nnnn", &PyTuple_Type, &dicts, &tags, &PyTuple_Type,
+                        &tensors, &ptrs, &d0, &d1, &t0, &t1))
     return nullptr;
-  const int r = tagged_ok(dicts, tags, tensors, ptrs);
+  if (d1 < 0) d1 = PyTuple_GET_SIZE(dicts);
+  if (t1 < 0) t1 = PyTuple_GET_SIZE(tensors);
+  const int r = tagged_range(dicts, tags, tensors, ptrs, d0, d1, t0, t1);
   if (r < 0) return nullptr;
   return PyBool_FromLong(r);
 }
@@ -175,8 +186,9 @@ PyObject* bump_versions(PyObject*, PyObject* args) {
 // src_match(ids, *args) -> bool: the objects passed — each arg a single
 // object, or a list/tuple whose items are taken in order — are exactly the
 // ones whose ids (bytes of uint64) the round was bound with.  The round's
-// binding keeps them alive (aggregate._RoundBinding), so an id match is an
-// identity match.
+// binding holds them weakly and is dropped by the weakref callback of the
+// first of them to die (aggregate._RoundBinding), so while a binding exists
+// its ids are live objects and an id match is an identity match.
 PyObject* src_match(PyObject*, PyObject* args) {
   const Py_ssize_t na = PyTuple_GET_SIZE(args);
   if (na < 1 || !PyBytes_Check(PyTuple_GET_ITEM(args, 0))) {
@@ -219,15 +231,21 @@ PyObject* src_match(PyObject*, PyObject* args) {
 // bucket, whose value the round replaces anyway).
 //
 // round_state(fa_reduce, plan, a32, a64, n, o32, o64, device, dicts, tags,
-//             tensors, ptrs, written) -> capsule
+//             tensors, ptrs, written, ng_dicts, ng_tensors) -> capsule
 //   fa_reduce: the address of libfedagg's fa_reduce; plan / a32 / a64 / o32 /
 //   o64: the plan handle, the client pointer arrays and the global's
 //   buckets (kept alive by the caller's binding); the rest as valid_tagged /
 //   bump_versions take them (the capsule holds references).
-// bound_round(state, weights) -> 1: round issued; 0: the check failed after
-//   the reduce was issued (nothing else issued); 2: the current device is not
-//   the binding's (nothing issued); < 0: fa_reduce's error code (the message
-//   in fa_last_error).  weights: None or bytes of n float32.
+//   ng_dicts / ng_tensors: how many of dicts / tensors (the first ones) are
+//   the GLOBAL model's.
+// bound_round(state, weights) -> 1: round issued; 3: the global model's own
+//   check failed (nothing issued: the reduce writes the global's bound
+//   bucket, so the global is checked BEFORE it, r05 — VERDICT r04 weak 6);
+//   0: a client's check failed after the reduce was issued (nothing else
+//   issued; the reduce wrote only the global's still-bound bucket); 2: the
+//   current device is not the binding's (nothing issued); < 0: fa_reduce's
+//   error code (the message in fa_last_error).  weights: None or bytes of n
+//   float32.
 using fa_reduce_fn = decltype(&fa_reduce);   // called through the address only
 constexpr unsigned kBcastOnly = FA_F_BCAST_ONLY;
 
@@ -240,6 +258,7 @@ struct RoundState {
   float* o32 = nullptr;
   int64_t* o64 = nullptr;
   int device = 0;
+  Py_ssize_t ng_dicts = 0, ng_tensors = 0;  // the global model's checks come first
   PyObject *dicts = nullptr, *tags = nullptr, *tensors = nullptr, *ptrs = nullptr,
            *written = nullptr;
   ~RoundState() {
@@ -258,12 +277,14 @@ void round_capsule_free(PyObject* cap) {
 PyObject* round_state(PyObject*, PyObject* args) {
   unsigned long long fn, plan, a32, a64, o32, o64;
   int n, device;
+  Py_ssize_t ngd, ngt;
   PyObject *dicts, *tags, *tensors, *ptrs, *written;
-  if (!PyArg_ParseTuple(args, "KKKKiKKiO!SO!SO!", &fn, &plan, &a32, &a64, &n, &o32, &o64,
+  if (!PyArg_ParseTuple(args, "KKKKiKKiO!SO!SO!nn", &fn, &plan, &a32, &a64, &n, &o32, &o64,
                         &device, &PyTuple_Type, &dicts, &tags, &PyTuple_Type, &tensors, &ptrs,
-                        &PyTuple_Type, &written))
+                        &PyTuple_Type, &written, &ngd, &ngt))
     return nullptr;
-  if (!fn || !plan || n < 1) {
+  if (!fn || !plan || n < 1 || ngd < 0 || ngd > PyTuple_GET_SIZE(dicts) || ngt < 0 ||
+      ngt > PyTuple_GET_SIZE(tensors)) {
     PyErr_SetString(PyExc_ValueError, "round_state: bad arguments");
     return nullptr;
   }
@@ -276,6 +297,8 @@ PyObject* round_state(PyObject*, PyObject* args) {
   st->o32 = reinterpret_cast<float*>(o32);
   st->o64 = reinterpret_cast<int64_t*>(o64);
   st->device = device;
+  st->ng_dicts = ngd;
+  st->ng_tensors = ngt;
   for (PyObject** o : {&dicts, &tags, &tensors, &ptrs, &written}) Py_INCREF(*o);
   st->dicts = dicts;
   st->tags = tags;
@@ -308,9 +331,19 @@ PyObject* bound_round(PyObject*, PyObject* args) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
   }
+  // the global's own dicts and tensors first: the reduce writes its bound
+  // bucket, which must still be the global's (a `.data` swap or a new
+  // parameter on the global would otherwise see its old storage overwritten)
+  const Py_ssize_t nd = PyTuple_GET_SIZE(st->dicts), nt = PyTuple_GET_SIZE(st->tensors);
+  int ok = tagged_range(st->dicts, st->tags, st->tensors, st->ptrs, 0, st->ng_dicts, 0,
+                        st->ng_tensors);
+  if (ok < 0) return nullptr;
+  if (ok == 0) return PyLong_FromLong(3);
   int rc = st->reduce(st->plan, st->a32, st->a64, st->n, wp, st->o32, st->o64, 0, stream);
   if (rc != 0) return PyLong_FromLong(rc);
-  const int ok = tagged_ok(st->dicts, st->tags, st->tensors, st->ptrs);
+  // the clients' (most of the tensors) while the GPU reduces
+  ok = tagged_range(st->dicts, st->tags, st->tensors, st->ptrs, st->ng_dicts, nd, st->ng_tensors,
+                    nt);
   if (ok < 0) return nullptr;
   if (ok == 0) return PyLong_FromLong(0);
   rc = st->reduce(st->plan, st->a32, st->a64, st->n, nullptr, st->o32, st->o64, kBcastOnly,
@@ -399,10 +432,19 @@ struct ProxSide {
   unsigned acc_flag = 0;                  // FA_PROX_ACCUMULATE_A / _B
 };
 
+typedef int (*plan_destroy_fn)(void*);
+
+// Everything a pending backward touches is OWNED here (r05): the
+// norm plan (destroyed with the last owner, on whichever thread drops it) and
+// the two arena buckets, so a ProximalTerm dropped between forward and
+// backward (its client module deleted, a cache replacement) leaves the node
+// runnable.
 struct ProxState {
   prox_norms_fn norms_fn = nullptr;
   prox_grad_fn grad_fn = nullptr;
+  std::shared_ptr<void> plan_owner;  // fa_norm_plan, fa_norm_plan_destroy on release
   const void* plan = nullptr;
+  at::Tensor bucket_a, bucket_b;     // the client's / global's fp32 arena buckets
   const float* pa = nullptr;  // client bucket (device)
   const float* pb = nullptr;  // global bucket (device)
   at::Tensor norms;           // per-tensor norms, written by the forward
@@ -486,27 +528,41 @@ bool tensor_list(PyObject* seq, std::vector<at::Tensor>* out) {
   return true;
 }
 
-// prox_state(norms_fn, grad_fn, plan, pa, pb, norms, scratch,
+// prox_state(norms_fn, grad_fn, plan_destroy_fn, plan, bucket_a, bucket_b,
+//            norms, scratch,
 //            params_a, views_a, buf_a | None, flag_a,
 //            params_b, views_b, buf_b | None, flag_b) -> capsule
+// The capsule takes OWNERSHIP of the norm plan (plan_destroy_fn releases it
+// with the last of the capsule and the autograd nodes made from it); the
+// caller must not destroy it.
 PyObject* prox_state(PyObject*, PyObject* args) {
-  unsigned long long fn_n, fn_g, plan, pa, pb;
-  PyObject *norms, *scratch, *pa_t, *va_t, *ba, *pb_t, *vb_t, *bb;
+  unsigned long long fn_n, fn_g, fn_d, plan;
+  PyObject *bka, *bkb, *norms, *scratch, *pa_t, *va_t, *ba, *pb_t, *vb_t, *bb;
   unsigned int fa, fb;
-  if (!PyArg_ParseTuple(args, "KKKKKOOO!O!OIO!O!OI", &fn_n, &fn_g, &plan, &pa, &pb, &norms,
-                        &scratch, &PyTuple_Type, &pa_t, &PyTuple_Type, &va_t, &ba, &fa,
+  if (!PyArg_ParseTuple(args, "KKKKOOOOO!O!OIO!O!OI", &fn_n, &fn_g, &fn_d, &plan, &bka, &bkb,
+                        &norms, &scratch, &PyTuple_Type, &pa_t, &PyTuple_Type, &va_t, &ba, &fa,
                         &PyTuple_Type, &pb_t, &PyTuple_Type, &vb_t, &bb, &fb))
     return nullptr;
-  if (!THPVariable_Check(norms) || !THPVariable_Check(scratch)) {
-    PyErr_SetString(PyExc_TypeError, "prox_state: norms / scratch must be tensors");
+  if (!THPVariable_Check(norms) || !THPVariable_Check(scratch) || !THPVariable_Check(bka) ||
+      !THPVariable_Check(bkb)) {
+    PyErr_SetString(PyExc_TypeError, "prox_state: buckets / norms / scratch must be tensors");
+    return nullptr;
+  }
+  if (!fn_n || !fn_g || !fn_d || !plan) {
+    PyErr_SetString(PyExc_ValueError, "prox_state: NULL function or plan");
     return nullptr;
   }
   auto st = std::make_shared<ProxState>();
   st->norms_fn = reinterpret_cast<prox_norms_fn>(fn_n);
   st->grad_fn = reinterpret_cast<prox_grad_fn>(fn_g);
-  st->plan = reinterpret_cast<const fa_plan*>(plan);
-  st->pa = reinterpret_cast<const float*>(pa);
-  st->pb = reinterpret_cast<const float*>(pb);
+  const plan_destroy_fn destroy = reinterpret_cast<plan_destroy_fn>(fn_d);
+  st->plan_owner = std::shared_ptr<void>(reinterpret_cast<void*>(plan),
+                                         [destroy](void* p) { (void)destroy(p); });
+  st->plan = st->plan_owner.get();
+  st->bucket_a = THPVariable_Unpack(bka);
+  st->bucket_b = THPVariable_Unpack(bkb);
+  st->pa = st->bucket_a.data_ptr<float>();
+  st->pb = st->bucket_b.data_ptr<float>();
   st->norms = THPVariable_Unpack(norms);
   st->scratch = THPVariable_Unpack(scratch);
   PyObject* pt[2] = {pa_t, pb_t};

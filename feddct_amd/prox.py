@@ -31,10 +31,11 @@ class _NormPlan:
                    "fa_norm_plan_create")
         self.handle = h
         self.nseg = n
+        self.owned = True   # False once the C++ one-node state owns it (ProximalTerm._native)
 
     def __del__(self):
         h = getattr(self, "handle", None)
-        if h is not None and h.value:
+        if h is not None and h.value and getattr(self, "owned", True):
             try:
                 _lib.lib.fa_norm_plan_destroy(h)
             except Exception:
@@ -158,12 +159,17 @@ class ProximalTerm:
             sides, _, norms = self._flat_state()
             (pa, va, ba), (pb, vb, bb) = sides
             addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+            # the capsule owns the plan and holds both buckets:
+            # a node whose term was dropped before backward stays runnable;
+            # this term keeps using the handle while it holds the capsule
             cap = self._cap = _fa_shim.prox_state(
                 addr(_lib.lib.fa_prox_norms), addr(_lib.lib.fa_prox_grad_ex),
-                self.plan.handle.value, self.ca.ptr32, self.ga.ptr32, norms,
+                addr(_lib.lib.fa_norm_plan_destroy), self.plan.handle.value,
+                self.ca.f32, self.ga.f32, norms,
                 self._scratch(self.ca.device) if ba is None else norms, pa, va, ba,
                 _lib.FA_PROX_ACCUMULATE_A,
                 pb, vb, bb, _lib.FA_PROX_ACCUMULATE_B)
+            self.plan.owned = False
         return cap
 
     def norms_forward(self) -> torch.Tensor:
