@@ -282,20 +282,54 @@ def pmc_traffic(n_gpus):
     return None, None
 
 
+def cpu_quota() -> dict:
+    """The process's CPU share as the kernel enforces it: the cgroup CPU
+    quota (v2 cpu.max or v1 cfs_quota_us / cfs_period_us), the cpuset and the
+    affinity mask (a container sees the whole machine's CPUs in both of the
+    latter, the quota is what it gets)."""
+    out = {"affinity_cpus": len(os.sched_getaffinity(0)), "host_cpus": os.cpu_count()}
+
+    def rd(path):
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            return None
+    v2 = rd("/sys/fs/cgroup/cpu.max")
+    if v2:
+        q, _, per = v2.partition(" ")
+        out["cgroup"] = f"v2 cpu.max = {v2}"
+        if q != "max":
+            out["quota_cpus"] = round(int(q) / int(per or 100000), 2)
+    else:
+        q = rd("/sys/fs/cgroup/cpu/cpu.cfs_quota_us")
+        per = rd("/sys/fs/cgroup/cpu/cpu.cfs_period_us")
+        if q is not None:
+            out["cgroup"] = f"v1 cfs_quota_us = {q}, cfs_period_us = {per}"
+            if int(q) > 0 and per:
+                out["quota_cpus"] = round(int(q) / int(per), 2)
+    cs = rd("/sys/fs/cgroup/cpuset.cpus.effective") or rd("/sys/fs/cgroup/cpuset/cpuset.cpus")
+    if cs:
+        out["cpuset"] = cs
+    out["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
+    return out
+
+
+CPU_THREADS = (1, 8, 16, 32, 64)
+
+
 def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
+    """The reference loop (oracle/torch_mirror.py, train_fedavg.py:138-149)
+    on this box's host cores, at torch intra-op thread counts 1, 8, 16, 32
+    and 64: value = the BEST count's rate.  The sweep
+    goes up in threads and stops once a count runs 3x slower than the best so
+    far (past the CPU quota the loop collapses: r02, 256 threads on a 16-CPU
+    share ran 160x slower)."""
     from oracle.torch_mirror import arithmetic_core, reference_loop, time_call
 
-    # The box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool).  The
-    # affinity mask lists every core of the machine (256), but the process
-    # only gets its share: measured r02, the loop at 256 torch threads took
-    # 64.1 s against 0.40 s at 16 (profiles/r02_cpu_threads.json), so the
-    # baseline runs on the share, and on 1 thread.
-    all_cores = len(os.sched_getaffinity(0))
-    share = int(os.environ.get("OMP_NUM_THREADS", all_cores) or all_cores)
-    counts = [max(1, min(share, all_cores))]
-    threads = counts[0]
-    torch.set_num_threads(threads)
-
+    quota = cpu_quota()
+    all_cores = quota["affinity_cpus"]
+    counts = [c for c in CPU_THREADS if c <= all_cores]
     Holder = _holder_class(layout)
 
     def to_module(f32, i64):
@@ -310,8 +344,13 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
 
     mods = [to_module(f, i) for f, i in clients]
     g = Holder()
-    by_threads = {}
+    by_threads, skipped = {}, []
     for th in counts:
+        if by_threads:
+            last = by_threads[max(by_threads)][0]
+            if last > 3 * min(v[0] for v in by_threads.values()):
+                skipped.append(th)
+                continue
         torch.set_num_threads(th)
         tl, rp = time_call(lambda: reference_loop(g, mods), 5, budget_s * 0.5 / len(counts))
         by_threads[th] = (tl, rp)
@@ -332,7 +371,8 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
     del fd
     # the same on one thread (SURVEY.md §8 d asks for both)
     torch.set_num_threads(1)
-    t_loop1, reps1 = time_call(lambda: reference_loop(g, mods), 3, budget_s * 0.3)
+    t_loop1, reps1 = by_threads[1] if 1 in by_threads else time_call(
+        lambda: reference_loop(g, mods), 3, budget_s * 0.3)
     t_core1, _ = time_call(lambda: arithmetic_core(states), 3, budget_s * 0.1)
     torch.set_num_threads(threads)
     nbytes = layout.algorithmic_bytes(len(clients))
@@ -349,9 +389,11 @@ def run_cpu_baseline(layout, manifest, clients, budget_s=25.0):
             "cfg1_n2": {"loop_ms": round(t_cfg1 * 1e3, 2), "runs": reps_cfg1},
             "cfg3_feddct_n5": {"loop_ms": round(t_fd * 1e3, 2), "runs": reps_fd},
             "loop_ms_by_threads": {str(k): round(v[0] * 1e3, 2) for k, v in by_threads.items()},
-            "threads_note": (f"torch intra-op threads = the box's CPU share ({share}; the "
-                             f"affinity mask shows {all_cores} but 256 threads ran the loop "
-                             "160x slower, r02), and 1 thread"),
+            "threads_skipped": skipped,
+            "best_threads": threads,
+            "threads_note": ("torch intra-op threads swept over 1/8/16/32/64 (stopping once a "
+                             "count runs 3x slower than the best); value = the best count"),
+            "cpu_quota": quota,
             "host_cpus": os.cpu_count(), "affinity_cpus": all_cores, "cpu": _cpu_model()}
 
 
@@ -506,8 +548,9 @@ def round_block(layout, clients, out32, out64, plan, extra, k=40):
         "bcast_alone_frac": round(bc_bytes / t_alone / 1e9 / HBM_PEAK_GBS, 4),
         "write_ceiling_GBps": round(wceil, 1),
         "write_ceiling_probe": (f"fa_write_probe_f32: {n} x {numel} floats of hashed register "
-                                "values into the client buckets, the broadcast's launch shape "
-                                "(1024-float parts, groups of <= 24), best of 3 passes"),
+                                "values into the client buckets, the shipped broadcast's launch "
+                                "shape (1024-float parts, client groups of <= 24, sc1 nt "
+                                "stores), best of 3 passes"),
     }
     if rceil:
         # the time the round's bytes take at this box's read and write ceilings
@@ -621,31 +664,24 @@ def other_configs(dev, steps=100, warmup=20):
                 d.startswith("weighted/") for d in digests.values())
                 else "bit_exact_vs_weighted_definition_digest"] = bool(ok)
         # the whole round: reduce + broadcast over the
-        # same rotated sets, as the product launches it (two launches), and
-        # the single-pass form (FA_F_BCAST inside the reduce) beside it
+        # same rotated sets, as the product launches it (two launches; the
+        # single-pass form measured slower on every layout, r04, and was
+        # removed in r05: DESIGN §4.2)
         rb_bytes = sum(r[2].algorithmic_bytes(r[3]) + (r[3] + 1) * r[2].state_bytes()
                        for r in sets[0])
-        for key, pflags in (("round", 0), ("round_fused", _lib.FA_PLAN_TUNE_FUSED_BCAST)):
-            rsets = []
-            for reds in sets:
-                rr = []
-                for names, prefixes, lay, n, red, o32, o64 in reds:
-                    plan = red.plan if pflags == 0 else _lib.Plan(
-                        lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
-                        flags=_lib.FA_PLAN_GAPS_ARE_PADDING | pflags)
-                    rr.append(Reducer(lay, red._keep[0], o32, o64,
-                                      weights=None if red.w is None else list(red.w),
-                                      flags=_lib.FA_F_BCAST, plan=plan))
-                rsets.append(rr)
-            kr = [0]
+        rsets = [[Reducer(lay, red._keep[0], o32, o64,
+                          weights=None if red.w is None else list(red.w),
+                          flags=_lib.FA_F_BCAST, plan=red.plan)
+                  for names, prefixes, lay, n, red, o32, o64 in reds] for reds in sets]
+        kr = [0]
 
-            def rstep(rsets=rsets, kr=kr):
-                for r in rsets[kr[0] % rot]:
-                    r()
-                kr[0] += 1
-            tr, _ = timed_launches(rstep, steps, warmup)
-            out[f"{key}_us"] = round(tr * 1e6, 1)
-            out[f"{key}_frac"] = round(rb_bytes / tr / 1e9 / HBM_PEAK_GBS, 4)
+        def rstep():
+            for r in rsets[kr[0] % rot]:
+                r()
+            kr[0] += 1
+        tr, _ = timed_launches(rstep, steps, warmup)
+        out["round_us"] = round(tr * 1e6, 1)
+        out["round_frac"] = round(rb_bytes / tr / 1e9 / HBM_PEAK_GBS, 4)
         out["round_algorithmic_bytes"] = rb_bytes
         res[name] = out
 
@@ -1631,6 +1667,13 @@ def main():
             extra["round"] = round_block(layout, clients, out32, out64, reducer.plan,
                                          extra, max(20, args.steps // 2))
             extra["round_with_broadcast_us"] = extra["round"]["us"]
+            # the write probe overwrote the client buckets: their synthetic
+            # state again, for the drop-in timings and the CPU baseline below
+            # 
+            from feddct_amd.workload import fill_client
+            for j, (c32, c64) in enumerate(clients):
+                fill_client(layout, manifest, c32, c64, first + j)
+            torch.cuda.synchronize()
             extra["dropin"] = dropin_timing(layout, clients, dev)
             try:
                 extra["dropin_feddct_cfg3"] = dropin_feddct_timing(dev)

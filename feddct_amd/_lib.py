@@ -35,42 +35,14 @@ FA_PROX_ACCUMULATE = 1
 FA_PROX_ACCUMULATE_A = 2
 FA_PROX_ACCUMULATE_B = 4
 FA_PLAN_GAPS_ARE_PADDING = 1
-FA_PLAN_TUNE_NO_NT = 2
 FA_PLAN_TUNE_BATCH8 = 4
 FA_PLAN_TUNE_BATCH16 = 8
-FA_PLAN_TUNE_XCD = 16
-FA_PLAN_TUNE_WAVE_CONTIG = 32
-FA_PLAN_TUNE_ST_PLAIN = 64
-FA_PLAN_TUNE_LD_PLAIN = 128
-FA_PLAN_TUNE_ST_SC1 = 0x10000
-FA_PLAN_TUNE_BATCH1 = 0x20000
-FA_PLAN_TUNE_BATCH4 = 0x40000
-FA_PLAN_TUNE_FUSED_BCAST = 0x80000
-FA_PLAN_TUNE_ISSUE_ALL = 0x100000
-FA_PLAN_TUNE_TGPU_NARROW = 0x200000
-FA_PLAN_TUNE_BCAST_TILES = 0x400000
-FA_PLAN_TUNE_BCAST_TABLE = 0x800000
-FA_PLAN_TUNE_ST_NT = 0x1000000
-FA_PLAN_TUNE_BCAST_XCD = 0x2000000
 FA_PLAN_TUNE_NO_BALANCE = 0x10000000
-FA_PLAN_TUNE_BCAST_R03 = 0x20000000
-FA_PLAN_TUNE_BCAST_U2 = 0x40000000
-FA_PLAN_TUNE_BCAST_G10 = 0x80000000
+# every other plan flag bit is refused by the library since r05 (fedagg.h)
+FA_PLAN_FLAGS_KNOWN = FA_PLAN_GAPS_ARE_PADDING | FA_PLAN_TUNE_BATCH8 | FA_PLAN_TUNE_BATCH16 \
+    | FA_PLAN_TUNE_NO_BALANCE
 FA_ORDER_TORCH_CPU = 0
 FA_ORDER_TORCH_GPU = 1
-
-
-def FA_PLAN_TUNE_BLOCKS_PER_CU(c):
-    return (int(c) & 0xF) << 8
-
-
-def FA_PLAN_TUNE_PACK(c):
-    return (int(c) & 3) << 26
-
-
-def FA_PLAN_TUNE_PERSIST(k):
-    return (int(k) & 0xF) << 12
-
 
 
 EXPORTS = [
@@ -80,7 +52,7 @@ EXPORTS = [
     "fa_synth_fill_f32", "fa_synth_fill_i64", "fa_copy_f32",
     "fa_norm_plan_create", "fa_norm_plan_destroy", "fa_prox_norms", "fa_prox_grad",
     "fa_prox_grad_ex",
-    "fa_read_probe_f32", "fa_write_probe_f32", "fa_tune_bcast_store", "fa_tune_prox_store", "fa_tune_prox_cpw", "fa_tune_tgpu_batch", "fa_chain_levels", "fa_reduce_chain", "fa_torch_gpu_config",
+    "fa_read_probe_f32", "fa_write_probe_f32", "fa_tune_prox_store", "fa_tune_prox_cpw", "fa_chain_levels", "fa_reduce_chain", "fa_torch_gpu_config",
     "fa_plan_create_order", "fa_table_bytes", "fa_reduce_tab",
     "fa_plan_balance_host", "fa_plan_launch_shape",
 ]
@@ -148,10 +120,8 @@ def _load():
         "fa_copy_f32": (_I, [_P, _P, _I64, _P]),
         "fa_read_probe_f32": (_I, [_P, _I64, _P, _I, _P]),
         "fa_write_probe_f32": (_I, [_P, _I, _I64, ctypes.c_uint, _P]),
-        "fa_tune_bcast_store": (_I, [_I]),
         "fa_tune_prox_store": (_I, [_I]),
         "fa_tune_prox_cpw": (_I, [_I]),
-        "fa_tune_tgpu_batch": (_I, [_I]),
         "fa_chain_levels": (ctypes.c_uint, [_I, _I]),
         "fa_torch_gpu_config": (_I, [_I, _I64, ctypes.POINTER(_I)]),
         "fa_plan_create_order": (_I, [_P, _I, _I64, _P, _I, _I64, _I, _I, ctypes.c_uint,

@@ -9,8 +9,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # fedagg_k*.hip: the reduce kernel variants, split over units that compile
 # in parallel (one unit held them all: 5 minutes of device compilation)
 SRCS = [os.path.join(HERE, "csrc", f) for f in
-        ("fedagg.hip", "fedagg_k1a.hip", "fedagg_k1b.hip", "fedagg_k2a.hip", "fedagg_k2b.hip",
-         "fedagg_k2c.hip", "fedagg_k2d.hip", "fedagg_k4a.hip", "fedagg_k4b.hip", "prox.hip")]
+        ("fedagg.hip", "fedagg_k1.hip", "fedagg_k2.hip", "fedagg_k2w.hip", "fedagg_k4.hip",
+         "prox.hip")]
 HEADERS = [os.path.join(HERE, "csrc", "common.h"), os.path.join(HERE, "csrc", "reduce_impl.h"),
            os.path.join(HERE, "..", "include", "fedagg.h")]
 DEPS = SRCS + HEADERS

@@ -53,13 +53,6 @@ int fa::set_err(int code, const char* fmt, ...) {
 // the reduce kernels' launchers are instantiated in the fedagg_k*.hip units
 FA_K_UNITS(extern)
 
-namespace fa_k {
-thread_local size_t t_dyn_lds = 0;  // tuning: occupancy cap through dynamic LDS
-thread_local int t_grid_cap = 0;     // tuning: persistent grid size
-thread_local int t_tgpu_batch = 0;  // tuning: rows per load batch of the S = 1 torch-GPU tiles (0: by N)
-thread_local int t_bcast_store = 2;  // the r04 flat broadcast's store policy (default sc1 nt)
-}  // namespace fa_k
-
 namespace {
 using fa::set_err;
 using namespace fa_k;
@@ -80,184 +73,23 @@ __global__ void div_trunc_i64_kernel(const float* __restrict__ x, float d,
     out[j] = (int64_t)__fdiv_rn(x[j], d);
 }
 
-// The round's broadcast (train_fedavg.py:148-149) after the reduce, over the
-// same tile table: every tile's result range copied into every client bucket
-// (only segment elements are written, as the fused form).  A pure write
-// stream after a pure read stream: 4 % faster than writing the client buckets
-// from inside the reduce (tools/archive/exp_bcast.py: 300.6 vs 313.2 us for the cfg2
-// round), where the interleaved read and write streams pay bus turnarounds.
-__global__ __launch_bounds__(kBlock) void bcast_tiles_kernel(ReduceArgs args) {
-  (void)args;
-  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  for (int ti = blockIdx.x; ti < a.ntiles; ti += gridDim.x) {
-    const Tile t = a.tiles[ti];
-    if (t.kind == K_F32_VEC) {
-      // two vectors per lane per pass (a 2048-float tile in one pass): both
-      // loads issue before the 2N stores
-      const uint32_t nv = (uint32_t)t.count / 4;
-      for (uint32_t v = threadIdx.x; v < nv; v += 2 * kBlock) {
-        const uint32_t v2 = v + kBlock;
-        const bool two = v2 < nv;
-        const f4 r = ldg4<true>(a.out32 + t.start, v);
-        const f4 r2 = two ? ldg4<true>(a.out32 + t.start, v2) : r;
-        for (int i = 0; i < a.n; ++i) {
-          float* d = const_cast<float*>(cptr32(a, i)) + t.start;
-          stg4<true>(d, v, r);
-          if (two) stg4<true>(d, v2, r2);
-        }
-      }
-    } else if ((int)threadIdx.x < t.count) {
-      int64_t e = t.start + threadIdx.x;
-      bool is64 = kind_is64(t.kind);
-      if ((t.kind & 0xFF) == K_SCALAR_PACKED) {
-        const int64_t ent = a.sidx[e];
-        e = ent >> 4;
-        is64 = kind_is64((int)(ent & 15));
-      }
-      if (!is64) {
-        const float r = a.out32[e];
-        for (int i = 0; i < a.n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
-      } else {
-        const int64_t r = a.out64[e];
-        for (int i = 0; i < a.n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
-      }
-    }
-  }
-}
-
-// (part, client group) of broadcast block v.  xcd: the groups of one part
-// are blocks b, b + 8, b + 16, ... — one XCD under the round-robin dispatch
-// (MI355X_MICROARCH.md, workgroup dispatch; speed only, never correctness),
-// so the part is fetched into that XCD's L2 once and the other groups read
-// it there; the grid covers ceil(nparts / 8) * 8 * groups blocks (false:
-// padding).  Plain form: groups fastest on consecutive blocks, which land on
-// different XCDs — every group fetched its own copy (FETCH_SIZE 2 B at
-// N = 20 with two groups, r02).
-__device__ __forceinline__ bool bcast_part(uint32_t v, uint32_t nparts, uint32_t groups, bool xcd,
-                                           uint32_t* p, uint32_t* g) {
-  if (xcd) {
-    const uint32_t q = v / 8;
-    *g = q % groups;
-    *p = (q / groups) * 8 + v % 8;
-    return *p < nparts;
-  }
+// The round's broadcast (train_fedavg.py:148-149) after the reduce: one
+// workgroup per (part, group of <= G consecutive clients), groups fastest
+// (consecutive blocks), so a part's groups run side by side and its source
+// is fetched once.  (r01-r03 forms — one workgroup per tile writing every
+// client, 2048-float parts in groups of <= 10, per-client pointer loads
+// behind a vmcnt(0) wait, XCD-contiguous groups, the broadcast fused into
+// the reduce — measured and dropped; tools/bcastlab.hip,
+// tools/writelab.hip, tools/roundlab.hip keep them for A/B.)
+__device__ __forceinline__ void bcast_part(uint32_t v, uint32_t groups, uint32_t* p,
+                                           uint32_t* g) {
   *p = v / groups;
   *g = v % groups;
-  return true;
 }
-__host__ __device__ inline uint32_t bcast_blocks(uint32_t nparts, uint32_t groups, bool xcd) {
-  return (xcd ? (nparts + 7) / 8 * 8 : nparts) * groups;
-}
-
-// The round's broadcast (default since r02): one workgroup per (tile, group
-// of G consecutive clients), groups fastest, so a tile's groups run side by
-// side and its source is fetched once and then served from the caches; the
-// tile's loads (U float4 per lane) go out before the group's G*U stores.
-// G = ceil(n / ceil(n / kBcastGroup)) (20 clients: 10, 10).  tools/bcastlab.hip
-// on hashed data (profiles/r02_bcastlab_gsweep_hashed.jsonl), 20 x 43.9 MB,
-// U = 2: G = 10 150.7-151.7 us, G = 5/7 158.7-160.5, G = 4 164, G = 2 173,
-// one workgroup per tile writing all 20 (bcast_tiles_kernel above, the r01
-// form, kept as FA_PLAN_TUNE_BCAST_TILES) 173-176, one client per workgroup
-// 169-170 us.  (On zero-filled buffers every form is faster and G = 1 looks
-// best: 130 us — not a real-data ceiling.)
-constexpr int kBcastGroup = 10;
-__global__ __launch_bounds__(kBlock) void bcast_group_kernel(ReduceArgs args, uint32_t groups,
-                                                             uint32_t gsize, int xcd) {
-  (void)args;
-  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  const uint32_t total = bcast_blocks((uint32_t)a.ntiles, groups, xcd);
-  for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
-    uint32_t ti, g;
-    if (!bcast_part(v, (uint32_t)a.ntiles, groups, xcd, &ti, &g)) continue;
-    const int c0 = (int)(g * gsize);
-    const int c1 = min(a.n, c0 + (int)gsize);
-    const Tile t = a.tiles[ti];
-    const int kb = t.kind & 0xFF;
-    if (kb == K_F32_VEC || kb == K_F32_TGPU_V || kb == K_F32_TGPU_W) {
-      const uint32_t nv = (uint32_t)t.count / 4;
-      // up to 4 vectors per lane (the table's U)
-      f4 r[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t vi = threadIdx.x + u * kBlock;
-        if (vi < nv) r[u] = ldg4<false>(a.out32 + t.start, vi);
-      }
-      for (int c = c0; c < c1; ++c) {
-        float* d = const_cast<float*>(cptr32(a, c)) + t.start;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t vi = threadIdx.x + u * kBlock;
-          if (vi < nv) stg4<true>(d, vi, r[u]);
-        }
-      }
-    } else if ((int)threadIdx.x < t.count) {
-      int64_t e = t.start + threadIdx.x;
-      bool is64 = kind_is64(t.kind);
-      if (kb == K_SCALAR_PACKED) {  // a packed column: its element and kind
-        const int64_t ent = a.sidx[e];
-        e = ent >> 4;
-        is64 = kind_is64((int)(ent & 15));
-      }
-      if (!is64) {
-        const float r = a.out32[e];
-        for (int c = c0; c < c1; ++c) const_cast<float*>(cptr32(a, c))[e] = r;
-      } else {
-        const int64_t r = a.out64[e];
-        for (int c = c0; c < c1; ++c) const_cast<int64_t*>(cptr64(a, c))[e] = r;
-      }
-    }
-  }
-}
-
-// The flat form of the round's broadcast (the default for plans cut from a
-// segment list with FA_PLAN_GAPS_ARE_PADDING, i.e. every Python plan: their
-// buckets hold tensors and padding, so the whole fp32 bucket may be copied
-// without the tile table): bcast_group_kernel's shape — one workgroup per
-// (2048-float part, group of <= kBcastGroup clients), groups fastest — over
-// the flat bucket, so no workgroup waits on a tile-descriptor fetch; the
-// int64 bucket is one extra part.  cfg2 round (tools/archive/exp_bcast.py, same
-// box, profiles/r02_exp_bcast_flatgroups.jsonl): 308.7 us against 312.4 us
-// through the tile table (FA_PLAN_TUNE_BCAST_TABLE) and 331.7 us for r01's
-// form; one client per workgroup instead: 403-407 us.
-__global__ __launch_bounds__(kBlock) void bcast_flat_kernel(ReduceArgs args, uint32_t parts,
-                                                            uint32_t groups, uint32_t gsize,
-                                                            int64_t f32_numel,
-                                                            int64_t i64_numel, int xcd) {
-  (void)args;
-  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  const uint32_t nparts = parts + (i64_numel > 0 ? 1u : 0u);
-  const uint32_t total = bcast_blocks(nparts, groups, xcd);
-  const int64_t nv = f32_numel / 4;
-  for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
-    uint32_t p, g;
-    if (!bcast_part(v, nparts, groups, xcd, &p, &g)) continue;
-    const int c0 = (int)(g * gsize);
-    const int c1 = min(a.n, c0 + (int)gsize);
-    if (p < parts) {
-      const int64_t base = (int64_t)p * (8 * kBlock);  // floats
-      const int64_t v0 = (int64_t)p * 2 * kBlock + threadIdx.x, v1 = v0 + kBlock;
-      f4 r0 = {0.f, 0.f, 0.f, 0.f}, r1 = r0;
-      if (v0 < nv) r0 = ldg4<false>(a.out32 + base, threadIdx.x);
-      if (v1 < nv) r1 = ldg4<false>(a.out32 + base, threadIdx.x + kBlock);
-      for (int c = c0; c < c1; ++c) {
-        float* d = const_cast<float*>(cptr32(a, c)) + base;
-        if (v0 < nv) stg4<true>(d, threadIdx.x, r0);
-        if (v1 < nv) stg4<true>(d, threadIdx.x + kBlock, r1);
-      }
-      if (p == parts - 1 && (int64_t)threadIdx.x < f32_numel - 4 * nv)
-        for (int c = c0; c < c1; ++c)
-          const_cast<float*>(cptr32(a, c))[4 * nv + threadIdx.x] = a.out32[4 * nv + threadIdx.x];
-    } else {
-      for (int64_t e = threadIdx.x; e < i64_numel; e += kBlock) {
-        const int64_t r = a.out64[e];
-        for (int c = c0; c < c1; ++c) const_cast<int64_t*>(cptr64(a, c))[e] = r;
-      }
-    }
-  }
-}
+constexpr int kBcastGroupMax = 24;  // clients per broadcast workgroup
 
 // r04: the round's broadcast with every client pointer a scalar load
-// (sptr32) and a group's G stores back to back.  The two kernels above fetch
+// (sptr32) and a group's G stores back to back.  The r02/r03 kernels fetched
 // each destination through cptr32, which the compiler serves with an
 // `s_waitcnt vmcnt(0)` before every client's stores — a wave's previous
 // client's stores had to complete first (ISA checked; vmcnt counts stores on
@@ -267,37 +99,27 @@ __global__ __launch_bounds__(kBlock) void bcast_flat_kernel(ReduceArgs args, uin
 // source fetch: 7.23 TB/s of B read + N*B written; a pure write of the same
 // N*B 124 us = 7.08 TB/s), 134.3 us at U = 2 in groups of 10, against
 // 156.2 us for the r03 product kernel of the U = 2, groups-of-10 shape.
-// One workgroup per (part of U*1024 floats, group of <= G clients); G is the
+// One workgroup per (part of 1024 floats, group of <= G clients); G is the
 // template bound, the host's group size `gsize` <= G.  The int64 bucket is
-// one more part.
-// Store policy of the broadcast's destination stores (tuning,
-// fa_tune_bcast_store): 0 global nt, 1 sc1, 2 sc1 nt (default), 3 sc0 sc1
-// (buffer stores with those cache-policy bits: sc1 writes through and drops
-// the line from the XCD's L2, so the launch ends with no dirty lines to write
-// back), 4 plain.
-template <int SP>
+// one more part.  Destination stores sc1 nt (a buffer store with those
+// cache-policy bits: sc1 writes through and drops the line from the XCD's
+// L2, so the launch ends with no dirty lines to write back; against nt
+// stores r110 47.3 vs 47.9 us, cfg3 79.5 vs 79.8, the rest within 0.3 %).
 __device__ __forceinline__ void st_bc(float* base, uint32_t vidx, f4 v) {
-  if constexpr (SP == 0) {
-    stg4<true>(base, vidx, v);
-  } else if constexpr (SP == 4) {
-    stg4<false>(base, vidx, v);
-  } else {
-    const __amdgpu_buffer_rsrc_t r =
-        __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(16 * vidx), 0,
-                                           SP == 1 ? 16 : SP == 2 ? 18 : 17);
-  }
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(16 * vidx), 0, 18);
 }
-template <int U, int G, int SP = 0>
+template <int G>
 __global__ __launch_bounds__(kBlock) void bcast_flat2_kernel(ReduceArgs args, uint32_t parts,
                                                              uint32_t groups, uint32_t gsize,
                                                              int64_t f32_numel,
-                                                             int64_t i64_numel, int xcd) {
+                                                             int64_t i64_numel) {
   (void)args;
+  constexpr int U = 1;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  const uint32_t nparts = parts + (i64_numel > 0 ? 1u : 0u);
   uint32_t p, g;
-  if (!bcast_part(blockIdx.x, nparts, groups, xcd, &p, &g)) return;
+  bcast_part(blockIdx.x, groups, &p, &g);
   const int c0 = (int)(g * gsize);
   const int cnt = min(a.n - c0, (int)gsize);
   if (p < parts) {
@@ -317,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void bcast_flat2_kernel(ReduceArgs args, ui
         if (i == 0 || i < cnt) {
           float* d = sptr32(a, c0 + i) + 4 * vb;
 #pragma unroll
-          for (int u = 0; u < U; ++u) st_bc<SP>(d, threadIdx.x + u * kBlock, r[u]);
+          for (int u = 0; u < U; ++u) st_bc(d, threadIdx.x + u * kBlock, r[u]);
         }
       }
     } else {
@@ -353,11 +175,11 @@ __global__ __launch_bounds__(kBlock) void bcast_flat2_kernel(ReduceArgs args, ui
 // group's stores.
 template <int G>
 __global__ __launch_bounds__(kBlock) void bcast_group2_kernel(ReduceArgs args, uint32_t groups,
-                                                              uint32_t gsize, int xcd) {
+                                                              uint32_t gsize) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   uint32_t ti, g;
-  if (!bcast_part(blockIdx.x, (uint32_t)a.ntiles, groups, xcd, &ti, &g)) return;
+  bcast_part(blockIdx.x, groups, &ti, &g);
   const int c0 = (int)(g * gsize);
   const int cnt = min(a.n - c0, (int)gsize);
   const Tile t = a.tiles[ti];
@@ -375,7 +197,7 @@ __global__ __launch_bounds__(kBlock) void bcast_group2_kernel(ReduceArgs args, u
         if (i == 0 || i < cnt) {
           float* d = sptr32(a, c0 + i) + t.start;
 #pragma unroll
-          for (int u = 0; u < 2; ++u) st_bc<2>(d, threadIdx.x + u * kBlock, r[u]);
+          for (int u = 0; u < 2; ++u) st_bc(d, threadIdx.x + u * kBlock, r[u]);
         }
       }
       return;
@@ -557,8 +379,6 @@ __device__ __forceinline__ void tgpu_wide(KArgs& a, int64_t start, int count, fl
     if (!sum_only)
       r = f4{__fmul_rn(r.x, fac), __fmul_rn(r.y, fac), __fmul_rn(r.z, fac), __fmul_rn(r.w, fac)};
     st_out<5>(a.out32, start, vi[u], r);  // sc1: see reduce_impl.h st_out
-    if (a.flags & FA_F_BCAST)
-      for (int i = 0; i < n; ++i) stg4<true>(const_cast<float*>(cptr32(a, i)) + start, vi[u], r);
   }
 }
 
@@ -648,8 +468,6 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
     if (!sum_only)
       r = f4{__fmul_rn(r.x, fac), __fmul_rn(r.y, fac), __fmul_rn(r.z, fac), __fmul_rn(r.w, fac)};
     st_out<5>(a.out32, t.start, v, r);
-    if (a.flags & FA_F_BCAST)
-      for (int i = 0; i < n; ++i) stg4<true>(const_cast<float*>(cptr32(a, i)) + t.start, v, r);
     return;
   }
   if (base == K_F32_TGPU || base == K_I64_TGPU) {
@@ -658,15 +476,9 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
     const int64_t e = t.start + j;
     if (base == K_F32_TGPU) {
       const float s = tgpu_outer<SrcF32, S>(SrcF32{a, false}, e, n);
-      const float r = sum_only ? s : __fmul_rn(s, fac);
-      a.out32[e] = r;
-      if (a.flags & FA_F_BCAST)
-        for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
+      a.out32[e] = sum_only ? s : __fmul_rn(s, fac);
     } else {
-      const int64_t r = (int64_t)__fmul_rn(tgpu_outer<SrcI64, S>(SrcI64{a}, e, n), fac);
-      a.out64[e] = r;
-      if (a.flags & FA_F_BCAST)
-        for (int i = 0; i < n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
+      a.out64[e] = (int64_t)__fmul_rn(tgpu_outer<SrcI64, S>(SrcI64{a}, e, n), fac);
     }
     return;
   }
@@ -679,21 +491,11 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   if (base == K_F32_TGPU_IN) {
     const float s = vec ? tgpu_inner_vec(SrcF32{a, false}, e, n, bw, lane)
                         : tgpu_inner(SrcF32{a, false}, e, n, bw, lane);
-    if (lane == 0) {
-      const float r = sum_only ? s : __fmul_rn(s, fac);
-      a.out32[e] = r;
-      if (a.flags & FA_F_BCAST)
-        for (int i = 0; i < n; ++i) const_cast<float*>(cptr32(a, i))[e] = r;
-    }
+    if (lane == 0) a.out32[e] = sum_only ? s : __fmul_rn(s, fac);
   } else {
     const float s = vec ? tgpu_inner_vec(SrcI64{a}, e, n, bw, lane)
                         : tgpu_inner(SrcI64{a}, e, n, bw, lane);
-    if (lane == 0) {
-      const int64_t r = (int64_t)__fmul_rn(s, fac);
-      a.out64[e] = r;
-      if (a.flags & FA_F_BCAST)
-        for (int i = 0; i < n; ++i) const_cast<int64_t*>(cptr64(a, i))[e] = r;
-    }
+    if (lane == 0) a.out64[e] = (int64_t)__fmul_rn(s, fac);
   }
 }
 
@@ -706,17 +508,17 @@ struct BcastArgs {
   int n;
   float* dst[kBcastInline];
 };
-// One workgroup per (2048-float part, group of <= kBcastGroup destinations),
-// groups fastest (bcast_group_kernel's shape); the last part also copies the
-// numel % 4 tail.
+// One workgroup per (2048-float part, group of <= kBcastGroupMax
+// destinations), groups fastest; the last part also copies the numel % 4
+// tail.
 __global__ __launch_bounds__(kBlock) void bcast_kernel(BcastArgs a, int64_t numel,
                                                        uint32_t parts, uint32_t groups,
                                                        uint32_t gsize) {
   const int64_t nv = numel / 4;
-  const uint32_t total = bcast_blocks(parts, groups, false);
+  const uint32_t total = parts * groups;
   for (uint32_t v = blockIdx.x; v < total; v += gridDim.x) {
     uint32_t p, g;
-    if (!bcast_part(v, parts, groups, false, &p, &g)) continue;
+    bcast_part(v, groups, &p, &g);
     const int c0 = (int)(g * gsize);
     const int c1 = min(a.n, c0 + (int)gsize);
     const int64_t v0 = (int64_t)p * 2 * kBlock + threadIdx.x, v1 = v0 + kBlock;
@@ -765,8 +567,9 @@ __global__ __launch_bounds__(kBlock) void read_probe_kernel(const float* __restr
 }
 
 // Write-only probe in the round broadcast's own shape (fa_write_probe_f32,
-// r04): one workgroup per (1024-float part, group of <= gsize
-// destinations), one 16-B non-temporal store per lane per destination, the
+// r04): one workgroup per (1024-float part, group of <= kBcastGroupMax
+// destinations, as bcast_flat2_kernel), one 16-B store per lane per
+// destination with the broadcast's sc1 nt policy, the
 // values non-zero and non-repeating (an integer hash of the element index
 // and `seed`, computed in registers: nothing is read).  Zero-filled or
 // constant stores are no write ceiling on this chip.
@@ -782,7 +585,7 @@ __global__ __launch_bounds__(kBlock) void write_probe_kernel(BcastArgs a, int64_
                                                              uint32_t parts, uint32_t groups,
                                                              uint32_t gsize, uint32_t seed) {
   uint32_t p, g;
-  if (!bcast_part(blockIdx.x, parts, groups, false, &p, &g)) return;
+  bcast_part(blockIdx.x, groups, &p, &g);
   const int c0 = (int)(g * gsize);
   const int c1 = min(a.n, c0 + (int)gsize);
   const int64_t nv = numel / 4;
@@ -790,7 +593,7 @@ __global__ __launch_bounds__(kBlock) void write_probe_kernel(BcastArgs a, int64_
   if (v >= nv) return;
   const uint32_t b = (uint32_t)(4 * v) ^ seed;
   const f4 x = {probe_val(b), probe_val(b + 1), probe_val(b + 2), probe_val(b + 3)};
-  for (int c = c0; c < c1; ++c) st4<true>(a.dst[c] + 4 * v, x);
+  for (int c = c0; c < c1; ++c) st_bc(a.dst[c], (uint32_t)v, x);
 }
 
 // Read-only probe in the reduce's own shape (grid = 0 in fa_read_probe_f32):
@@ -1050,9 +853,7 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // Clients per load batch of the reduce kernel a call runs (launch_reduce).
 int pick_batch(int n, int vec_u, unsigned pflags) {
-  const int b = (pflags & FA_PLAN_TUNE_BATCH1)    ? 1
-                : (pflags & FA_PLAN_TUNE_BATCH4)  ? 4
-                : (pflags & FA_PLAN_TUNE_BATCH8)  ? 8
+  const int b = (pflags & FA_PLAN_TUNE_BATCH8)    ? 8
                 : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (n < 16 ? 8 : 16);
   return (vec_u == 4 && b == 16) ? 8 : b;  // no 16-client kernels at U = 4
 }
@@ -1090,16 +891,10 @@ int kernel_slots(int dev, int u, int b, bool deep, bool w) {
   if (it != cache.end()) return it->second;
   int occ = 0;
   switch (u * 100 + b) {
-    case 101: occ = occupancy_u<1, 1>(deep, w); break;
-    case 104: occ = occupancy_u<1, 4>(deep, w); break;
     case 108: occ = occupancy_u<1, 8>(deep, w); break;
     case 116: occ = occupancy_u<1, 16>(deep, w); break;
-    case 201: occ = occupancy_u<2, 1>(deep, w); break;
-    case 204: occ = occupancy_u<2, 4>(deep, w); break;
     case 208: occ = occupancy_u<2, 8>(deep, w); break;
     case 216: occ = occupancy_u<2, 16>(deep, w); break;
-    case 401: occ = occupancy_u<4, 1>(deep, w); break;
-    case 404: occ = occupancy_u<4, 4>(deep, w); break;
     case 408: occ = occupancy_u<4, 8>(deep, w); break;
     default: break;
   }
@@ -1111,11 +906,10 @@ int kernel_slots(int dev, int u, int b, bool deep, bool w) {
   return slots;
 }
 
-// The slot count a plain (non-chain) reduce call runs on; 0 where a tuning
-// flag shapes the grid itself (persistent grid, per-CU cap, issue-all form).
+// The slot count a plain (non-chain) reduce call runs on; 0 for a plan that
+// launches its tiles as given (FA_PLAN_TUNE_NO_BALANCE).
 int call_slots(int dev, int n, int vec_u, bool w, unsigned pflags) {
-  if (pflags & (FA_PLAN_TUNE_NO_BALANCE | FA_PLAN_TUNE_ISSUE_ALL | (0xFu << 8) | (0xFu << 12)))
-    return 0;
+  if (pflags & FA_PLAN_TUNE_NO_BALANCE) return 0;
   return kernel_slots(dev, vec_u, pick_batch(n, vec_u, pflags), n >= 256, w);
 }
 
@@ -1124,9 +918,7 @@ int call_slots(int dev, int n, int vec_u, bool w, unsigned pflags) {
 // one.  Explicit batch tuning flags and grid-shaping flags keep their batch.
 int round_batch(int dev, int n, int vec_u, bool w, unsigned pflags, int ntiles) {
   const int b = pick_batch(n, vec_u, pflags);
-  if (b != 16 || (pflags & (FA_PLAN_TUNE_BATCH16 | FA_PLAN_TUNE_NO_BALANCE |
-                            FA_PLAN_TUNE_ISSUE_ALL | (0xFu << 8) | (0xFu << 12))))
-    return b;
+  if (b != 16 || (pflags & (FA_PLAN_TUNE_BATCH16 | FA_PLAN_TUNE_NO_BALANCE))) return b;
   const int s16 = kernel_slots(dev, vec_u, 16, n >= 256, w);
   const int s8 = kernel_slots(dev, vec_u, 8, n >= 256, w);
   return (s16 > 0 && s8 > s16 && ntiles > s16 && ntiles <= s8) ? 8 : 16;
@@ -1241,8 +1033,6 @@ std::vector<Tile> balance_vec(const std::vector<Tile>& tiles, int cmax, int nsca
 hipError_t launch_chain(const ReduceArgs& a, int ntiles, int vec_u, hipStream_t st) {
   const bool deep = a.n_total >= 256;
   const bool w = a.flags & 0x100u;
-  t_dyn_lds = 0;
-  t_grid_cap = 0;
   if (vec_u == 1) return launch_chain_ub<1, 8>(a, ntiles, deep, w, st);
   if (vec_u == 4) return launch_chain_ub<4, 8>(a, ntiles, deep, w, st);
   if (w || a.n < 16) return launch_chain_ub<2, 8>(a, ntiles, deep, w, st);
@@ -1252,60 +1042,19 @@ hipError_t launch_chain(const ReduceArgs& a, int ntiles, int vec_u, hipStream_t 
 
 hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pflags,
                          hipStream_t st, int batch = 0) {
-  // DEEP (n >= 256): cascade levels 2-3 and the constant-space table loads
+  // DEEP (n >= 256): cascade levels 2-3 and the constant-space table loads.
+  // Weighted reductions take the mean's 16-client batches too since the
+  // batch's weights are read once up front (r02 sweep, same box: weighted
+  // U2xB16 140.5 us vs U2xB8 143.3 us, unweighted 143.0 us).
   const bool deep = a.n >= 256;
   const bool w = a.flags & 0x100u;  // internal: weighted
-  if ((pflags & FA_PLAN_TUNE_ISSUE_ALL) && a.n <= kInline && vec_u == 2) {
-    t_dyn_lds = 0;
-    t_grid_cap = 0;
-    const bool b4 = pflags & FA_PLAN_TUNE_BATCH4;
-    if (w) return b4 ? launch_one<2, 4, false, true, 11>(a, ntiles, st)
-                     : launch_one<2, 8, false, true, 11>(a, ntiles, st);
-    return b4 ? launch_one<2, 4, false, false, 11>(a, ntiles, st)
-              : launch_one<2, 8, false, false, 11>(a, ntiles, st);
-  }
-  // cache policy (launch_u's pol): bit 0 nt loads, bit 1 nt result stores,
-  // bit 2 result stores through a buffer op with sc1.  r04 default: nt loads
-  // and sc1 result stores (pol 5) — see st_out; the tuning flags give the
-  // r01-r03 forms (nt stores: FA_PLAN_TUNE_ST_NT) and the older experiments.
-  int nt = (pflags & FA_PLAN_TUNE_NO_NT) ? 0 : 3;
-  if (pflags & FA_PLAN_TUNE_ST_PLAIN) nt &= ~2;
-  if (pflags & FA_PLAN_TUNE_LD_PLAIN) nt &= ~1;
-  if (pflags & FA_PLAN_TUNE_ST_SC1) nt |= 4;
-  if (!(pflags & (FA_PLAN_TUNE_ST_NT | FA_PLAN_TUNE_NO_NT | FA_PLAN_TUNE_ST_PLAIN |
-                  FA_PLAN_TUNE_LD_PLAIN | FA_PLAN_TUNE_ST_SC1)))
-    nt = 5;
-  // weighted reductions take the mean's 16-client batches too since the
-  // batch's weights are read once up front (r02 sweep, same box: weighted
-  // U2xB16 140.5 us vs U2xB8 143.3 us, unweighted 143.0 us)
-  const int b_env = batch > 0 ? batch : pick_batch(a.n, vec_u, pflags);
-  const unsigned cap = (pflags >> 8) & 0xFu;  // FA_PLAN_TUNE_BLOCKS_PER_CU(c)
-  // (the scalar tiles' static LDS stage counts against the cap's share)
-  t_dyn_lds = cap ? (size_t)std::max<long>(
-                        0, (long)((160u * 1024u / cap) & ~1023u) - (long)(kStageFloats * 4))
-                  : 0;
-  t_grid_cap = 256 * (int)((pflags >> 12) & 0xFu);  // FA_PLAN_TUNE_PERSIST(k)
+  const int b = batch > 0 ? batch : pick_batch(a.n, vec_u, pflags);
   switch (vec_u) {
-    case 1:
-      switch (b_env) {
-        case 1: return launch_u<1, 1>(a, ntiles, deep, w, nt, st);
-        case 4: return launch_u<1, 4>(a, ntiles, deep, w, nt, st);
-        case 16: return launch_u<1, 16>(a, ntiles, deep, w, nt, st);
-        default: return launch_u<1, 8>(a, ntiles, deep, w, nt, st);
-      }
-    case 4:
-      switch (b_env) {
-        case 1: return launch_u<4, 1>(a, ntiles, deep, w, nt, st);
-        case 4: return launch_u<4, 4>(a, ntiles, deep, w, nt, st);
-        default: return launch_u<4, 8>(a, ntiles, deep, w, nt, st);
-      }
-    default:
-      switch (b_env) {
-        case 1: return launch_u<2, 1>(a, ntiles, deep, w, nt, st);
-        case 4: return launch_u<2, 4>(a, ntiles, deep, w, nt, st);
-        case 16: return launch_u<2, 16>(a, ntiles, deep, w, nt, st);
-        default: return launch_u<2, 8>(a, ntiles, deep, w, nt, st);
-      }
+    case 1: return b == 16 ? launch_u<1, 16>(a, ntiles, deep, w, st)
+                           : launch_u<1, 8>(a, ntiles, deep, w, st);
+    case 4: return launch_u<4, 8>(a, ntiles, deep, w, st);
+    default: return b == 16 ? launch_u<2, 16>(a, ntiles, deep, w, st)
+                            : launch_u<2, 8>(a, ntiles, deep, w, st);
   }
 }
 
@@ -1415,9 +1164,8 @@ namespace {
 // tiles did).
 std::vector<Tile> pack_scalar(const std::vector<Tile>& t, std::vector<int64_t>* sidx,
                               int* nscalar, unsigned flags) {
-  // tuning: FA_PLAN_TUNE_PACK(c) -> kPackCols >> c columns per tile (the
-  // entry stride stays kPackCols: tile k's entries at k * kPackCols)
-  const int pack = kPackCols >> ((flags >> 26) & 3u);
+  (void)flags;
+  const int pack = kPackCols;
   std::vector<std::pair<int, int64_t>> cols;
   std::vector<Tile> vec;
   for (const Tile& x : t) {
@@ -1479,9 +1227,7 @@ hipError_t upload_tables(fa_plan* p, const std::vector<Tile>& tiles,
   // balanced tables for every slot count a call on this plan may run on
   // (main table: the 16-client kernels, deep or not, weighted or not; the
   // alt table: its unweighted 16-client kernels)
-  if (e != hipSuccess || (p->flags & (FA_PLAN_TUNE_NO_BALANCE | FA_PLAN_TUNE_ISSUE_ALL |
-                                      (0xFu << 8) | (0xFu << 12))))
-    return e;
+  if (e != hipSuccess || (p->flags & FA_PLAN_TUNE_NO_BALANCE)) return e;
   struct Req {
     int u, slots, batch;
     const std::vector<Tile>* host;
@@ -1545,6 +1291,9 @@ int fa_plan_create(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_
                    fa_plan** out) {
   if (!out) return set_err(FA_E_INVAL, "fa_plan_create: out is NULL");
   *out = nullptr;
+  if (flags & ~(unsigned)FA_PLAN_FLAGS_KNOWN)
+    return set_err(FA_E_INVAL, "fa_plan_create: unknown flag bits 0x%x (removed tuning flags?)",
+                   flags & ~(unsigned)FA_PLAN_FLAGS_KNOWN);
   if (f32_numel < 0 || i64_numel < 0) return set_err(FA_E_INVAL, "negative bucket size");
   const bool autosel = tile_elems == 0;
   if (tile_elems == 0) tile_elems = 4 * kBlock * kDefaultU;
@@ -1716,6 +1465,9 @@ void tgpu_split_tail(std::vector<Tile>* t, std::vector<float>* fac, int lo[6], i
 int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, const fa_seg* seg64,
                          int nseg64, int64_t i64_numel, int n, int order, unsigned flags,
                          fa_plan** out) {
+  if (flags & ~(unsigned)FA_PLAN_FLAGS_KNOWN)
+    return set_err(FA_E_INVAL, "fa_plan_create_order: unknown flag bits 0x%x",
+                   flags & ~(unsigned)FA_PLAN_FLAGS_KNOWN);
   if (order == FA_ORDER_TORCH_CPU)
     return fa_plan_create(seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, 0, flags, out);
   if (!out) return set_err(FA_E_INVAL, "fa_plan_create_order: out is NULL");
@@ -1738,7 +1490,6 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
   // bit) share one run cut into 2048-element tiles across key boundaries, as
   // the default plan's vector runs are: no partial tile per key (cfg2: 5432
   // -> ~5381 tiles).  Gaps join a run only when declared padding.
-  const bool wide_ok = !(flags & FA_PLAN_TUNE_TGPU_NARROW);
   int64_t run_s = -1, run_e = -1;
   float run_f = 0.f;
   auto flush = [&]() {
@@ -1785,9 +1536,8 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
       const int64_t head = std::min<int64_t>((4 - g.offset % 4) % 4, g.numel);
       const int64_t body = (g.numel - head) / 4 * 4;
       // S = 1: 2048-element tiles, the default reduce's load shape (r02:
-      // 151.9 us on cfg2 with the 1024-element form; FA_PLAN_TUNE_TGPU_NARROW
-      // keeps that form for A/B)
-      const bool wide = S == 1 && wide_ok;
+      // 151.9 us on cfg2 with the 1024-element form)
+      const bool wide = S == 1;
       if (wide && head == 0 && body > 0) {
         const bool extend = run_s >= 0 && run_f == f &&
                             (run_e == g.offset ||
@@ -1882,6 +1632,9 @@ int fa_plan_build_host(const fa_seg* seg32, int nseg32, int64_t f32_numel, const
                        int nseg64, int64_t i64_numel, int tile_elems, unsigned flags,
                        fa_tile_desc* tiles, int cap, fa_plan_info* info) {
   if (!info) return set_err(FA_E_INVAL, "fa_plan_build_host: info is NULL");
+  if (flags & ~(unsigned)FA_PLAN_FLAGS_KNOWN)
+    return set_err(FA_E_INVAL, "fa_plan_build_host: unknown flag bits 0x%x",
+                   flags & ~(unsigned)FA_PLAN_FLAGS_KNOWN);
   if (tile_elems == 0) tile_elems = 4 * kBlock * kDefaultU;
   if (tile_elems != 4 * kBlock && tile_elems != 8 * kBlock && tile_elems != 16 * kBlock)
     return set_err(FA_E_INVAL, "tile_elems must be 1024, 2048 or 4096 (got %d)", tile_elems);
@@ -1911,6 +1664,9 @@ int fa_plan_create_from_tiles(const fa_tile_desc* tiles, int ntiles, int64_t f32
                               fa_plan** out) {
   if (!out) return set_err(FA_E_INVAL, "fa_plan_create_from_tiles: out is NULL");
   *out = nullptr;
+  if (flags & ~(unsigned)FA_PLAN_FLAGS_KNOWN)
+    return set_err(FA_E_INVAL, "fa_plan_create_from_tiles: unknown flag bits 0x%x",
+                   flags & ~(unsigned)FA_PLAN_FLAGS_KNOWN);
   if (ntiles < 0 || (ntiles > 0 && !tiles))
     return set_err(FA_E_INVAL, "fa_plan_create_from_tiles: bad tile array");
   if (tile_elems == 0) tile_elems = 4 * kBlock * kDefaultU;
@@ -1987,98 +1743,45 @@ int fa_plan_get_info(const fa_plan* plan, fa_plan_info* info) {
 
 namespace {
 // The round's broadcast launch (after the reduce, over the arguments the
-// reduce used): the flat copy in client groups on gap-padded plans, client
-// groups per tile through the tile table otherwise (or with
-// FA_PLAN_TUNE_BCAST_TABLE); r01's one-workgroup-per-tile form with
-// FA_PLAN_TUNE_BCAST_TILES (CPU-order tables only: tiles_ok).
-// r04 default: bcast_flat2_kernel / bcast_group2_kernel (scalar pointer
-// loads), client groups of <= kBcastGroupMax = 24 (FA_PLAN_TUNE_BCAST_G10:
-// <= 10), U = 1 float4 per lane per part (FA_PLAN_TUNE_BCAST_U2: 2),
-// destination stores sc1 nt (fa_tune_bcast_store); the r02/r03 kernels with
-// FA_PLAN_TUNE_BCAST_R03.  Measured inside the round, same process, after
-// the reduce's result stores became sc1 (tools/exp_round2.py,
-// profiles/r04_exp_round2_bcast_forms.jsonl): groups of <= 24 vs <= 10 cfg2
-// 283.7 / 282.4 vs 284.9 / 285.0 us, cfg5 (24 slots: one group vs three)
-// 350.0 vs 363.5 us, the small layouts equal; and one source fetch instead
-// of one per group (PMC: broadcast traffic 1.0012 vs 1.0486 x algorithmic,
-// profiles/r04_round_pmc_round*.json).  (Before the sc1 result stores the
-// groups of <= 24 lost inside the round, 289-319 vs 284-309 us: the source
-// they read at once was the freshly written one)  sc1 nt vs nt
-// destination stores: r110 47.3 vs 47.9 us, cfg3 79.5 vs 79.8, cfg2 / cfg5 /
-// sf32 within 0.3 %.
-constexpr int kBcastGroupMax = 24;
+// reduce used): the flat copy in client groups on gap-padded plans
+// (bcast_flat2_kernel), client groups per tile through the tile table
+// otherwise (bcast_group2_kernel).  Scalar pointer loads, client groups of
+// <= kBcastGroupMax = 24, 1024-float parts, destination stores sc1 nt.
+// Measured inside the round, same process, after the reduce's result stores
+// became sc1 (tools/exp_round2.py, profiles/r04_exp_round2_bcast_forms.jsonl):
+// groups of <= 24 vs <= 10 cfg2 283.7 / 282.4 vs 284.9 / 285.0 us, cfg5 (24
+// slots: one group vs three) 350.0 vs 363.5 us, the small layouts equal; and
+// one source fetch instead of one per group (PMC: broadcast traffic 1.0012
+// vs 1.0486 x algorithmic, profiles/r04_round_pmc_round*.json).
 extern "C++" template <int G>
 void launch_bcast2(const fa_plan* plan, ReduceArgs& a, int ntiles, uint32_t groups,
-                   uint32_t gsize, int xcd, hipStream_t st) {
-  if (plan->flat_bcast && !(plan->flags & FA_PLAN_TUNE_BCAST_TABLE)) {
+                   uint32_t gsize, hipStream_t st) {
+  if (plan->flat_bcast) {
     const int64_t f = plan->has32 ? plan->info.f32_numel : 0;
     const int64_t i = plan->has64 ? plan->info.i64_numel : 0;
-    const int U = (plan->flags & FA_PLAN_TUNE_BCAST_U2) ? 2 : 1;
-    const int64_t parts = f > 0 ? std::max<int64_t>(1, (f / 4 + U * kBlock - 1) / (U * kBlock)) : 0;
+    const int64_t parts = f > 0 ? std::max<int64_t>(1, (f / 4 + kBlock - 1) / kBlock) : 0;
     const int64_t np = parts + (i > 0 ? 1 : 0);
     if (np == 0) return;
-    const unsigned grid = bcast_blocks((uint32_t)np, groups, xcd);
-#define FA_BC2(U_, SP_)                                                                   \
-  hipLaunchKernelGGL((bcast_flat2_kernel<U_, G, SP_>), dim3(grid), dim3(kBlock), 0, st, a, \
-                     (uint32_t)parts, groups, gsize, f, i, xcd)
-    if (U == 2) FA_BC2(2, 0);
-    else if (t_bcast_store == 1) FA_BC2(1, 1);
-    else if (t_bcast_store == 2) FA_BC2(1, 2);
-    else if (t_bcast_store == 3) FA_BC2(1, 3);
-    else if (t_bcast_store == 4) FA_BC2(1, 4);
-    else FA_BC2(1, 0);
-#undef FA_BC2
+    hipLaunchKernelGGL((bcast_flat2_kernel<G>), dim3((unsigned)(np * groups)), dim3(kBlock), 0,
+                       st, a, (uint32_t)parts, groups, gsize, f, i);
   } else if (ntiles > 0) {
-    const unsigned grid = bcast_blocks((uint32_t)ntiles, groups, xcd);
-    hipLaunchKernelGGL((bcast_group2_kernel<G>), dim3(grid), dim3(kBlock), 0, st, a, groups,
-                       gsize, xcd);
+    hipLaunchKernelGGL((bcast_group2_kernel<G>), dim3((unsigned)ntiles * groups), dim3(kBlock), 0,
+                       st, a, groups, gsize);
   }
 }
 
-hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, bool tiles_ok,
-                        hipStream_t st) {
+hipError_t launch_bcast(const fa_plan* plan, ReduceArgs& a, int n, int ntiles, hipStream_t st) {
   a.flags |= FA_F_BCAST;
   if (n <= 0) return hipSuccess;
-  if (!(plan->flags & FA_PLAN_TUNE_BCAST_R03) && !(tiles_ok && (plan->flags & FA_PLAN_TUNE_BCAST_TILES))) {
-    const int gmax = (plan->flags & FA_PLAN_TUNE_BCAST_G10) ? 10 : kBcastGroupMax;
-    const uint32_t groups = (uint32_t)((n + gmax - 1) / gmax);
-    const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
-    const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_XCD) ? 1 : 0;
-    // grids stay below 2^32 blocks: n clients of >= 4 KB parts would outgrow
-    // any GPU's memory long before
-    const int64_t units = plan->flat_bcast ? (plan->info.f32_numel / 1024 + 2) : ntiles;
-    if ((units + 8) * (int64_t)groups > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
-    if (gsize <= 8) launch_bcast2<8>(plan, a, ntiles, groups, gsize, xcd, st);
-    else if (gsize <= 16) launch_bcast2<16>(plan, a, ntiles, groups, gsize, xcd, st);
-    else launch_bcast2<24>(plan, a, ntiles, groups, gsize, xcd, st);
-    return hipGetLastError();
-  }
-  const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
+  const uint32_t groups = (uint32_t)((n + kBcastGroupMax - 1) / kBcastGroupMax);
   const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
-  if (tiles_ok && (plan->flags & FA_PLAN_TUNE_BCAST_TILES)) {
-    hipLaunchKernelGGL(bcast_tiles_kernel, dim3(ntiles), dim3(kBlock), 0, st, a);
-  } else if (!(plan->flags & FA_PLAN_TUNE_BCAST_TABLE) && plan->flat_bcast &&
-             ((plan->has32 ? plan->info.f32_numel : 0) > 0 || plan->has64)) {
-    const int64_t f = plan->has32 ? plan->info.f32_numel : 0;
-    const int64_t i = plan->has64 ? plan->info.i64_numel : 0;
-    const int64_t parts =
-        f > 0 ? std::max<int64_t>(1, (f / 4 + 2 * kBlock - 1) / (2 * kBlock)) : 0;
-    const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_XCD) ? 1 : 0;
-    const int64_t np = parts + (i > 0 ? 1 : 0);
-    if ((np + 8) * groups > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
-    const int64_t total = bcast_blocks((uint32_t)np, groups, xcd);
-    const unsigned grid = (unsigned)std::min<int64_t>(total, 1ll << 30);
-    hipLaunchKernelGGL(bcast_flat_kernel, dim3(grid), dim3(kBlock), 0, st, a, (uint32_t)parts,
-                       groups, gsize, f, i, xcd);
-  } else if (ntiles > 0) {
-    // ntiles * groups < 2^32: n clients of ntiles 4-16 KB tiles would
-    // outgrow any GPU's memory long before
-    const int xcd = (plan->flags & FA_PLAN_TUNE_BCAST_XCD) ? 1 : 0;
-    const unsigned grid =
-        (unsigned)std::min<int64_t>(bcast_blocks((uint32_t)ntiles, groups, xcd), 1ll << 30);
-    hipLaunchKernelGGL(bcast_group_kernel, dim3(grid), dim3(kBlock), 0, st, a, groups, gsize,
-                       xcd);
-  }
+  // grids stay below 2^32 blocks: n clients of >= 4 KB parts would outgrow
+  // any GPU's memory long before
+  const int64_t units = plan->flat_bcast ? (plan->info.f32_numel / 1024 + 2) : ntiles;
+  if (units * (int64_t)groups > (int64_t)UINT32_MAX) return hipErrorInvalidValue;
+  if (gsize <= 8) launch_bcast2<8>(plan, a, ntiles, groups, gsize, st);
+  else if (gsize <= 16) launch_bcast2<16>(plan, a, ntiles, groups, gsize, st);
+  else launch_bcast2<24>(plan, a, ntiles, groups, gsize, st);
   return hipGetLastError();
 }
 }  // namespace
@@ -2098,10 +1801,9 @@ struct Launch {
 Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) {
   Launch L{plan->d_tiles, plan->nt_dev, plan->ns_dev, plan->d_sidx, plan->vec_u, 0, 0};
   bool alt = false;
-  // 1024-float tiles for unweighted N >= 64, and for the fused broadcast
-  // (tuning form) at any N (cfg2 round: 313 vs 318 us, tools/archive/exp_bcast.py)
-  if (plan->d_tiles_alt && !weighted &&
-      (n >= 64 || ((flags & FA_F_BCAST) && (plan->flags & FA_PLAN_TUNE_FUSED_BCAST)))) {
+  (void)flags;
+  // 1024-float tiles for unweighted N >= 64 (tools/tune.py sweep)
+  if (plan->d_tiles_alt && !weighted && n >= 64) {
     L.tiles = plan->d_tiles_alt;
     L.nt = plan->nt_alt_dev;
     L.ns = plan->ns_alt_dev;
@@ -2194,8 +1896,7 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
   a.out64 = out64;
   a.n = n;
   a.n_total = n;
-  a.flags = flags | (weights ? 0x100u : 0u) |
-            ((plan->flags & FA_PLAN_TUNE_WAVE_CONTIG) ? kWaveContig : 0u);
+  a.flags = flags | (weights ? 0x100u : 0u);
   const bool need32 = plan->has32, need64 = plan->has64;
   if (need32) {
     if (!c32 || !out32) return set_err(FA_E_INVAL, "fa_reduce: fp32 buckets required");
@@ -2254,7 +1955,7 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
     const int nt = plan->order == FA_ORDER_TORCH_GPU ? in.ntiles : plan->nt_dev;
     a.ntiles = nt;
     a.sidx = plan->d_sidx;
-    hipError_t e = launch_bcast(plan, a, n, nt, plan->order != FA_ORDER_TORCH_GPU, st);
+    hipError_t e = launch_bcast(plan, a, n, nt, st);
     if (table) {
       hipError_t e2 = hipFreeAsync(table, st);
       if (e == hipSuccess) e = e2;
@@ -2281,7 +1982,7 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
       a.ntiles = cnt;
       switch (g) {
         case 0:
-          if ((t_tgpu_batch ? t_tgpu_batch : plan->tgpu_batch) == 8)
+          if (plan->tgpu_batch == 8)
             hipLaunchKernelGGL((tgpu_kernel<0, 8>), dim3(cnt), dim3(kBlock), 0, st, a);
           else
             hipLaunchKernelGGL(tgpu_kernel<0>, dim3(cnt), dim3(kBlock), 0, st, a);
@@ -2296,7 +1997,7 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
     if (e == hipSuccess && bc && plan->tg_lo[5] > 0) {
       a.tiles = plan->d_tiles;
       a.ntiles = plan->tg_lo[5];
-      e = launch_bcast(plan, a, n, a.ntiles, false, st);
+      e = launch_bcast(plan, a, n, a.ntiles, st);
     }
     if (table) {
       hipError_t e2 = hipFreeAsync(table, st);
@@ -2311,11 +2012,11 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
   a.sidx = L.sidx;
   const int ntiles = L.nt, vec_u = L.vec_u;
   a.ntiles = ntiles;
-  a.xcd_swz = (plan->flags & FA_PLAN_TUNE_XCD) ? 1 : 0;
-  const bool split_bcast = (flags & FA_F_BCAST) && !(plan->flags & FA_PLAN_TUNE_FUSED_BCAST);
-  if (split_bcast) a.flags &= ~FA_F_BCAST;
+  // the broadcast is its own launch after the reduce
+  const bool bcast = (flags & FA_F_BCAST) != 0;
+  a.flags &= ~FA_F_BCAST;
   hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st, L.batch);
-  if (e == hipSuccess && split_bcast) e = launch_bcast(plan, a, n, ntiles, true, st);
+  if (e == hipSuccess && bcast) e = launch_bcast(plan, a, n, ntiles, st);
   if (table) {
     hipError_t e2 = hipFreeAsync(table, st);
     if (e == hipSuccess) e = e2;
@@ -2486,32 +2187,16 @@ int fa_broadcast_f32(const float* src, float* const* dst, int n, int64_t numel, 
     a.n = std::min(kBcastInline, n - i0);
     for (int i = 0; i < a.n; ++i) a.dst[i] = dst[i0 + i];
     const int64_t parts = std::max<int64_t>(1, (numel / 4 + 2 * kBlock - 1) / (2 * kBlock));
-    const uint32_t groups = (uint32_t)((a.n + kBcastGroup - 1) / kBcastGroup);
+    const uint32_t groups = (uint32_t)((a.n + kBcastGroupMax - 1) / kBcastGroupMax);
     const uint32_t gsize = (uint32_t)((a.n + groups - 1) / groups);
-    if ((parts + 8) * groups > (int64_t)UINT32_MAX)
+    if (parts * groups > (int64_t)UINT32_MAX)
       return set_err(FA_E_RANGE, "fa_broadcast_f32: numel=%lld", (long long)numel);
-    const unsigned grid =
-        (unsigned)std::min<int64_t>(bcast_blocks((uint32_t)parts, groups, false), 1ll << 30);
+    const unsigned grid = (unsigned)std::min<int64_t>(parts * groups, 1ll << 30);
     hipLaunchKernelGGL(bcast_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a, numel,
                        (uint32_t)parts, groups, gsize);
     HIP_TRY(hipGetLastError());
   }
   return FA_OK;
-}
-
-int fa_tune_tgpu_batch(int rows) {
-  if (rows != 0 && rows != 8 && rows != 16)
-    return set_err(FA_E_INVAL, "fa_tune_tgpu_batch: %d", rows);
-  const int old = t_tgpu_batch;
-  t_tgpu_batch = rows;
-  return old;
-}
-
-int fa_tune_bcast_store(int policy) {
-  if (policy < 0 || policy > 4) return set_err(FA_E_INVAL, "fa_tune_bcast_store: %d", policy);
-  const int old = t_bcast_store;
-  t_bcast_store = policy;
-  return old;
 }
 
 int fa_write_probe_f32(float* const* dst, int n, int64_t numel, unsigned seed, void* stream) {
@@ -2528,7 +2213,7 @@ int fa_write_probe_f32(float* const* dst, int n, int64_t numel, unsigned seed, v
     a.dst[i] = dst[i];
   }
   const int64_t parts = (numel / 4 + kBlock - 1) / kBlock;
-  const uint32_t groups = (uint32_t)((n + kBcastGroup - 1) / kBcastGroup);
+  const uint32_t groups = (uint32_t)((n + kBcastGroupMax - 1) / kBcastGroupMax);
   const uint32_t gsize = (uint32_t)((n + groups - 1) / groups);
   if (parts * groups > (int64_t)UINT32_MAX)
     return set_err(FA_E_RANGE, "fa_write_probe_f32: numel=%lld", (long long)numel);

@@ -1,4 +1,4 @@
-// fedagg_k1b.hip — reduce_kernel instantiations of libfedagg.so (see
+// fedagg_k1.hip — reduce_kernel instantiations of libfedagg.so (see
 // reduce_impl.h): one share of the (U, B) launcher set, compiled in
 // parallel with the other units.
 #include "reduce_impl.h"

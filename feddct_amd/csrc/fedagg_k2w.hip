@@ -1,7 +1,7 @@
-// fedagg_k2a.hip — reduce_kernel instantiations of libfedagg.so (see
+// fedagg_k2w.hip — reduce_kernel instantiations of libfedagg.so (see
 // reduce_impl.h): one share of the (U, B) launcher set, compiled in
 // parallel with the other units.
 #include "reduce_impl.h"
 
-FA_K_LAUNCH_U(, 2, 1)
-FA_K_LAUNCH_U(, 2, 4)
+FA_K_LAUNCH_U(, 2, 16)
+FA_K_LAUNCH_CHAIN(, 2, 16)

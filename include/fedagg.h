@@ -86,55 +86,20 @@ extern "C" {
 #define FA_PLAN_GAPS_ARE_PADDING 1u /* bytes between segments may be written
                                        (vector runs span them); with full
                                        coverage also FA_F_BCAST's flat copy */
-#define FA_PLAN_TUNE_NO_NT 2u       /* tuning: plain (temporal) loads/stores   */
-#define FA_PLAN_TUNE_BATCH8 4u     /* tuning: force 8 clients per load batch  */
-#define FA_PLAN_TUNE_BATCH16 8u    /* tuning: force 16 clients per load batch */
-#define FA_PLAN_TUNE_XCD 16u       /* tuning: contiguous tile range per XCD   */
-#define FA_PLAN_TUNE_WAVE_CONTIG 32u /* tuning: each wave reads adjacent KiBs  */
-#define FA_PLAN_TUNE_ST_PLAIN 64u  /* tuning: plain (temporal) stores only     */
-#define FA_PLAN_TUNE_LD_PLAIN 128u /* tuning: plain (temporal) loads only      */
-#define FA_PLAN_TUNE_ST_SC1 0x10000u /* tuning: result stores with sc1 + nt     */
-#define FA_PLAN_TUNE_BATCH1 0x20000u /* tuning: 1 client per load batch         */
-#define FA_PLAN_TUNE_BATCH4 0x40000u /* tuning: 4 clients per load batch        */
-#define FA_PLAN_TUNE_FUSED_BCAST 0x80000u /* tuning: FA_F_BCAST inside the reduce */
-#define FA_PLAN_TUNE_ISSUE_ALL 0x100000u /* tuning: a batch's loads back to back
-                                            (n <= FA_INLINE_CLIENTS, 2048-float tiles,
-                                            BATCH4 or 8 clients per batch)     */
-#define FA_PLAN_TUNE_BCAST_TABLE 0x800000u /* tuning: FA_F_BCAST through the tile
-                                              table (client groups per tile) also
-                                              on gap-padded plans, which copy
-                                              their buckets flat by default    */
-#define FA_PLAN_TUNE_ST_NT 0x1000000u /* tuning: the reduce's result stores
-                                        non-temporal, as r01-r03 (default since r04:
-                                        sc1 write-through stores, see reduce_impl.h
-                                        st_out) */
-#define FA_PLAN_TUNE_BCAST_XCD 0x2000000u /* tuning: the broadcast's client groups
-                                              of a part on one XCD (blocks b, b+8,
-                                              ...: one source fetch) instead of on
-                                              consecutive blocks (measured r03: the
-                                              round 3.7 % slower, kept for A/B)   */
-#define FA_PLAN_TUNE_BCAST_TILES 0x400000u /* tuning: FA_F_BCAST as one workgroup per
-                                              tile writing every client (r01 form) */
-#define FA_PLAN_TUNE_TGPU_NARROW 0x200000u /* tuning: torch-GPU order, S = 1 tensors in
-                                              1024-element tiles (r02 form)      */
-#define FA_PLAN_TUNE_NO_BALANCE 0x10000000u /* tuning: launch the plain tile table
-                                               with the default batch only (by
+#define FA_PLAN_TUNE_BATCH8 4u     /* force 8 clients per load batch          */
+#define FA_PLAN_TUNE_BATCH16 8u    /* force 16 clients per load batch         */
+#define FA_PLAN_TUNE_NO_BALANCE 0x10000000u /* launch the plain tile table with
+                                               the default batch only (by
                                                default the launch shape follows
-                                               the round count, below)          */
-#define FA_PLAN_TUNE_BCAST_R03 0x20000000u /* tuning: FA_F_BCAST through the r02/r03
-                                               kernels (each client's pointer behind
-                                               a vmcnt(0) wait; groups of <= 10,
-                                               2048-float parts) */
-#define FA_PLAN_TUNE_BCAST_U2 0x40000000u /* tuning: the r04 broadcast with
-                                              2048-float parts (default 1024) */
-#define FA_PLAN_TUNE_BCAST_G10 0x80000000u /* tuning: the r04 broadcast in client
-                                               groups of <= 10 (default <= 24) */
-/* tuning: packed scalar tiles of 64 >> c columns (c = 0..3; default 64) */
-#define FA_PLAN_TUNE_PACK(c) (((unsigned)(c) & 3u) << 26)
-/* tuning: cap resident workgroups per CU at c (1..15) via dynamic LDS */
-#define FA_PLAN_TUNE_BLOCKS_PER_CU(c) (((unsigned)(c) & 0xFu) << 8)
-/* tuning: persistent grid of 256*k workgroups striding over the tiles */
-#define FA_PLAN_TUNE_PERSIST(k) (((unsigned)(k) & 0xFu) << 12)
+                                               the round count)    */
+/* Every other bit is refused (FA_E_INVAL) since r05: the r01-r04 tuning
+ * flags (cache policies, XCD / wave-contiguous tile orders, persistent grids,
+ * occupancy caps, issue-all batches, fused / per-tile / r03 broadcasts,
+ * packed-tile widths, ...) were measured, dropped and removed from the
+ * library, and a caller still passing one gets an error, not a silently
+ * different kernel. */
+#define FA_PLAN_FLAGS_KNOWN \
+  (FA_PLAN_GAPS_ARE_PADDING | FA_PLAN_TUNE_BATCH8 | FA_PLAN_TUNE_BATCH16 | FA_PLAN_TUNE_NO_BALANCE)
 
 /* One tensor (state_dict key) inside a flat bucket: [offset, offset+numel). */
 typedef struct fa_seg {
@@ -358,19 +323,9 @@ int fa_tune_prox_store(int policy);
  * workgroup of fa_prox_norms' partial-sum launch, 1..4 (0: the default, 1);
  * the result bits do not depend on it.  Returns the previous setting. */
 int fa_tune_prox_cpw(int cpw);
-/* Tuning (experiments only; calling thread): rows per load batch of the
- * torch-GPU order's S = 1 tiles, 8 or 16 (0: the default, 8 for plans cut
- * for N < 16, else 16).  The bits do not depend on it.  Returns the
- * previous setting. */
-int fa_tune_tgpu_batch(int rows);
-
-/* Tuning (experiments only; calling thread): the store policy of the round
- * broadcast's flat kernel — 0 global nt, 1 sc1, 2 sc1 nt (default),
- * 3 sc0 sc1, 4 plain.  Returns the previous policy, or FA_E_INVAL. */
-int fa_tune_bcast_store(int policy);
 /* Write-only streaming probe (write-bandwidth ceiling, r04): the round
  * broadcast's launch shape — one workgroup per (1024-float part, group of
- * <= 10 destinations) — storing non-zero hashed values (a function of the
+ * <= 24 destinations), sc1 nt stores — storing non-zero hashed values (a function of the
  * element index and `seed`) into n <= 256 destination buckets of numel
  * floats (the last numel % 4 are not written); nothing is read. */
 int fa_write_probe_f32(float *const *dst, int n, int64_t numel, unsigned seed,

@@ -164,4 +164,25 @@ def test_header_constants_match_binding():
             assert getattr(_lib, name) == int(val, 0), name
             checked += 1
     assert checked >= 10
-    assert _lib.FA_PLAN_TUNE_FUSED_BCAST == 0x80000
+    assert _lib.FA_PLAN_FLAGS_KNOWN == 0x1000000D
+
+
+@pytest.mark.parametrize("bit", [2, 16, 32, 64, 0x10000, 0x80000, 0x400000, 0x800000, 0x1000000,
+                                 0x20000000, 0x80000000, 3 << 26, 3 << 8, 5 << 12])
+def test_removed_tuning_flags_are_refused(bit):
+    """r05: the r01-r04 tuning flags are gone
+    from the library, and a caller still passing one (e.g. 0x1000000, which
+    named two different r03 / r04 flags) gets FA_E_INVAL, not a silently
+    different kernel.  fa_plan_build_host is host-only: no GPU needed."""
+    import ctypes
+    import numpy as np
+    segs, n = _lib.seg_array(np.array([[0, 4096]], np.int64))
+    info = _lib.FaPlanInfo()
+    rc = _lib.lib.fa_plan_build_host(segs, n, 4096, None, 0, 0, 0,
+                                     _lib.FA_PLAN_GAPS_ARE_PADDING | bit, None, 0,
+                                     ctypes.byref(info))
+    assert rc == _lib.FA_E_INVAL, (hex(bit), rc)
+    assert b"unknown flag bits" in _lib.lib.fa_last_error()
+    rc = _lib.lib.fa_plan_build_host(segs, n, 4096, None, 0, 0, 0,
+                                     _lib.FA_PLAN_FLAGS_KNOWN, None, 0, ctypes.byref(info))
+    assert rc == 0

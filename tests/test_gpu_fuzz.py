@@ -51,12 +51,10 @@ def test_random_layouts_bit_exact(seed):
     c = _case(seed)
     rng, n, numel = c["rng"], c["n"], c["numel"]
     flags = _lib.FA_PLAN_GAPS_ARE_PADDING if c["gaps_pad"] else 0
-    # FA_F_BCAST cases rotate over the broadcast forms: the default (a flat
-    # copy in client groups on gap-padded plans, client groups per tile on
-    # the others), fused into the reduce, one workgroup per tile (r01),
-    # client groups per tile on every plan
-    flags |= (0, _lib.FA_PLAN_TUNE_FUSED_BCAST, _lib.FA_PLAN_TUNE_BCAST_TILES,
-              _lib.FA_PLAN_TUNE_BCAST_TABLE, _lib.FA_PLAN_TUNE_ST_NT)[seed % 5]
+    # the broadcast (FA_F_BCAST cases) is a flat copy in client groups on
+    # gap-padded plans, client groups per tile on the others; launch shapes
+    # rotate over the balanced tables (default) and the plain one
+    flags |= (0, _lib.FA_PLAN_TUNE_NO_BALANCE)[seed % 2]
     plan = _lib.Plan(c["segs"], numel, c["segs64"], c["numel64"], tile_elems=c["tile"],
                      flags=flags)
     # adversarial-range values, exact small integers for the int64 keys

@@ -243,23 +243,20 @@ def test_bcast_of_a_partial_plan_leaves_other_keys_alone(lib, which):
             assert torch.equal(i[o:o + m], want[o:o + m]), (which, o)
 
 
-@pytest.mark.parametrize("n", [1, 7, 20, 21, 300])
-@pytest.mark.parametrize("form", ["flat", "flat_xcd", "table", "table_xcd", "tgpu"])
+@pytest.mark.parametrize("n", [1, 7, 20, 21, 24, 25, 49, 300])
+@pytest.mark.parametrize("form", ["flat", "table", "tgpu"])
 def test_broadcast_forms_and_bcast_only(lib, n, form):
     """Every broadcast form writes the global state into every client —
     FA_F_BCAST after the reduce and FA_F_BCAST_ONLY alone (the reference's
-    initial sync, train_fedavg.py:244-250) — with consecutive client groups
-    (default) and XCD-paired ones (tuning, r03), client counts that leave a
-    short last group, and part counts that are not a multiple of 8."""
+    initial sync, train_fedavg.py:244-250): the flat copy (gap-padded plans),
+    client groups per tile (plans without gap padding: only segments are
+    written) and the torch-GPU-order table; client counts that leave a short
+    last group of <= 24 and part counts that are not a multiple of 8."""
     from feddct_amd._lib import FA_F_BCAST, FA_F_BCAST_ONLY
     man = _rand_manifest(None, [100, 4096, 7, 3000, 1, 64, 20000])
     layout = BucketLayout.from_manifest(man)
     states = [synth.gen_state(man, i % 9, synth.MODE_ADVERSARIAL) for i in range(n)]
-    fl = lib.FA_PLAN_GAPS_ARE_PADDING
-    if form.startswith("table"):
-        fl |= lib.FA_PLAN_TUNE_BCAST_TABLE
-    if form.endswith("xcd"):
-        fl |= lib.FA_PLAN_TUNE_BCAST_XCD
+    fl = 0 if form == "table" else lib.FA_PLAN_GAPS_ARE_PADDING
     kw = dict(order=lib.FA_ORDER_TORCH_GPU, n=n) if form == "tgpu" else {}
     if form == "tgpu" and not 2 <= n <= 128:
         pytest.skip("the torch-GPU order: N >= 2, and no row split past 16 warps (N=300 "
@@ -969,8 +966,7 @@ def test_checkpoint_from_device_bucket(tmp_path):
     assert list(bucket_state_dict(g)) == list(g.state_dict())
 
 
-@pytest.mark.parametrize("flags", ["xcd", "cap3", "batch8", "batch16", "plain", "persist",
-                                   "wavecontig", "st_nt", "st_sc1nt"])
+@pytest.mark.parametrize("flags", ["batch8", "batch16", "no_balance", "tile1024", "tile4096"])
 def test_tuning_flags_keep_bits(lib, flags):
     from feddct_amd.workload import make_clients
     man = load_manifest("wrnsl16_8_sf4_c10_proxy")
@@ -978,16 +974,14 @@ def test_tuning_flags_keep_bits(lib, flags):
     n = 19
     cl = make_clients(layout, man, range(n), DEV, synth.MODE_ADVERSARIAL)
     ref32, ref64 = _reduce(lib, layout, cl)
-    fl = lib.FA_PLAN_GAPS_ARE_PADDING | {
-        "xcd": lib.FA_PLAN_TUNE_XCD, "cap3": lib.FA_PLAN_TUNE_BLOCKS_PER_CU(3),
-        "batch8": lib.FA_PLAN_TUNE_BATCH8, "batch16": lib.FA_PLAN_TUNE_BATCH16,
-        "plain": lib.FA_PLAN_TUNE_NO_NT, "persist": lib.FA_PLAN_TUNE_PERSIST(1),
-        "wavecontig": lib.FA_PLAN_TUNE_WAVE_CONTIG,
-        # the reduce's result stores: r01-r03's nt, and sc1 + nt (the r04
-        # default is sc1 alone, reduce_impl.h st_out)
-        "st_nt": lib.FA_PLAN_TUNE_ST_NT, "st_sc1nt": lib.FA_PLAN_TUNE_ST_SC1}[flags]
+    # r05: the launch-shape choices that remain (every other tuning flag
+    # was removed, test_abi.py::test_removed_tuning_flags_are_refused)
+    extra, tile = {"batch8": (lib.FA_PLAN_TUNE_BATCH8, 1024),
+                   "batch16": (lib.FA_PLAN_TUNE_BATCH16, 2048),
+                   "no_balance": (lib.FA_PLAN_TUNE_NO_BALANCE, 2048),
+                   "tile1024": (0, 1024), "tile4096": (0, 4096)}[flags]
     plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
-                    4096 if flags == "wavecontig" else 1024, fl)
+                    tile, lib.FA_PLAN_GAPS_ARE_PADDING | extra)
     from feddct_amd.workload import Reducer
     o32 = torch.full_like(ref32, np.nan)
     o64 = torch.full_like(ref64, -1)

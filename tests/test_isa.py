@@ -1,6 +1,8 @@
 """Code-object checks on the built libraries (CPU only, no GPU): the gfx950
-code object is present, no kernel uses scratch, and the hot kernel's loads
-are global (not flat) non-temporal 16-B loads."""
+code object is present, no kernel uses scratch, the hot kernel's loads are
+global (not flat) non-temporal 16-B loads, the reduce family holds only the
+shipped variants (r05), and no kernel contracts a multiply and an add into
+an FMA (parity depends on -ffp-contract=off: VERDICT r04 weak 9)."""
 import os
 import re
 import shutil
@@ -13,7 +15,9 @@ from conftest import ROOT
 LLVM = "/opt/rocm/lib/llvm/bin"
 LIBS = [os.path.join(ROOT, "feddct_amd", "libfedagg.so"),
         os.path.join(ROOT, "feddct_amd", "libfedagg_comm.so")]
-HOT = "_ZN4fa_k13reduce_kernelILi2ELi16ELb0ELb0ELi3ELb0EEEvNS_10ReduceArgsE"
+# the default reduce: U = 2 (2048-float tiles), 16-client batches, not deep,
+# unweighted, POL 5 (nt loads, sc1 result stores), not a chain segment
+HOT = "_ZN4fa_k13reduce_kernelILi2ELi16ELb0ELb0ELi5ELb0EEEvNS_10ReduceArgsE"
 
 
 def _have_tools():
@@ -103,3 +107,99 @@ def test_hot_kernel_uses_global_nt_loads(tmp_path):
     nt = re.findall(r"global_load_dwordx4[^\n]*\bnt\b", body)
     assert len(nt) >= 32, "hot loads should be non-temporal global_load_dwordx4"
     assert "scratch_" not in body
+
+
+def _bodies(co):
+    dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", co],
+                         check=True, capture_output=True, text=True).stdout
+    for m in re.finditer(r"^[0-9a-f]+ <(\S+)>:\n(.*?)(?=\n\n|\Z)", dis, flags=re.S | re.M):
+        yield m.group(1), [ln.split("//")[0].strip() for ln in m.group(2).splitlines()]
+
+
+FMA = re.compile(r"^v_(?:pk_)?(?:fma|fmac|fmamk|fmaak|mac|mad)(?:_legacy)?_f(?:16|32|64)"
+                 r"(?:_e32|_e64|_dpp|_sdwa)?$|^v_fma_mix\w*$")
+TWO32 = ("0x4f800000", "0xcf800000")   # +-2^32: the 64-bit integer <-> fp32 idioms
+
+
+def _contractions(lines):
+    """FMA-class instructions a kernel's own arithmetic could only have come
+    from by contraction.  Exempt: the expansions the compiler emits for
+    operations that are correctly rounded by definition — IEEE division
+    (v_div_scale_f32 .. v_div_fixup_f32, __fdiv_rn), IEEE square root (the
+    residual checks after v_sqrt_f32), and the exact +-2^32 split of the
+    64-bit integer <-> fp32 conversions (the int64 keys' truncation, 64-bit
+    loop-count division)."""
+    bad, open_div, since_sqrt = [], 0, 99
+    two32_sregs = {ln.split()[1].rstrip(",") for ln in lines
+                   if ln.startswith("s_mov_b32") and ln.split()[-1] in TWO32}
+    for ln in lines:
+        op = ln.split(" ")[0] if ln else ""
+        since_sqrt += 1
+        if op.startswith("v_div_scale_f32"):
+            open_div += 1
+        elif op.startswith("v_div_fixup_f32"):
+            open_div = max(0, open_div - 2)
+        elif op.startswith("v_sqrt_f32"):
+            since_sqrt = 0
+        elif FMA.match(op):
+            if op.startswith("v_div_fmas") or open_div > 0 or since_sqrt <= 12:
+                continue
+            args = [a.strip().strip("-|") for a in ln[len(op):].split(",")]
+            if any(a in TWO32 or a in two32_sregs for a in args):
+                continue
+            bad.append(ln)
+    return bad
+
+
+@pytest.mark.skipif(not _have_tools(), reason="ROCm llvm tools / objcopy not available")
+@pytest.mark.parametrize("lib", LIBS)
+def test_no_fma_contraction_in_shipped_kernels(lib, tmp_path):
+    """Every reduce, broadcast, fold, stack, torch-GPU-order and proximal-term
+    kernel: no v_fma / v_fmac / v_mad / v_mac on its own multiply-add (the
+    weighted product x_i * w_i must round before the add, as torch's CPU
+    kernels round it); build.py compiles with -ffp-contract=off, and this
+    pins the result in the shipped code objects."""
+    seen, bad = 0, {}
+    for co in _code_objects(lib, tmp_path):
+        for name, lines in _bodies(co):
+            seen += 1
+            b = _contractions(lines)
+            if b:
+                bad[name] = b[:3]
+    assert seen > 0
+    assert not bad, bad
+
+
+def test_contraction_checker_sees_a_contraction():
+    """The checker itself: a contracted multiply-add is flagged, the
+    division / sqrt / int64-conversion idioms are not."""
+    div = ["v_div_scale_f32 v7, s[14:15], s10, s10, v6", "v_rcp_f32_e32 v9, v7",
+           "v_div_scale_f32 v8, vcc, v6, s10, v6", "v_fma_f32 v10, -v7, v9, 1.0",
+           "v_fmac_f32_e32 v9, v10, v9", "v_div_fmas_f32 v7, v7, v9, v10",
+           "v_div_fixup_f32 v6, v7, s10, v6"]
+    conv = ["s_mov_b32 s12, 0xcf800000", "v_fma_f32 v6, v7, s12, |v6|",
+            "v_cvt_u32_f32_e32 v6, v6"]
+    sq = ["v_sqrt_f32_e32 v15, v14", "v_add_u32_e32 v17, -1, v15",
+          "v_fma_f32 v18, -v17, v15, v14"]
+    assert _contractions(div + conv + sq) == []
+    assert _contractions(div + ["v_fmac_f32_e32 v3, v1, v2"]) == ["v_fmac_f32_e32 v3, v1, v2"]
+    assert _contractions(["v_pk_fma_f32 v[0:1], v[2:3], v[4:5], v[6:7]"])
+
+
+@pytest.mark.skipif(not _have_tools(), reason="ROCm llvm tools / objcopy not available")
+def test_reduce_family_is_the_shipped_set(tmp_path):
+    """r05: the reduce kernel family holds only the
+    shipped variants — U x B in {1x8, 1x16, 2x8, 2x16, 4x8}, deep x weighted,
+    POL 5 for the reduce and POL 3 for chain segments: 36 instances."""
+    names = set()
+    for co in _code_objects(LIBS[0], tmp_path):
+        names |= {k for k in _kernels(co) if "reduce_kernel" in k}
+    pat = re.compile(r"reduce_kernelILi(\d)ELi(\d+)ELb([01])ELb([01])ELi(\d+)ELb([01])E")
+    got = set()
+    for k in names:
+        m = pat.search(k)
+        assert m, k
+        got.add(tuple(int(x) for x in m.groups()))
+    want = {(u, b, d, w, 3 if c else 5, c) for u, b in ((1, 8), (1, 16), (2, 8), (2, 16), (4, 8))
+            for d in (0, 1) for w in (0, 1) for c in (0, 1) if not (c and (u, b) == (1, 16))}
+    assert got == want, (sorted(got - want), sorted(want - got))

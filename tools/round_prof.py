@@ -2,10 +2,7 @@
 separate FETCH_SIZE / WRITE_SIZE passes of tools/gpu_round_pmc.sh):
 
     python tools/round_prof.py round K        # reduce + broadcast launch (FA_F_BCAST)
-    python tools/round_prof.py round_xcd K  # ... XCD-paired client groups (FA_PLAN_TUNE_BCAST_XCD)
-    python tools/round_prof.py round_g10 K  # ... client groups of <= 10 (r04 first form)
     python tools/round_prof.py bcast K        # the broadcast launch alone (FA_F_BCAST_ONLY)
-    python tools/round_prof.py bcast_xcd K
     python tools/round_prof.py tgpu K         # the torch-GPU-order reduce (tgpu_kernel<0>)
     python tools/round_prof.py sf32 K         # FedDCT sweep layouts' reduce alone (joint
     python tools/round_prof.py resnet110sl K  #   main + proxy bucket, rotated past the MALL)
@@ -58,12 +55,9 @@ def main():
     n = 20
     cl = make_clients(lay, man, range(n), dev)
     o32, o64 = torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])
-    xc = _lib.FA_PLAN_GAPS_ARE_PADDING | _lib.FA_PLAN_TUNE_BCAST_XCD
-    if mode in ("round", "bcast", "round_xcd", "bcast_xcd", "round_g10", "bcast_g10"):
-        fl = (xc if mode.endswith("xcd") else
-              _lib.FA_PLAN_GAPS_ARE_PADDING | _lib.FA_PLAN_TUNE_BCAST_G10 if mode.endswith("g10")
-              else _lib.FA_PLAN_GAPS_ARE_PADDING)
-        plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel, flags=fl)
+    if mode in ("round", "bcast"):
+        plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
+                         flags=_lib.FA_PLAN_GAPS_ARE_PADDING)
         red = Reducer(lay, cl, o32, o64, plan=plan,
                       flags=_lib.FA_F_BCAST if mode.startswith("round") else _lib.FA_F_BCAST_ONLY)
     elif mode == "tgpu":
