@@ -279,6 +279,80 @@ def test_broadcast_forms_and_bcast_only(lib, n, form):
             assert torch.equal(i[:layout.i64_numel], g64[:layout.i64_numel]), (form, flag)
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 15, 16, 20])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("tile", [0, 1024, 4096])
+def test_round_one_launch_and_two(lib, n, weighted, tile):
+    """r05: FA_F_BCAST rounds of < 16 clients run as ONE launch
+    (reduce_impl.h round_kernel: reducers publish each tile, broadcasters
+    wait for it), 16 and more as reduce + broadcast launches.  Both: the
+    global is the oracle's bits and every client's segments equal it; every
+    tile width (the kernel's U = 1, 2, 4), weighted or not, packed scalar
+    columns and int64 keys included."""
+    man = _rand_manifest(None, [100, 4096, 7, 3000, 1, 64, 20000, 3, 9000])
+    layout = BucketLayout.from_manifest(man)
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    bk = states_to_buckets(layout, states, DEV)
+    w = O.weights_from_sizes(np.arange(1, n + 1) * 7 + 3) if weighted else None
+    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
+                    tile_elems=tile, flags=lib.FA_PLAN_GAPS_ARE_PADDING)
+    o32 = torch.full_like(bk[0][0], np.nan)
+    o64 = torch.full_like(bk[0][1], -7)
+    wa = None if w is None else (ctypes.c_float * n)(*[float(x) for x in w])
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    lib.check(lib.lib.fa_reduce(plan.handle, lib.ptr_array([b[0].data_ptr() for b in bk]),
+                                lib.ptr_array([b[1].data_ptr() for b in bk]), n, wa,
+                                o32.data_ptr(), o64.data_ptr(), lib.FA_F_BCAST, s))
+    torch.cuda.synchronize()
+    if w is None:
+        want = O.aggregate_state(states)
+    else:
+        want = []
+        for j, (k, v0) in enumerate(states[0]):
+            x = np.stack([np.asarray(st[j][1]) for st in states])
+            want.append((k, O.mean_i64_trunc(x) if x.dtype == np.int64 else O.weighted_sum0(x, w)))
+    for (k, v), (_, g) in zip(want, buckets_to_state(layout, o32, o64)):
+        assert bits_equal(g, v), (n, weighted, tile, k)
+    for f, i in bk:
+        for o, m in layout.segs32:
+            assert torch.equal(f[o:o + m].view(torch.int32), o32[o:o + m].view(torch.int32)), o
+        assert torch.equal(i[:layout.i64_numel], o64[:layout.i64_numel])
+
+
+def test_round_one_launch_across_streams(lib):
+    """The one-launch round's hand-off words belong to the plan: rounds on
+    one plan issued on two streams without any host synchronisation are
+    serialised by the plan (a call on another stream waits for the last
+    one), so every round is exact.  Eight client sets of 5, the streams
+    alternating."""
+    man = _rand_manifest(None, [4096, 33, 50000, 1, 7000])
+    layout = BucketLayout.from_manifest(man)
+    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
+                    flags=lib.FA_PLAN_GAPS_ARE_PADDING)
+    sets, wants = [], []
+    for k in range(8):
+        states = [synth.gen_state(man, 10 * k + i, synth.MODE_ADVERSARIAL) for i in range(5)]
+        sets.append(states_to_buckets(layout, states, DEV))
+        wants.append(O.aggregate_state(states))
+    outs = [(torch.full_like(b[0][0], np.nan), torch.full_like(b[0][1], -7)) for b in sets]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)]
+    for k, bk in enumerate(sets):
+        st = streams[k % 2]
+        lib.check(lib.lib.fa_reduce(plan.handle, lib.ptr_array([b[0].data_ptr() for b in bk]),
+                                    lib.ptr_array([b[1].data_ptr() for b in bk]), 5, None,
+                                    outs[k][0].data_ptr(), outs[k][1].data_ptr(), lib.FA_F_BCAST,
+                                    ctypes.c_void_p(st.cuda_stream)))
+    torch.cuda.synchronize()
+    for k in range(8):
+        for (key, v), (_, g) in zip(wants[k], buckets_to_state(layout, *outs[k])):
+            assert bits_equal(g, v), (k, key)
+        for f, i in sets[k]:
+            for o, m in layout.segs32:
+                assert torch.equal(f[o:o + m].view(torch.int32),
+                                   outs[k][0][o:o + m].view(torch.int32))
+
+
 def test_int64_adversarial(lib):
     man = {"keys": [{"key": f"i{j}", "shape": s, "dtype": "int64"}
                     for j, s in enumerate([[], [1], [3], [9], [40], [300]])]}

@@ -154,6 +154,41 @@ __global__ __launch_bounds__(256) void lagged_k(Args a) {
   if (go) bcast_tile(a, j);
 }
 
+// split grid with a bounded number of broadcasters (deadlock-free whatever
+// the dispatch order: P < the resident slots, so spinning broadcasters can
+// never hold every slot a pending reducer needs): blocks T .. T+P-1 each
+// broadcast tiles j = b - T, b - T + P, ... in a loop
+__global__ __launch_bounds__(256) void persist_k(Args a) {
+  const int w = blockIdx.x;
+  __shared__ int go;
+  if (w < a.ntiles) {
+    reduce_tile(a, w);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __builtin_amdgcn_raw_buffer_store_b32(a.epoch, rsrc(a.flags), 4 * w, 0, 16);
+    return;
+  }
+  for (int j = w - a.ntiles; j < a.ntiles; j += a.lag) {
+    if (threadIdx.x == 0) {
+      int ok = 0;
+      for (int it = 0; it < (1 << 22); ++it) {
+        const unsigned f = __builtin_amdgcn_raw_buffer_load_b32(rsrc(a.flags), 4 * j, 0, 16);
+        if (f == a.epoch) {
+          ok = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (!ok) atomicAdd(a.err, 1u);
+      go = ok;
+    }
+    __syncthreads();
+    if (go) bcast_tile(a, j);
+    __syncthreads();
+  }
+}
+
 __global__ void hash_fill(float* p, int64_t n, uint32_t seed) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -223,7 +258,13 @@ int main(int argc, char** argv) {
                          {"lab_two_launches", -1}, {"product_round", -2},
                          {"lag_split_grid", T},    {"lag_4096", 4096},
                          {"lag_2048", 2048},       {"lag_1024", 1024},
-                         {"lag_512", 512}};
+                         {"lag_512", 512},         {"persist_full", -10},
+                         {"persist_half", -11},    {"persist_quarter", -12}};
+    int occ = 0, cus = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(persist_k),
+                                                    256, 0));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const int slots = occ * cus;
     int ctr = 0;
     auto run = [&](const V& v) {
       Args a = args[ctr++ % L.rot];
@@ -236,6 +277,12 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(bcast_k, dim3(T), dim3(256), 0, 0, a);
       } else if (v.lag == -2) {
         FA(fa_reduce(plan, a.c, nullptr, L.n, nullptr, a.out, nullptr, FA_F_BCAST, nullptr));
+      } else if (v.lag <= -10) {
+        const int P = std::max(1, std::min(T, v.lag == -10 ? slots - 1
+                                              : v.lag == -11 ? slots / 2 : slots / 4));
+        a.lag = P;
+        a.epoch = ++epoch;
+        hipLaunchKernelGGL(persist_k, dim3(T + P), dim3(256), 0, 0, a);
       } else {
         a.lag = std::min(v.lag, T);
         a.epoch = ++epoch;
