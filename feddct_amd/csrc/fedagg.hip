@@ -703,17 +703,6 @@ struct fa_plan {
   // cut from a segment list with FA_PLAN_GAPS_ARE_PADDING: every byte of
   // the buckets is a tensor's or padding, so the broadcast may copy them flat
   bool flat_bcast = false;
-  // the one-launch round (reduce_impl.h round_kernel, calls of < 16
-  // clients): the tiles' hand-off words (+ a poll-timeout counter), made on
-  // the first such call; each call's token; the stream and an event of the
-  // last such call — a call on another stream waits for it, so two rounds
-  // never share the words at once
-  mutable std::mutex round_mu;
-  mutable unsigned* d_pub = nullptr;
-  mutable int pub_cap = 0;
-  mutable unsigned token = 0;
-  mutable hipStream_t round_stream = nullptr;
-  mutable hipEvent_t round_ev = nullptr;
 };
 
 namespace {
@@ -1067,88 +1056,6 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
     default: return b == 16 ? launch_u<2, 16>(a, ntiles, deep, w, st)
                             : launch_u<2, 8>(a, ntiles, deep, w, st);
   }
-}
-
-// The one-launch round (reduce_impl.h round_kernel): for calls of fewer than
-// 16 clients (the 8-client-batch kernels), CPU order.
-// FA_EXP_ROUND (experiment runs only, read once): "two" never, "one" for
-// every call below 256 clients; FA_EXP_ROUND_NBC=split: one broadcaster per
-// tile (not deadlock-free: timing only).
-int exp_round_mode() {
-  static const int m = [] {
-    const char* e = getenv("FA_EXP_ROUND");
-    return !e ? 0 : strcmp(e, "two") == 0 ? 1 : strcmp(e, "one") == 0 ? 2 : 0;
-  }();
-  return m;
-}
-bool use_round_kernel(const fa_plan* plan, int n) {
-  if (plan->order != FA_ORDER_TORCH_CPU || n < 1 || n > kInline) return false;
-  const int m = exp_round_mode();
-  if (m == 1) return false;
-  if (m == 2) return n < 256;
-  return n < 16;
-}
-
-// resident workgroups of round_kernel<U, W> per CU on `dev` (cached)
-int round_occupancy(int dev, int u, bool w, int* cus) {
-  static std::mutex mu;
-  static std::map<int, std::pair<int, int>> cache;
-  const int key = (dev * 8 + u) * 2 + (w ? 1 : 0);
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find(key);
-  if (it == cache.end()) {
-    const int occ = u == 1 ? occupancy_round_u<1>(w) : u == 4 ? occupancy_round_u<4>(w)
-                                                             : occupancy_round_u<2>(w);
-    int c = 0;
-    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) c = 0;
-    it = cache.emplace(key, std::make_pair(occ, c)).first;
-  }
-  *cus = it->second.second;
-  return it->second.first;
-}
-
-hipError_t launch_round(const fa_plan* plan, ReduceArgs& a, int vec_u, bool w, int cap,
-                        hipStream_t st) {
-  std::lock_guard<std::mutex> lk(plan->round_mu);
-  if (plan->pub_cap < cap + 1) {
-    if (plan->d_pub) {
-      hipError_t e = hipStreamSynchronize(plan->round_stream);
-      if (e == hipSuccess) e = hipFree(plan->d_pub);
-      if (e != hipSuccess) return e;
-      plan->d_pub = nullptr;
-    }
-    hipError_t e = hipMalloc(&plan->d_pub, (size_t)(cap + 1) * sizeof(unsigned));
-    if (e == hipSuccess) e = hipMemset(plan->d_pub, 0, (size_t)(cap + 1) * sizeof(unsigned));
-    if (e != hipSuccess) return e;
-    plan->pub_cap = cap + 1;
-    plan->token = 0;
-  }
-  if (plan->round_ev && plan->round_stream != st) {
-    const hipError_t e = hipStreamWaitEvent(st, plan->round_ev, 0);
-    if (e != hipSuccess) return e;
-  }
-  if (++plan->token == 0) ++plan->token;  // the words start at 0: never a token
-  int cus = 0;
-  const int occ = round_occupancy(plan->device, vec_u, w, &cus);
-  // one slot per CU never holds a broadcaster (round_kernel: the launch
-  // always completes, whatever the dispatch order)
-  int nbc = occ >= 2 && cus > 0 ? (occ - 1) * cus : 1;
-  static const bool split = [] {
-    const char* e = getenv("FA_EXP_ROUND_NBC");
-    return e && strcmp(e, "split") == 0;
-  }();
-  if (split) nbc = a.ntiles;
-  a.pub = plan->d_pub;
-  a.token = plan->token;
-  a.nbc = std::max(1, std::min(nbc, a.ntiles));
-  hipError_t e = vec_u == 1 ? launch_round_u<1>(a, w, st)
-               : vec_u == 4 ? launch_round_u<4>(a, w, st) : launch_round_u<2>(a, w, st);
-  if (e != hipSuccess) return e;
-  if (!plan->round_ev && (e = hipEventCreateWithFlags(&plan->round_ev, hipEventDisableTiming)))
-    return e;
-  e = hipEventRecord(plan->round_ev, st);
-  plan->round_stream = st;
-  return e;
 }
 
 // Stateless-API plan cache, keyed by device + layout.
@@ -1818,8 +1725,6 @@ int fa_plan_create_from_tiles(const fa_tile_desc* tiles, int ntiles, int64_t f32
 
 int fa_plan_destroy(fa_plan* plan) {
   if (!plan) return FA_OK;
-  if (plan->round_ev) HIP_TRY(hipEventDestroy(plan->round_ev));
-  if (plan->d_pub) HIP_TRY(hipFree(plan->d_pub));
   if (plan->d_fac) HIP_TRY(hipFree(plan->d_fac));
   if (plan->d_tiles) HIP_TRY(hipFree(plan->d_tiles));
   if (plan->d_tiles_alt) HIP_TRY(hipFree(plan->d_tiles_alt));
@@ -2107,19 +2012,11 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
   a.sidx = L.sidx;
   const int ntiles = L.nt, vec_u = L.vec_u;
   a.ntiles = ntiles;
-  // the broadcast: in the same launch for calls of < 16 clients, else its
-  // own launch after the reduce
+  // the broadcast is its own launch after the reduce
   const bool bcast = (flags & FA_F_BCAST) != 0;
   a.flags &= ~FA_F_BCAST;
-  hipError_t e;
-  if (bcast && use_round_kernel(plan, n)) {
-    int cap = std::max(plan->nt_dev, plan->nt_alt_dev);
-    for (const fa_plan::BalTable& b : plan->bal) cap = std::max(cap, b.nt);
-    e = launch_round(plan, a, vec_u, weights != nullptr, cap, st);
-  } else {
-    e = launch_reduce(a, ntiles, vec_u, plan->flags, st, L.batch);
-    if (e == hipSuccess && bcast) e = launch_bcast(plan, a, n, ntiles, st);
-  }
+  hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st, L.batch);
+  if (e == hipSuccess && bcast) e = launch_bcast(plan, a, n, ntiles, st);
   if (table) {
     hipError_t e2 = hipFreeAsync(table, st);
     if (e == hipSuccess) e = e2;

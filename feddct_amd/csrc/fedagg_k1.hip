@@ -6,4 +6,3 @@
 FA_K_LAUNCH_U(, 1, 8)
 FA_K_LAUNCH_U(, 1, 16)
 FA_K_LAUNCH_CHAIN(, 1, 8)
-FA_K_LAUNCH_ROUND(, 1)

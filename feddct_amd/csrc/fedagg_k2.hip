@@ -5,4 +5,3 @@
 
 FA_K_LAUNCH_U(, 2, 8)
 FA_K_LAUNCH_CHAIN(, 2, 8)
-FA_K_LAUNCH_ROUND(, 2)

@@ -5,4 +5,3 @@
 
 FA_K_LAUNCH_U(, 4, 8)
 FA_K_LAUNCH_CHAIN(, 4, 8)
-FA_K_LAUNCH_ROUND(, 4)

@@ -93,11 +93,6 @@ struct ReduceArgs {
   int64_t plane;
   const float* tfac;  // torch-GPU order: per-tile mean factor fl(M)/fl(N*M)
   const int64_t* sidx;  // packed scalar tiles' entries (K_SCALAR_PACKED)
-  // the one-launch round (round_kernel): tile t's hand-off word, this call's
-  // token, the broadcasting workgroups
-  unsigned* pub;
-  unsigned token;
-  int nbc;
   const float* const* tab32;
   const int64_t* const* tab64;
   const float* tabw;
@@ -533,22 +528,7 @@ struct SrcLdsCol {
 };
 
 // One scalar column's order and result (kind: K_F32_* 1-3, K_I64_* 4-6).
-// PUB (the one-launch round): the results stored sc1 (write-through), the
-// hand-off's producer side (round_kernel)
-template <bool PUB>
-__device__ __forceinline__ void st_res32(float* p, float v) {
-  if constexpr (PUB)
-    __hip_atomic_store(reinterpret_cast<unsigned*>(p), __builtin_bit_cast(unsigned, v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <bool PUB>
-__device__ __forceinline__ void st_res64(int64_t* p, int64_t v) {
-  if constexpr (PUB) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-
-template <bool WEIGHTED, class SrcF, class SrcI, bool PUB = false>
+template <bool WEIGHTED, class SrcF, class SrcI>
 __device__ __forceinline__ void scalar_column(KArgs& a, const SrcF& sf, const SrcI& si, int64_t e,
                                               int kind) {
   const int n = a.n;
@@ -560,7 +540,7 @@ __device__ __forceinline__ void scalar_column(KArgs& a, const SrcF& sf, const Sr
     else s = inner_seq(sf, e, n);
     s = __fadd_rn(0.f, s);  // sum_out: out (=+0) += value
     const bool sum_only = WEIGHTED || (a.flags & FA_F_SUM_ONLY);
-    st_res32<PUB>(a.out32 + e, sum_only ? s : __fdiv_rn(s, fn));
+    a.out32[e] = sum_only ? s : __fdiv_rn(s, fn);
   } else {
     float s;
     if (kind == K_I64_CASC) s = cascade_seq(si, e, 0, 1, n);
@@ -568,7 +548,7 @@ __device__ __forceinline__ void scalar_column(KArgs& a, const SrcF& sf, const Sr
     else s = inner_seq(si, e, n);
     s = __fadd_rn(0.f, s);
     // load_state_dict copy_: fp32 -> int64 truncates toward zero
-    st_res64<PUB>(a.out64 + e, (int64_t)__fdiv_rn(s, fn));
+    a.out64[e] = (int64_t)__fdiv_rn(s, fn);
   }
 }
 
@@ -584,7 +564,7 @@ constexpr int kPackCols = 64;
 // slots -1), so a scalar workgroup needs no tile descriptor: its first load
 // is its entries, one dependent round trip fewer on the critical path of
 // these latency-bound workgroups.
-template <bool WEIGHTED, bool PUB = false>
+template <bool WEIGHTED>
 __device__ __forceinline__ void tile_scalar_packed(KArgs& a, int k) {
   __shared__ float stage[kStageFloats];
   const int n = a.n;
@@ -595,8 +575,7 @@ __device__ __forceinline__ void tile_scalar_packed(KArgs& a, int k) {
     if (wv == 0) {
       const int64_t ent = ents[lane];
       if (ent >= 0)
-        scalar_column<WEIGHTED, SrcF32, SrcI64, PUB>(a, SrcF32{a, WEIGHTED}, SrcI64{a}, ent >> 4,
-                                                     (int)(ent & 15));
+        scalar_column<WEIGHTED>(a, SrcF32{a, WEIGHTED}, SrcI64{a}, ent >> 4, (int)(ent & 15));
     }
     return;
   }
@@ -625,17 +604,17 @@ __device__ __forceinline__ void tile_scalar_packed(KArgs& a, int k) {
     __syncthreads();
     if (wv == 0 && mine) {
       const SrcLdsCol src{stage, m, lane};
-      scalar_column<WEIGHTED, SrcLdsCol, SrcLdsCol, PUB>(a, src, src, e, kind);
+      scalar_column<WEIGHTED>(a, src, src, e, kind);
     }
     __syncthreads();
   }
 }
 
-template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN, bool PUB = false>
+template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN>
 __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
   if constexpr (!CHAIN) {
     if (ti < a.nscalar) {  // the packed scalar tiles lead the table
-      tile_scalar_packed<WEIGHTED, PUB>(a, ti);
+      tile_scalar_packed<WEIGHTED>(a, ti);
       return;
     }
   }
@@ -656,130 +635,6 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs args) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   run_tile<U, B, DEEP, WEIGHTED, POL, CHAIN>(a, blockIdx.x);
-}
-
-// ------------------------------------------------- the one-launch round --
-// The whole round (reduce, global load, broadcast: train_fedavg.py:145-149)
-// as ONE launch, for calls of fewer than 16 clients (r05): a
-// launch boundary costs ~2 us (MI355X_MICROARCH.md), and these rounds' two
-// short phases run side by side instead of ramping and draining twice
-// (tools/laglab.hip, profiles/r05_laglab*.jsonl: sf32 N = 3 27.5 vs 30.9 us
-// for the same lab kernels as two launches, cfg3 N = 5 77.4 vs 80.5; at
-// N = 20 one launch is 1 % slower, so larger calls keep two launches).
-//   blocks [0, ntiles): the reduce of their tile exactly as reduce_kernel
-//     (B = 8, not deep; the vector results stored sc1 as always, the packed
-//     scalar results sc1 too), then every wave waits for its stores
-//     (vmcnt(0)), a barrier, and lane 0 stores the tile's hand-off word =
-//     this call's token (sc1): MI355X_MICROARCH.md's inter-workgroup
-//     hand-off, the sc1 table's first row;
-//   blocks [ntiles, ntiles + nbc): broadcasters, tiles j = b - ntiles,
-//     b - ntiles + nbc, ...: lane 0 polls tile j's word with sc1 loads until
-//     it holds the token, a barrier, then every load of the tile's result is
-//     an sc1 load and every client gets it (sc1 nt stores, as the two-launch
-//     broadcast).  nbc is below the resident workgroups of this kernel by one
-//     per CU, so however the hardware orders the dispatch, broadcasters can
-//     never hold every slot a pending reducer needs: the launch always
-//     completes.  (The poll is bounded besides; a poll that runs out counts
-//     in pub[ntiles] and leaves that tile unbroadcast — never seen, tested.)
-// Bits: the reducers run reduce_kernel's code, so the result is the same.
-constexpr int kPollMax = 1 << 24;
-
-__device__ __forceinline__ void st_pub(float* base, uint32_t vidx, f4 v) {
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(16 * vidx), 0, 18);  // sc1 nt
-}
-__device__ __forceinline__ f4 ld_pub(const float* base, uint32_t vidx) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
-  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(16 * vidx), 0, 16));
-}
-
-template <int U>
-__device__ __forceinline__ void round_bcast_tile(KArgs& a, int j) {
-  const Tile t = a.tiles[j];
-  const int n = a.n;
-  if (t.kind == K_F32_VEC) {
-    const uint32_t nv = (uint32_t)t.count / 4;
-    f4 r[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t vi = threadIdx.x + u * kBlock;
-      if (vi < nv) r[u] = ld_pub(a.out32 + t.start, vi);
-    }
-    for (int i = 0; i < n; ++i) {
-      float* d = sptr32(a, i) + t.start;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t vi = threadIdx.x + u * kBlock;
-        if (vi < nv) st_pub(d, vi, r[u]);
-      }
-    }
-  } else if ((int)threadIdx.x < t.count) {  // K_SCALAR_PACKED: one column per lane
-    const int64_t ent = a.sidx[t.start + threadIdx.x];
-    if (ent < 0) return;
-    const int64_t e = ent >> 4;
-    if (!kind_is64((int)(ent & 15))) {
-      const unsigned x = __hip_atomic_load(reinterpret_cast<unsigned*>(a.out32 + e),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int i = 0; i < n; ++i) sptr32(a, i)[e] = __builtin_bit_cast(float, x);
-    } else {
-      const int64_t x = __hip_atomic_load(a.out64 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int i = 0; i < n; ++i) sptr64(a, i)[e] = x;
-    }
-  }
-}
-
-template <int U, bool W>
-__global__ __launch_bounds__(kBlock) void round_kernel(ReduceArgs args) {
-  (void)args;
-  KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  const int b = blockIdx.x;
-  if (b < a.ntiles) {
-    run_tile<U, 8, false, W, 5, false, true>(a, b);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store(a.pub + b, a.token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  __shared__ int go;
-  for (int j = b - a.ntiles; j < a.ntiles; j += a.nbc) {
-    if (threadIdx.x == 0) {
-      int ok = 0;
-      for (int it = 0; it < kPollMax; ++it) {
-        if (__hip_atomic_load(a.pub + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.token) {
-          ok = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      if (!ok) atomicAdd(a.pub + a.ntiles, 1u);
-      go = ok;
-    }
-    __syncthreads();
-    if (go) round_bcast_tile<U>(a, j);
-    __syncthreads();
-  }
-}
-
-template <int U, bool W>
-hipError_t launch_round_uw(const ReduceArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((round_kernel<U, W>), dim3(a.ntiles + a.nbc), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
-}
-template <int U>
-hipError_t launch_round_u(const ReduceArgs& a, bool w, hipStream_t st) {
-  return w ? launch_round_uw<U, true>(a, st) : launch_round_uw<U, false>(a, st);
-}
-template <int U>
-int occupancy_round_u(bool w) {
-  int nb = 0;
-  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &nb, w ? reinterpret_cast<const void*>(round_kernel<U, true>)
-             : reinterpret_cast<const void*>(round_kernel<U, false>),
-      kBlock, 0);
-  return e == hipSuccess ? nb : 0;
 }
 
 // --------------------------------------------------------------- launches --
@@ -836,9 +691,6 @@ int occupancy_u(bool deep, bool w) {
   EXT template hipError_t fa_k::launch_u<U, B>(const fa_k::ReduceArgs&, int, bool, bool,      \
                                                 hipStream_t);                                 \
   EXT template int fa_k::occupancy_u<U, B>(bool, bool);
-#define FA_K_LAUNCH_ROUND(EXT, U)                                                              \
-  EXT template hipError_t fa_k::launch_round_u<U>(const fa_k::ReduceArgs&, bool, hipStream_t); \
-  EXT template int fa_k::occupancy_round_u<U>(bool);
 #define FA_K_LAUNCH_CHAIN(EXT, U, B)                                                          \
   EXT template hipError_t fa_k::launch_chain_ub<U, B>(const fa_k::ReduceArgs&, int, bool, bool, \
                                                        hipStream_t);
@@ -846,5 +698,4 @@ int occupancy_u(bool deep, bool w) {
   FA_K_LAUNCH_U(EXT, 1, 8) FA_K_LAUNCH_U(EXT, 1, 16) FA_K_LAUNCH_CHAIN(EXT, 1, 8)       \
   FA_K_LAUNCH_U(EXT, 2, 8) FA_K_LAUNCH_CHAIN(EXT, 2, 8)                                  \
   FA_K_LAUNCH_U(EXT, 2, 16) FA_K_LAUNCH_CHAIN(EXT, 2, 16)                                \
-  FA_K_LAUNCH_U(EXT, 4, 8) FA_K_LAUNCH_CHAIN(EXT, 4, 8)                                  \
-  FA_K_LAUNCH_ROUND(EXT, 1) FA_K_LAUNCH_ROUND(EXT, 2) FA_K_LAUNCH_ROUND(EXT, 4)
+  FA_K_LAUNCH_U(EXT, 4, 8) FA_K_LAUNCH_CHAIN(EXT, 4, 8)

@@ -282,13 +282,12 @@ def test_broadcast_forms_and_bcast_only(lib, n, form):
 @pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 15, 16, 20])
 @pytest.mark.parametrize("weighted", [False, True])
 @pytest.mark.parametrize("tile", [0, 1024, 4096])
-def test_round_one_launch_and_two(lib, n, weighted, tile):
-    """r05: FA_F_BCAST rounds of < 16 clients run as ONE launch
-    (reduce_impl.h round_kernel: reducers publish each tile, broadcasters
-    wait for it), 16 and more as reduce + broadcast launches.  Both: the
+def test_round_small_n_every_tile_width(lib, n, weighted, tile):
+    """FA_F_BCAST rounds around the 8- / 16-client kernel boundary: the
     global is the oracle's bits and every client's segments equal it; every
-    tile width (the kernel's U = 1, 2, 4), weighted or not, packed scalar
-    columns and int64 keys included."""
+    tile width (U = 1, 2, 4), weighted or not, packed scalar columns and
+    int64 keys included.  (r05 measured a one-launch form of these rounds —
+    slower, DESIGN §4.2 item 5 — and kept reduce + broadcast.)"""
     man = _rand_manifest(None, [100, 4096, 7, 3000, 1, 64, 20000, 3, 9000])
     layout = BucketLayout.from_manifest(man)
     states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
@@ -319,12 +318,10 @@ def test_round_one_launch_and_two(lib, n, weighted, tile):
         assert torch.equal(i[:layout.i64_numel], o64[:layout.i64_numel])
 
 
-def test_round_one_launch_across_streams(lib):
-    """The one-launch round's hand-off words belong to the plan: rounds on
-    one plan issued on two streams without any host synchronisation are
-    serialised by the plan (a call on another stream waits for the last
-    one), so every round is exact.  Eight client sets of 5, the streams
-    alternating."""
+def test_round_one_plan_two_streams(lib):
+    """A plan is read-only in a round: rounds on one plan issued on two
+    streams without any host synchronisation are each exact (eight client
+    sets of 5, the streams alternating)."""
     man = _rand_manifest(None, [4096, 33, 50000, 1, 7000])
     layout = BucketLayout.from_manifest(man)
     plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
