@@ -2012,14 +2012,6 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
   a.sidx = L.sidx;
   const int ntiles = L.nt, vec_u = L.vec_u;
   a.ntiles = ntiles;
-  {
-    // experiment (FA_EXP_BURST=k): the last k rounds' tiles issue a batch's
-    // loads at once
-    const char* ev = getenv("FA_EXP_BURST");
-    const int kb = ev ? atoi(ev) : 0;
-    a.burst_from = (kb > 0 && L.slots > 0 && n <= kInline) ? std::max(1, ntiles - kb * L.slots)
-                                                           : ntiles;
-  }
   // the broadcast is its own launch after the reduce
   const bool bcast = (flags & FA_F_BCAST) != 0;
   a.flags &= ~FA_F_BCAST;

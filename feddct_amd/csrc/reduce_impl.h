@@ -93,7 +93,6 @@ struct ReduceArgs {
   int64_t plane;
   const float* tfac;  // torch-GPU order: per-tile mean factor fl(M)/fl(N*M)
   const int64_t* sidx;  // packed scalar tiles' entries (K_SCALAR_PACKED)
-  int burst_from;  // experiment: tiles (== blocks) from here (> 0; 0 = off) issue loads at once
   const float* const* tab32;
   const int64_t* const* tab64;
   const float* tabw;
@@ -289,18 +288,9 @@ __device__ __forceinline__ void promote(Acc<U, DEEP>& A, int ii, int lp, int mas
   }
 }
 
-// DIRECT (experiment): the kernarg pointer array read directly (n <= the
-// inline count), which lets the compiler issue the batch's loads back to back
-template <bool TAB, bool DIRECT>
-__device__ __forceinline__ const float* bptr(KArgs& a, int i) {
-  if constexpr (DIRECT) return a.c32[i];
-  else return vptr32<TAB>(a, i);
-}
-
 // One batch of NB clients starting at b0.  FULL: every lane's U vectors are
 // inside the tile (no per-lane predicate).
-template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool TAB,
-          bool DIRECT = false>
+template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool TAB>
 __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t start,
                                       const uint32_t (&vi)[U], const bool (&ok)[U],
                                       int lp, int mask, int r0) {
@@ -309,7 +299,7 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t
   if constexpr (WEIGHTED) load_weights<NB>(a, b0, NB, wb);
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const float* p = bptr<TAB, DIRECT>(a, b0 + b) + start;
+    const float* p = vptr32<TAB>(a, b0 + b) + start;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
@@ -330,8 +320,7 @@ __device__ __forceinline__ void batch(KArgs& a, Acc<U, DEEP>& A, int b0, int64_t
 
 // The last, partial batch (nb < NB clients): same issue-all-then-add shape,
 // every step guarded by a uniform (scalar) branch.
-template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool TAB,
-          bool DIRECT = false>
+template <int U, int NB, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool TAB>
 __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, int nb,
                                            int64_t start, const uint32_t (&vi)[U],
                                            const bool (&ok)[U], int lp, int mask, int r0) {
@@ -341,7 +330,7 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     if (b < nb) {
-      const float* p = bptr<TAB, DIRECT>(a, b0 + b) + start;
+      const float* p = vptr32<TAB>(a, b0 + b) + start;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if constexpr (FULL) x[b][u] = ldg4<(POL & 1) != 0>(p, vi[u]);
@@ -404,19 +393,11 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
     }
   }
   int b0 = 0;
-  if (!CHAIN && !TAB && a.burst_from > 0 && (int)blockIdx.x >= a.burst_from) {
-    for (; b0 + B <= n; b0 += B)
-      batch<U, B, FULL, DEEP, WEIGHTED, POL, TAB, true>(a, A, b0, start, vi, ok, lp, mask, r0);
-    if (b0 < n)
-      batch_tail<U, B, FULL, DEEP, WEIGHTED, POL, TAB, true>(a, A, b0, n - b0, start, vi, ok, lp,
-                                                             mask, r0);
-  } else {
-    for (; b0 + B <= n; b0 += B)
-      batch<U, B, FULL, DEEP, WEIGHTED, POL, TAB>(a, A, b0, start, vi, ok, lp, mask, r0);
-    if (b0 < n)
-      batch_tail<U, B, FULL, DEEP, WEIGHTED, POL, TAB>(a, A, b0, n - b0, start, vi, ok, lp, mask,
-                                                       r0);
-  }
+  for (; b0 + B <= n; b0 += B)
+    batch<U, B, FULL, DEEP, WEIGHTED, POL, TAB>(a, A, b0, start, vi, ok, lp, mask, r0);
+  if (b0 < n)
+    batch_tail<U, B, FULL, DEEP, WEIGHTED, POL, TAB>(a, A, b0, n - b0, start, vi, ok, lp, mask,
+                                                     r0);
   if constexpr (CHAIN) {
     if (a.st_out) {
       const int lo = a.lev_out;
