@@ -1,6 +1,9 @@
 """Summarise rocprofv3 output for the reduce kernel into profiles/.
 
-    python tools/pmc_summary.py <kernel_trace_dir> <fetch_dir> <write_dir> <out.json>
+    python tools/pmc_summary.py <kernel_trace_dir> <fetch_dir> <write_dir> <out.json> [bench_log]
+    env FA_PMC_KERNEL / FA_PMC_WORKLOAD / FA_PMC_ALG_BYTES / FA_PMC_COMMAND:
+    another kernel or workload than the headline (e.g. cfg3 from
+    tools/cfg3_prof.sh, the proximal term's kernels from tools/prox_prof.sh)
 
 FETCH_SIZE / WRITE_SIZE come from separate --pmc passes (they do not fit in
 one pass on gfx950).  Corrections per MI355X_MICROARCH.md §HBM: both are in
@@ -15,7 +18,7 @@ import os
 import sys
 import time
 
-KERNEL = "reduce_kernel"
+KERNEL = os.environ.get("FA_PMC_KERNEL", "reduce_kernel")
 
 
 def rows(d, pattern):
@@ -49,7 +52,7 @@ def main():
     med = lambda v: sorted(v)[len(v) // 2] if v else None  # noqa: E731
     fk, wk = med(fetch), med(write)
     res = {
-        "workload": "wrn16_8_c10/n20",
+        "workload": os.environ.get("FA_PMC_WORKLOAD", "wrn16_8_c10/n20"),
         "kernel": stats[0]["Name"] if stats else None,
         "calls": int(stats[0]["Calls"]) if stats else None,
         "avg_ns": float(stats[0]["AverageNs"]) if stats else None,
@@ -58,12 +61,14 @@ def main():
         "fetch_bytes_corrected": None if fk is None else 2 * fk * 1024,
         "write_bytes": None if wk is None else wk * 1024,
         "hbm_bytes_per_launch": None if fk is None or wk is None else 2 * fk * 1024 + wk * 1024,
-        "algorithmic_bytes_per_launch": 20 * 43888744 + 43888744,
+        "algorithmic_bytes_per_launch": int(os.environ.get("FA_PMC_ALG_BYTES",
+                                                            20 * 43888744 + 43888744)),
         "correction": "FETCH_SIZE x2 (gfx950 wide-stream half count), KiB x1024",
         # the HIP-event launch time bench.py measured inside the profiled run
         "bench_kernel_us_same_run": (bench_line or {}).get("roofline", {}).get("kernel_us"),
-        "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --kernel-only "
-                   "--no-cpu-baseline --steps 100 --warmup 100",
+        "command": os.environ.get("FA_PMC_COMMAND",
+                                  "rocprofv3 --kernel-trace --stats -- python3 bench.py "
+                                  "--kernel-only --no-cpu-baseline --steps 100 --warmup 100"),
         # where and when the counters were taken (the bench line cites them)
         "date_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
         "host": os.uname().nodename,

@@ -3,7 +3,9 @@ r03 next 6): bench next_rows' step (train_fedprox.py:113-136 shape: the
 client's gradients zeroed, the one-node proximal term, its backward) on the
 wrn16_8 C100 layout, split into host phases (perf_counter, no sync inside:
 what the Python / autograd side costs) and the same step's GPU time (its
-three launches back to back).  One JSON line.  Usage: prox_profile.py [REPS]"""
+three launches back to back).  One JSON line.  Usage: prox_profile.py [REPS]
+    prox_profile.py prof K   -> only the term's kernels, K times (rocprofv3
+                                kernel trace / PMC passes, tools/prox_prof.sh)"""
 import json
 import os
 import sys
@@ -20,7 +22,8 @@ from feddct_amd.workload import load_manifest  # noqa: E402
 
 
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    prof = len(sys.argv) > 2 and sys.argv[1] == "prof"
+    reps = int(sys.argv[2 if prof else 1]) if len(sys.argv) > 1 else 50
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     lay = BucketLayout.from_manifest(load_manifest("wrn16_8_c100"))
@@ -29,6 +32,34 @@ def main():
         client.zero_grad(set_to_none=True)
         proximal_term(client, glob, flat_grads=True).backward()
     torch.cuda.synchronize()
+    if prof:
+        # bench next_rows' kernel-only leg: fa_prox_norms + fa_prox_grad (both
+        # gradients overwritten: 24 B/param) over 4 rotated bucket sets
+        import ctypes
+        from feddct_amd import _lib
+        term = client.__dict__["_fa_prox"][id(glob)]
+        norms = torch.empty(max(1, term.plan.nseg), device=dev)
+        total = torch.empty((), device=dev)
+        one = torch.ones((), device=dev)
+        sets = [(term.ca.f32.clone(), term.ga.f32.clone(), torch.empty_like(term.ca.f32),
+                 torch.empty_like(term.ga.f32)) for _ in range(4)]
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        # beside them, a one-workgroup kernel that reads 256 B (the read
+        # probe at n = 64): the floor of any single-workgroup launch, for
+        # the finish's duration
+        tiny = torch.ones(64, device=dev)
+        sink = torch.zeros(256, device=dev)
+        for i in range(reps):
+            _lib.check(_lib.lib.fa_read_probe_f32(tiny.data_ptr(), 64, sink.data_ptr(), 0, st))
+            a, b, ga, gb = sets[i % 4]
+            _lib.check(_lib.lib.fa_prox_norms(term.plan.handle, a.data_ptr(), b.data_ptr(),
+                                              norms.data_ptr(), total.data_ptr(), st))
+            _lib.check(_lib.lib.fa_prox_grad(term.plan.handle, a.data_ptr(), b.data_ptr(),
+                                             norms.data_ptr(), one.data_ptr(), 1.0,
+                                             ga.data_ptr(), gb.data_ptr(), st))
+        torch.cuda.synchronize()
+        print(f"prox term kernels: {reps} steps, {lay.f32_numel} floats per bucket")
+        return
     ph = {k: [] for k in ("zero_grad", "term_call", "backward", "step_host", "step_wall")}
     for _ in range(reps):
         torch.cuda.synchronize()
