@@ -1069,6 +1069,24 @@ def next_rows(dev, steps=30):
           "note": "step = the client's zero_grad (as the reference's optimizer) + the term's "
                   "fwd + bwd incl. autograd; term_fwd_bwd_us without the zero_grad; "
                   "reference = its loop on torch-ROCm"}
+    # where the kernels' time goes, from the committed profiler run of this
+    # leg (tools/prox_prof.sh -> profiles/r05_prox_pmc.json)
+    try:
+        with open(os.path.join(ROOT, "profiles", "r05_prox_pmc.json")) as f:
+            d = json.load(f)
+        s = d["summary"]
+        f3["kernels_pmc"] = {
+            "partials_us": round(d["prox_partials"]["avg_ns"] / 1e3, 2),
+            "finish_us": round(d["prox_finish"]["avg_ns"] / 1e3, 2),
+            "grad_us": round(d["prox_grad"]["avg_ns"] / 1e3, 2),
+            "one_workgroup_floor_us": round(d["one_workgroup_floor"]["avg_ns"] / 1e3, 2),
+            "partials_traffic_over_algorithmic": s["partials_traffic_over_algorithmic"],
+            "partials_vs_same_shape_read_probe": s["partials_vs_same_shape_read_probe_lab"],
+            "frac_without_finish": s["frac_without_finish"],
+            "limiter": "the finish (one workgroup) = the one-workgroup launch floor",
+            "source": "profiles/r05_prox_pmc.json", "profile_tree": d["prox_partials"].get("tree")}
+    except Exception:
+        pass
     # f4: checkpoint save of the bound global model
     from feddct_amd.aggregate import server_aggregate
     server_aggregate(glob, [client])  # binds glob's arena (and client's)
