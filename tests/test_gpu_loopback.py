@@ -214,3 +214,26 @@ def test_loopback_cfg5_default_entry_matches_reference_digest(tmp_path):
             h.update(s.key[len(prefix):].encode())
             h.update(np.ascontiguousarray(src[s.offset:s.offset + s.numel]).tobytes())
         assert h.hexdigest() == want[f"feddct/wrnsl16_8_sf4_c100_{name}/n24"], name
+
+
+def test_loopback_default_entry_random_shards(tmp_path):
+    """The default entry over seeded random shard shapes (W = 2..8, 0..40
+    slots per rank, empty ranks, every root, weighted and not): whatever form
+    it picks (blocked or chained by the counts), the result equals one GPU's
+    reduction of all the slots bit for bit."""
+    from feddct_amd import dist
+    rng = np.random.default_rng(20260518)
+    cases, forms = [], set()
+    while len(cases) < 14:
+        w = int(rng.integers(2, 9))
+        counts = [int(c) for c in rng.integers(0, 41, size=w)]
+        counts = [c if rng.random() > 0.15 else 0 for c in counts]
+        if sum(counts) == 0:
+            continue
+        holders = [r for r, c in enumerate(counts) if c]
+        root = int(rng.choice(holders + [-1]))
+        forms.add(dist.exact_form(counts))
+        cases.append(f"multi:{w}:{','.join(map(str, counts))}:{root}:threads:"
+                     f"{int(rng.random() < 0.5)}:0")
+    assert forms == {"blocked", "chained"}, forms
+    _run(_small_layout(), cases, tmp_path, timeout=300)
