@@ -1451,12 +1451,14 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
                     r["ulp_histogram_fp32"] = ulp_hist(o32[segmask], ex32[segmask])
                     r["int64_bit_exact"] = bool(torch.equal(o64, ex64))
             report[name] = r
-        # the headline: the fastest mode whose result is the reference's bits
-        # (decided on rank 0, shared so every rank agrees)
+        # the headline: the fastest EXACT-class mode whose result is the
+        # reference's bits (an e1 round is bit-exact by accident at one rank:
+        # never the headline) — decided on rank 0, shared so every rank agrees
         best_t, best = float("inf"), ""
         if rank == 0:
             for name, r in report.items():
-                if r.get("bit_exact") and modes[name]["t"] < best_t:
+                if (r.get("bit_exact") and modes[name]["exact_class"]
+                        and modes[name]["t"] < best_t):
                     best_t, best = modes[name]["t"], name
         sel = [best, best_t]
         dist.broadcast_object_list(sel, src=0, group=group)
