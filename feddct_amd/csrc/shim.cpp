@@ -555,10 +555,7 @@ PyObject* prox_state(PyObject*, PyObject* args) {
   auto st = std::make_shared<ProxState>();
   st->norms_fn = reinterpret_cast<prox_norms_fn>(fn_n);
   st->grad_fn = reinterpret_cast<prox_grad_fn>(fn_g);
-  const plan_destroy_fn destroy = reinterpret_cast<plan_destroy_fn>(fn_d);
-  st->plan_owner = std::shared_ptr<void>(reinterpret_cast<void*>(plan),
-                                         [destroy](void* p) { (void)destroy(p); });
-  st->plan = st->plan_owner.get();
+  st->plan = reinterpret_cast<const void*>(plan);
   st->bucket_a = THPVariable_Unpack(bka);
   st->bucket_b = THPVariable_Unpack(bkb);
   st->pa = st->bucket_a.data_ptr<float>();
@@ -585,8 +582,18 @@ PyObject* prox_state(PyObject*, PyObject* args) {
     }
     sd.acc_flag = fl[k];
   }
-  return PyCapsule_New(new std::shared_ptr<ProxState>(st), "feddct_amd.prox_state",
-                       prox_capsule_free);
+  auto* holder = new std::shared_ptr<ProxState>(st);
+  PyObject* cap = PyCapsule_New(holder, "feddct_amd.prox_state", prox_capsule_free);
+  if (!cap) {
+    delete holder;  // the plan is still the caller's: nothing owned it yet
+    return nullptr;
+  }
+  // ownership of the plan passes only here, once nothing can fail: on any
+  // error above the caller still owns (and destroys) it
+  const plan_destroy_fn destroy = reinterpret_cast<plan_destroy_fn>(fn_d);
+  st->plan_owner = std::shared_ptr<void>(reinterpret_cast<void*>(plan),
+                                         [destroy](void* p) { (void)destroy(p); });
+  return cap;
 }
 
 // prox_apply(state, anchor, stream) -> the term (0-dim fp32 tensor), whose

@@ -59,3 +59,35 @@ def test_src_match_is_an_identity_check():
     assert _fa_shim.src_match(array("Q").tobytes())      # nothing recorded, nothing passed
     with pytest.raises(TypeError):
         _fa_shim.src_match("not bytes", g)
+
+
+def test_prox_state_takes_the_plan_only_on_success():
+    """prox_state (the one-node proximal term's capsule):
+    the norm plan's ownership passes to the capsule only once nothing can
+    fail — a rejected call leaves the plan with the caller (no destroy, so
+    the caller's own release is the only one), and a made capsule destroys it
+    exactly once, when the capsule goes (no autograd node holds it here)."""
+    import ctypes
+    import gc
+    import torch
+    freed = []
+    DESTROY = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+    cb = DESTROY(lambda p: freed.append(p) or 0)
+    addr = ctypes.cast(cb, ctypes.c_void_p).value
+    plan = 0x1234500
+    f = torch.zeros(64)
+    norms, scratch = torch.zeros(2), torch.zeros(64)
+    ps = (torch.nn.Parameter(torch.zeros(4)),)
+    vs = (torch.zeros(4),)
+    # the caller's fault after the tensors were checked: a params tuple of non-tensors
+    with pytest.raises(TypeError):
+        _fa_shim.prox_state(addr, addr, addr, plan, f, f, norms, scratch, (1, 2), vs, None, 1,
+                            ps, vs, None, 2)
+    gc.collect()
+    assert freed == []
+    cap = _fa_shim.prox_state(addr, addr, addr, plan, f, f, norms, scratch, ps, vs, None, 1,
+                              ps, vs, None, 2)
+    assert freed == []
+    del cap
+    gc.collect()
+    assert freed == [plan]
