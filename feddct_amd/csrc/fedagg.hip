@@ -1798,6 +1798,15 @@ struct Launch {
   int slots;  // resident workgroups of its kernel (0: unknown / tuning grid)
   int batch;  // clients per load batch of its kernel
 };
+// The clients two deep (reduce_impl.h pipe2_clients) where it measured
+// faster: unweighted calls of 17..63 clients (inline pointers) on the plain
+// 2048-float table — not the 1024-float table, not a table re-cut for the
+// round count (profiles/r05_exp_pipe2_*.jsonl)
+bool pipe_rule(const fa_plan* plan, const Launch& L, int n, bool weighted) {
+  return !weighted && n >= 17 && n <= 63 && n <= kInline && L.vec_u == 2 &&
+         L.tiles == plan->d_tiles;
+}
+
 Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) {
   Launch L{plan->d_tiles, plan->nt_dev, plan->ns_dev, plan->d_sidx, plan->vec_u, 0, 0};
   bool alt = false;
@@ -2012,6 +2021,7 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
   a.sidx = L.sidx;
   const int ntiles = L.nt, vec_u = L.vec_u;
   a.ntiles = ntiles;
+  a.pipe = pipe_rule(plan, L, n, weights != nullptr) ? 1 : 0;
   // the broadcast is its own launch after the reduce
   const bool bcast = (flags & FA_F_BCAST) != 0;
   a.flags &= ~FA_F_BCAST;

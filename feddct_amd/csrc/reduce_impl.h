@@ -93,6 +93,7 @@ struct ReduceArgs {
   int64_t plane;
   const float* tfac;  // torch-GPU order: per-tile mean factor fl(M)/fl(N*M)
   const int64_t* sidx;  // packed scalar tiles' entries (K_SCALAR_PACKED)
+  int pipe;  // 1: the clients two deep (pipe2_clients; the launch rule in fedagg.hip)
   const float* const* tab32;
   const int64_t* const* tab64;
   const float* tabw;
@@ -352,6 +353,46 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
   }
 }
 
+// The clients two deep (r05): client b+1's loads are issued before client
+// b's adds, one client after another in slot order (the same order as the
+// batches: the bits are the batches' bits).  The batch form's compiled
+// rhythm waits for each client's loads before issuing the next client's, and
+// re-reads the batch's pointers every B clients; this one keeps two clients'
+// loads in flight per lane throughout.  Measured (tools/exp_pipe2_n.py,
+// profiles/r05_exp_pipe2_n.jsonl, same process): 1.1-1.6 % faster for
+// unweighted calls of 20-48 clients on the plain 2048-float table (cfg2
+// 134.2 vs 135.6 us), equal at 16, 7.5 % SLOWER on the 1024-float table
+// (unweighted N >= 64), slower on tables re-cut for the round count
+// (profiles/r05_exp_pipe2_balance.jsonl: cfg4's C100 layout 143.6 vs
+// 137.6 us), no better weighted — so the launch
+// takes it only for unweighted calls of 17..63 clients on the plain
+// 2048-float table (fedagg.hip, pipe_rule).
+// The loads are unpredicated: a lane past the tile's end reads the tile's
+// last vector instead (inside the bucket; its sums are never stored), so the
+// loop's control flow stays uniform and the loads stay in flight
+template <int U, bool DEEP, int POL>
+__device__ __forceinline__ void pipe2_clients(KArgs& a, Acc<U, DEEP>& A, int n, int64_t start,
+                                              const uint32_t (&vl)[U], int lp, int mask) {
+  f4 cur[U], nxt[U];
+  {
+    const float* p = a.c32[0] + start;
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = ldg4<(POL & 1) != 0>(p, vl[u]);
+  }
+  for (int b = 0; b < n; ++b) {
+    if (b + 1 < n) {
+      const float* p = a.c32[b + 1] + start;
+#pragma unroll
+      for (int u = 0; u < U; ++u) nxt[u] = ldg4<(POL & 1) != 0>(p, vl[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) A.l0[u] = add4(A.l0[u], cur[u]);
+    promote<U, DEEP>(A, b + 1, lp, mask);
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+  }
+}
+
 template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool CHAIN>
 __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
                                          int count) {
@@ -393,6 +434,14 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
     }
   }
   int b0 = 0;
+  if (!CHAIN && !TAB && !WEIGHTED && a.pipe && n <= kInline) {
+    uint32_t vl[U];
+    const uint32_t vmax = (uint32_t)(count - 1) / 4;
+#pragma unroll
+    for (int u = 0; u < U; ++u) vl[u] = FULL ? vi[u] : min(vi[u], vmax);
+    pipe2_clients<U, DEEP, POL>(a, A, n, start, vl, lp, mask);
+    b0 = n;
+  }
   for (; b0 + B <= n; b0 += B)
     batch<U, B, FULL, DEEP, WEIGHTED, POL, TAB>(a, A, b0, start, vi, ok, lp, mask, r0);
   if (b0 < n)

@@ -318,6 +318,35 @@ def test_round_small_n_every_tile_width(lib, n, weighted, tile):
         assert torch.equal(i[:layout.i64_numel], o64[:layout.i64_numel])
 
 
+@pytest.mark.parametrize("n", [16, 17, 20, 31, 33, 48, 63, 64])
+def test_two_deep_clients_on_the_plain_table(lib, n):
+    """r05: unweighted calls of 17..63 clients on the plain 2048-float table
+    keep two clients' loads in flight (reduce_impl.h pipe2_clients;
+    fedagg.hip pipe_rule) — a ragged layout (tiles past tensor ends, packed
+    scalar columns, int64 keys) with the plain table forced, against the
+    oracle bit for bit, mean and round (16 and 64 take the batch form)."""
+    man = _rand_manifest(None, [100, 4096, 7, 3000, 1, 64, 20000, 3, 9000, 2050])
+    layout = BucketLayout.from_manifest(man)
+    states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
+    bk = states_to_buckets(layout, states, DEV)
+    plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
+                    flags=lib.FA_PLAN_GAPS_ARE_PADDING | lib.FA_PLAN_TUNE_NO_BALANCE)
+    want = O.aggregate_state(states)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for fl in (0, lib.FA_F_BCAST):
+        o32 = torch.full_like(bk[0][0], np.nan)
+        o64 = torch.full_like(bk[0][1], -7)
+        lib.check(lib.lib.fa_reduce(plan.handle, lib.ptr_array([b[0].data_ptr() for b in bk]),
+                                    lib.ptr_array([b[1].data_ptr() for b in bk]), n, None,
+                                    o32.data_ptr(), o64.data_ptr(), fl, s))
+        torch.cuda.synchronize()
+        for (k, v), (_, g) in zip(want, buckets_to_state(layout, o32, o64)):
+            assert bits_equal(g, v), (n, fl, k)
+    for f, i in bk:   # the round's broadcast (the last call)
+        for o, m in layout.segs32:
+            assert torch.equal(f[o:o + m].view(torch.int32), o32[o:o + m].view(torch.int32)), o
+
+
 def test_round_one_plan_two_streams(lib):
     """A plan is read-only in a round: rounds on one plan issued on two
     streams without any host synchronisation are each exact (eight client

@@ -5,7 +5,9 @@ several rounds, output bits compared between the builds.  Used to tell a
 code change from box-to-box variance.  Only the C ABI both builds share
 is called (fa_plan_create, fa_reduce, fa_synth_fill_*).
 
-    python tools/ab_lib.py LIB_A LIB_B [ROUNDS]
+    python tools/ab_lib.py LIB_A LIB_B [ROUNDS] [CASES]
+    AB_SLAB=1: each client set carved from one slab (feddct_amd/slab.py), as
+    the product places them
 """
 import ctypes
 import json
@@ -60,9 +62,16 @@ def layout_of(stem):
     return BucketLayout.from_manifest(m), [(m, "")]
 
 
+SLAB = os.environ.get("AB_SLAB", "0") == "1"   # clients carved from one slab (slab.py)
+
+
 def fill(lib, lay, parts, c, dev):
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    f32 = torch.zeros(max(lay.f32_numel, 64), dtype=torch.float32, device=dev)
+    if SLAB:
+        from feddct_amd import slab
+        f32 = slab.carve(max(lay.f32_numel, 64), torch.float32, dev)
+    else:
+        f32 = torch.zeros(max(lay.f32_numel, 64), dtype=torch.float32, device=dev)
     i64 = torch.zeros(max(lay.i64_numel, 1), dtype=torch.int64, device=dev)
     for man, pre in parts:
         for j, e in enumerate(man["keys"]):
@@ -96,7 +105,14 @@ def main():
             else None
         sets = []
         for _ in range(rot):
+            if SLAB:
+                from feddct_amd import slab
+                slab.release()
+                ctx = slab.expecting(n + 1)
+                ctx.__enter__()
             cl = [fill(libs[0], lay, parts, c, dev) for c in range(n)]
+            if SLAB:
+                ctx.__exit__(None, None, None)
             sets.append((cl, torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])))
         plans = []
         for lib in libs:
