@@ -1798,7 +1798,8 @@ struct Launch {
   int slots;  // resident workgroups of its kernel (0: unknown / tuning grid)
   int batch;  // clients per load batch of its kernel
 };
-// The clients two deep (reduce_impl.h pipe2_clients) where it measured
+// The next client's loads before the current client's adds
+// (reduce_impl.h pipe2_clients) where it measured
 // faster: unweighted calls of 17..63 clients (inline pointers) on the plain
 // 2048-float table — not the 1024-float table, not a table re-cut for the
 // round count (profiles/r05_exp_pipe2_*.jsonl)

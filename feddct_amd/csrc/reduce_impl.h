@@ -93,7 +93,7 @@ struct ReduceArgs {
   int64_t plane;
   const float* tfac;  // torch-GPU order: per-tile mean factor fl(M)/fl(N*M)
   const int64_t* sidx;  // packed scalar tiles' entries (K_SCALAR_PACKED)
-  int pipe;  // 1: the clients two deep (pipe2_clients; the launch rule in fedagg.hip)
+  int pipe;  // 1: pipe2_clients (the next client's loads before the adds; fedagg.hip pipe_rule)
   const float* const* tab32;
   const int64_t* const* tab64;
   const float* tabw;
@@ -353,23 +353,27 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
   }
 }
 
-// The clients two deep (r05): client b+1's loads are issued before client
-// b's adds, one client after another in slot order (the same order as the
-// batches: the bits are the batches' bits).  The batch form's compiled
-// rhythm waits for each client's loads before issuing the next client's, and
-// re-reads the batch's pointers every B clients; this one keeps two clients'
-// loads in flight per lane throughout.  Measured (tools/exp_pipe2_n.py,
-// profiles/r05_exp_pipe2_n.jsonl, same process): 1.1-1.6 % faster for
-// unweighted calls of 20-48 clients on the plain 2048-float table (cfg2
-// 134.2 vs 135.6 us), equal at 16, 7.5 % SLOWER on the 1024-float table
-// (unweighted N >= 64), slower on tables re-cut for the round count
-// (profiles/r05_exp_pipe2_balance.jsonl: cfg4's C100 layout 143.6 vs
-// 137.6 us), no better weighted — so the launch
-// takes it only for unweighted calls of 17..63 clients on the plain
-// 2048-float table (fedagg.hip, pipe_rule).
+// The clients one after another with the next client's loads issued
+// before the current client's adds (r05; the same order as the batches, so
+// the batches' bits).  As compiled (ISA read), each iteration issues client
+// b+1's loads, then waits for every outstanding load (vmcnt(0)), then adds
+// client b: still one client's data in flight per wave, as in the batch
+// form, but the adds, the promotion and the next pointer's scalar load no
+// longer sit between one client's data arriving and the next client's loads
+// leaving.  Measured (profiles/r05_exp_pipe2_*.jsonl, same process): 1.1-1.6 %
+// faster for unweighted calls of 20-48 clients on the plain 2048-float
+// table (cfg2 134.2 vs 135.6 us), equal at 16, 7.5 % SLOWER on the
+// 1024-float table (unweighted N >= 64), slower on tables re-cut for the
+// round count (cfg4's C100 layout 143.6 vs 137.6 us), no better weighted —
+// so the launch takes it only for unweighted calls of 17..63 clients on the
+// plain 2048-float table (fedagg.hip, pipe_rule).  A truly two-deep form
+// (two register sets, the waits for the older client only, vmcnt(U)) is 4 %
+// SLOWER on cfg2 (profiles/r05_ab_lib_pipe2_true_two_deep.jsonl): with two
+// clients per wave in flight the chip reads from twice as many places at
+// once, as the issue-all batch form did (r04).
 // The loads are unpredicated: a lane past the tile's end reads the tile's
 // last vector instead (inside the bucket; its sums are never stored), so the
-// loop's control flow stays uniform and the loads stay in flight
+// loop's control flow stays uniform.
 template <int U, bool DEEP, int POL>
 __device__ __forceinline__ void pipe2_clients(KArgs& a, Acc<U, DEEP>& A, int n, int64_t start,
                                               const uint32_t (&vl)[U], int lp, int mask) {
