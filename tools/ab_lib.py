@@ -26,7 +26,10 @@ _P, _I, _I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
 CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
          ("cfg3", "wrnsl16_8_sf4_c10", 5, 2), ("resnet110sl", "resnet110sl_sf4_c100", 25, 4),
          # torch-ROCm's GPU order (fa_plan_create_order, FA_ORDER_TORCH_GPU)
-         ("cfg2_tgpu", "wrn16_8_c10", 20, 1), ("cfg3_tgpu", "wrnsl16_8_sf4_c10", 5, 2)]
+         ("cfg2_tgpu", "wrn16_8_c10", 20, 1), ("cfg3_tgpu", "wrnsl16_8_sf4_c10", 5, 2),
+         # r05: the client-loop rule's range (17..63 unweighted, plain table)
+         ("c10_n17", "wrn16_8_c10", 17, 1), ("c10_n32", "wrn16_8_c10", 32, 1),
+         ("c10_n48", "wrn16_8_c10", 48, 1)]
 
 
 def load(path):
