@@ -7,7 +7,7 @@ is called (fa_plan_create, fa_reduce, fa_synth_fill_*).
 
     python tools/ab_lib.py LIB_A LIB_B [ROUNDS] [CASES]
     AB_SLAB=1: each client set carved from one slab (feddct_amd/slab.py), as
-    the product places them
+    the product places them; AB_FLAGS=1: whole rounds (FA_F_BCAST)
 """
 import ctypes
 import json
@@ -66,6 +66,7 @@ def layout_of(stem):
 
 
 SLAB = os.environ.get("AB_SLAB", "0") == "1"   # clients carved from one slab (slab.py)
+FLAGS = int(os.environ.get("AB_FLAGS", "0"))   # fa_reduce flags (1: FA_F_BCAST, the round)
 
 
 def fill(lib, lay, parts, c, dev):
@@ -136,7 +137,7 @@ def main():
         def call(k, i):
             p32, p64, o32, o64 = ptrs[i % rot]
             ok(libs[k], libs[k].fa_reduce(plans[k], p32, p64, n, wts, o32.data_ptr(),
-                                          o64.data_ptr(), 0, st), "reduce")
+                                          o64.data_ptr(), FLAGS, st), "reduce")
         times = [[], []]
         outs = [None, None]
         reps = 60 * rot if n > 10 else 200 * rot
