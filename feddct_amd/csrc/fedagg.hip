@@ -1041,7 +1041,7 @@ hipError_t launch_chain(const ReduceArgs& a, int ntiles, int vec_u, hipStream_t 
 
 
 hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pflags,
-                         hipStream_t st, int batch = 0) {
+                         hipStream_t st, int batch = 0, int pipe = 0) {
   // DEEP (n >= 256): cascade levels 2-3 and the constant-space table loads.
   // Weighted reductions take the mean's 16-client batches too since the
   // batch's weights are read once up front (r02 sweep, same box: weighted
@@ -1050,11 +1050,11 @@ hipError_t launch_reduce(const ReduceArgs& a, int ntiles, int vec_u, unsigned pf
   const bool w = a.flags & 0x100u;  // internal: weighted
   const int b = batch > 0 ? batch : pick_batch(a.n, vec_u, pflags);
   switch (vec_u) {
-    case 1: return b == 16 ? launch_u<1, 16>(a, ntiles, deep, w, st)
-                           : launch_u<1, 8>(a, ntiles, deep, w, st);
-    case 4: return launch_u<4, 8>(a, ntiles, deep, w, st);
-    default: return b == 16 ? launch_u<2, 16>(a, ntiles, deep, w, st)
-                            : launch_u<2, 8>(a, ntiles, deep, w, st);
+    case 1: return b == 16 ? launch_u<1, 16>(a, ntiles, deep, w, 0, st)
+                           : launch_u<1, 8>(a, ntiles, deep, w, 0, st);
+    case 4: return launch_u<4, 8>(a, ntiles, deep, w, 0, st);
+    default: return b == 16 ? launch_u<2, 16>(a, ntiles, deep, w, pipe, st)
+                            : launch_u<2, 8>(a, ntiles, deep, w, pipe, st);
   }
 }
 
@@ -1799,13 +1799,18 @@ struct Launch {
   int batch;  // clients per load batch of its kernel
 };
 // The next client's loads before the current client's adds
-// (reduce_impl.h pipe2_clients) where it measured
-// faster: unweighted calls of 17..63 clients (inline pointers) on the plain
-// 2048-float table — not the 1024-float table, not a table re-cut for the
-// round count (profiles/r05_exp_pipe2_*.jsonl)
-bool pipe_rule(const fa_plan* plan, const Launch& L, int n, bool weighted) {
-  return !weighted && n >= 17 && n <= 63 && n <= kInline && L.vec_u == 2 &&
-         L.tiles == plan->d_tiles;
+// (reduce_impl.h pipe2_clients) where it measured faster
+// (profiles/r05_exp_pipe2_*.jsonl, r05_ab_lib_pipe2_*.jsonl): unweighted
+// calls of 2..7 or 17..63 clients (inline pointers) on the full 2048-float
+// tiles of launches of three or more rounds of resident workgroups (partial
+// tiles — tensor ends, the halved tail of a table re-cut for the round count
+// — keep the batch form).  Not the 1024-float table, not weighted calls, not
+// 8..16 clients, not the short launches (resnet110sl N = 25 at two rounds:
+// +0.9 %; sf32 N = 3 at 2.5: +0.8 %).
+int pipe_rule(const fa_plan* plan, const Launch& L, int n, bool weighted) {
+  (void)plan;
+  if (weighted || n > kInline || L.vec_u != 2 || L.slots <= 0 || L.nt < 3 * L.slots) return 0;
+  return (n >= 2 && n <= 7) || (n >= 17 && n <= 63) ? 1 : 0;
 }
 
 Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) {
@@ -2022,11 +2027,11 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
   a.sidx = L.sidx;
   const int ntiles = L.nt, vec_u = L.vec_u;
   a.ntiles = ntiles;
-  a.pipe = pipe_rule(plan, L, n, weights != nullptr) ? 1 : 0;
   // the broadcast is its own launch after the reduce
   const bool bcast = (flags & FA_F_BCAST) != 0;
   a.flags &= ~FA_F_BCAST;
-  hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st, L.batch);
+  hipError_t e = launch_reduce(a, ntiles, vec_u, plan->flags, st, L.batch,
+                               pipe_rule(plan, L, n, weights != nullptr));
   if (e == hipSuccess && bcast) e = launch_bcast(plan, a, n, ntiles, st);
   if (table) {
     hipError_t e2 = hipFreeAsync(table, st);

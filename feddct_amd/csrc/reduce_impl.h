@@ -93,7 +93,6 @@ struct ReduceArgs {
   int64_t plane;
   const float* tfac;  // torch-GPU order: per-tile mean factor fl(M)/fl(N*M)
   const int64_t* sidx;  // packed scalar tiles' entries (K_SCALAR_PACKED)
-  int pipe;  // 1: pipe2_clients (the next client's loads before the adds; fedagg.hip pipe_rule)
   const float* const* tab32;
   const int64_t* const* tab64;
   const float* tabw;
@@ -371,9 +370,9 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
 // SLOWER on cfg2 (profiles/r05_ab_lib_pipe2_true_two_deep.jsonl): with two
 // clients per wave in flight the chip reads from twice as many places at
 // once, as the issue-all batch form did (r04).
-// The loads are unpredicated: a lane past the tile's end reads the tile's
-// last vector instead (inside the bucket; its sums are never stored), so the
-// loop's control flow stays uniform.
+// Full tiles only (partial tiles keep the batch form: measured slower here,
+// and a separate instance that also took them compiled into a two-deep loop,
+// 5-8 % slower — profiles/r05_ab_lib_pipe2_instances.jsonl).
 template <int U, bool DEEP, int POL>
 __device__ __forceinline__ void pipe2_clients(KArgs& a, Acc<U, DEEP>& A, int n, int64_t start,
                                               const uint32_t (&vl)[U], int lp, int mask) {
@@ -397,7 +396,9 @@ __device__ __forceinline__ void pipe2_clients(KArgs& a, Acc<U, DEEP>& A, int n, 
   }
 }
 
-template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool CHAIN>
+// PIPE (r05): pipe2_clients for the full tiles (fedagg.hip pipe_rule); its
+// own kernel instances, so the other kernels' code is unchanged
+template <int U, int B, bool FULL, bool DEEP, bool WEIGHTED, int POL, bool CHAIN, int PIPE = 0>
 __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
                                          int count) {
   // TAB: the DEEP kernels' constant-space pointer table; a chain segment may
@@ -438,12 +439,8 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
     }
   }
   int b0 = 0;
-  if (!CHAIN && !TAB && !WEIGHTED && a.pipe && n <= kInline) {
-    uint32_t vl[U];
-    const uint32_t vmax = (uint32_t)(count - 1) / 4;
-#pragma unroll
-    for (int u = 0; u < U; ++u) vl[u] = FULL ? vi[u] : min(vi[u], vmax);
-    pipe2_clients<U, DEEP, POL>(a, A, n, start, vl, lp, mask);
+  if constexpr (PIPE != 0 && FULL && !CHAIN && !TAB && !WEIGHTED) {
+    pipe2_clients<U, DEEP, POL>(a, A, n, start, vi, lp, mask);
     b0 = n;
   }
   for (; b0 + B <= n; b0 += B)
@@ -663,7 +660,7 @@ __device__ __forceinline__ void tile_scalar_packed(KArgs& a, int k) {
   }
 }
 
-template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN>
+template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN, int PIPE = 0>
 __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
   if constexpr (!CHAIN) {
     if (ti < a.nscalar) {  // the packed scalar tiles lead the table
@@ -674,27 +671,27 @@ __device__ __forceinline__ void run_tile(KArgs& a, int ti) {
   const Tile t = a.tiles[ti];
   if (t.kind == K_F32_VEC) {
     if (t.count == 4 * U * kBlock)
-      tile_vec<U, B, true, DEEP, WEIGHTED, POL, CHAIN>(a, t.start, t.count);
+      tile_vec<U, B, true, DEEP, WEIGHTED, POL, CHAIN, PIPE>(a, t.start, t.count);
     else
-      tile_vec<U, B, false, DEEP, WEIGHTED, POL, CHAIN>(a, t.start, t.count);
+      tile_vec<U, B, false, DEEP, WEIGHTED, POL, CHAIN, PIPE>(a, t.start, t.count);
   }
 }
 
 // One workgroup per tile (grid == the table's tile count).  (A persistent
 // grid walking the table, an occupancy cap and an XCD-contiguous tile order
 // were measured slower, r01-r03; tools/reducelab.hip.)
-template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN = false>
+template <int U, int B, bool DEEP, bool WEIGHTED, int POL, bool CHAIN = false, int PIPE = 0>
 __global__ __launch_bounds__(kBlock) void reduce_kernel(ReduceArgs args) {
   (void)args;
   KArgs& a = *(KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  run_tile<U, B, DEEP, WEIGHTED, POL, CHAIN>(a, blockIdx.x);
+  run_tile<U, B, DEEP, WEIGHTED, POL, CHAIN, PIPE>(a, blockIdx.x);
 }
 
 // --------------------------------------------------------------- launches --
-template <int U, int B, bool DEEP, bool W, int POL, bool CHAIN = false>
+template <int U, int B, bool DEEP, bool W, int POL, bool CHAIN = false, int PIPE = 0>
 hipError_t launch_one(const ReduceArgs& a, int ntiles, hipStream_t st) {
-  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, POL, CHAIN>), dim3(ntiles), dim3(kBlock), 0,
-                     st, a);
+  hipLaunchKernelGGL((reduce_kernel<U, B, DEEP, W, POL, CHAIN, PIPE>), dim3(ntiles), dim3(kBlock),
+                     0, st, a);
   return hipGetLastError();
 }
 
@@ -707,9 +704,16 @@ hipError_t launch_chain_ub(const ReduceArgs& a, int ntiles, bool deep, bool w, h
   return w ? launch_one<U, B, false, true, 3, true>(a, ntiles, st)
            : launch_one<U, B, false, false, 3, true>(a, ntiles, st);
 }
-// The reduce: nt loads, sc1 result stores (POL 5, st_out).
+// The reduce: nt loads, sc1 result stores (POL 5, st_out).  pipe (fedagg.hip
+// pipe_rule; unweighted, not deep, U = 2 only): the PIPE instances.
 template <int U, int B>
-hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, hipStream_t st) {
+hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, int pipe,
+                    hipStream_t st) {
+  if constexpr (U == 2) {
+    if (pipe && !deep && !w) return launch_one<U, B, false, false, 5, false, 1>(a, ntiles, st);
+  } else {
+    (void)pipe;
+  }
   if (deep) return w ? launch_one<U, B, true, true, 5>(a, ntiles, st)
                      : launch_one<U, B, true, false, 5>(a, ntiles, st);
   return w ? launch_one<U, B, false, true, 5>(a, ntiles, st)
@@ -741,7 +745,7 @@ int occupancy_u(bool deep, bool w) {
 
 // The (U, B) launcher instantiations, each in one fedagg_k*.hip unit.
 #define FA_K_LAUNCH_U(EXT, U, B)                                                      \
-  EXT template hipError_t fa_k::launch_u<U, B>(const fa_k::ReduceArgs&, int, bool, bool,      \
+  EXT template hipError_t fa_k::launch_u<U, B>(const fa_k::ReduceArgs&, int, bool, bool, int, \
                                                 hipStream_t);                                 \
   EXT template int fa_k::occupancy_u<U, B>(bool, bool);
 #define FA_K_LAUNCH_CHAIN(EXT, U, B)                                                          \

@@ -318,13 +318,14 @@ def test_round_small_n_every_tile_width(lib, n, weighted, tile):
         assert torch.equal(i[:layout.i64_numel], o64[:layout.i64_numel])
 
 
-@pytest.mark.parametrize("n", [16, 17, 20, 31, 33, 48, 63, 64])
+@pytest.mark.parametrize("n", [2, 5, 7, 8, 16, 17, 20, 31, 33, 48, 63, 64])
 def test_two_deep_clients_on_the_plain_table(lib, n):
-    """r05: unweighted calls of 17..63 clients on the plain 2048-float table
-    keep two clients' loads in flight (reduce_impl.h pipe2_clients;
-    fedagg.hip pipe_rule) — a ragged layout (tiles past tensor ends, packed
-    scalar columns, int64 keys) with the plain table forced, against the
-    oracle bit for bit, mean and round (16 and 64 take the batch form)."""
+    """r05: unweighted calls of 2..7 / 17..63 clients run their full
+    2048-float tiles through the client loop (reduce_impl.h pipe2_clients,
+    the PIPE kernel instances; fedagg.hip pipe_rule) and their partial tiles
+    through the batch form — a ragged layout (tiles past tensor ends, packed
+    scalar columns, int64 keys), plain table forced, against the oracle bit
+    for bit, mean and round (16 and 64 take the batch form throughout)."""
     man = _rand_manifest(None, [100, 4096, 7, 3000, 1, 64, 20000, 3, 9000, 2050])
     layout = BucketLayout.from_manifest(man)
     states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]

@@ -17,7 +17,9 @@ LIBS = [os.path.join(ROOT, "feddct_amd", "libfedagg.so"),
         os.path.join(ROOT, "feddct_amd", "libfedagg_comm.so")]
 # the default reduce: U = 2 (2048-float tiles), 16-client batches, not deep,
 # unweighted, POL 5 (nt loads, sc1 result stores), not a chain segment
-HOT = "_ZN4fa_k13reduce_kernelILi2ELi16ELb0ELb0ELi5ELb0EEEvNS_10ReduceArgsE"
+HOT = "_ZN4fa_k13reduce_kernelILi2ELi16ELb0ELb0ELi5ELb0ELi0EEEvNS_10ReduceArgsE"
+# the headline call's kernel since r05 (pipe_rule: cfg2's 20 clients, plain table)
+HOT_PIPE = "_ZN4fa_k13reduce_kernelILi2ELi16ELb0ELb0ELi5ELb0ELi1EEEvNS_10ReduceArgsE"
 
 
 def _have_tools():
@@ -89,23 +91,28 @@ def test_every_reduce_variant_is_compiled_once(tmp_path):
         for name in _kernels(co):
             assert name not in seen, (name, seen.get(name), k)
             seen[name] = k
-    assert HOT in seen
+    assert HOT in seen and HOT_PIPE in seen
 
 
 @pytest.mark.skipif(not _have_tools(), reason="ROCm llvm tools / objcopy not available")
-def test_hot_kernel_uses_global_nt_loads(tmp_path):
+@pytest.mark.parametrize("hot,min_nt", [(HOT, 32), (HOT_PIPE, 32)])
+def test_hot_kernel_uses_global_nt_loads(tmp_path, hot, min_nt):
+    """The batch form's 16 clients x 2 vectors unrolled (>= 32 loads; the
+    client-loop kernel keeps it for partial tiles): every 16-B load nt
+    global."""
     body = None
     for co in _code_objects(LIBS[0], tmp_path):
         dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", co], check=True,
                              capture_output=True, text=True).stdout
-        m = re.search(re.escape(HOT) + r">:\n(.*?)(?:\n\n|\Z)", dis, flags=re.S)
+        m = re.search(re.escape(hot) + r">:\n(.*?)(?:\n\n|\Z)", dis, flags=re.S)
         if m:
             body = m.group(1)
     assert body, "default reduce kernel not found"
     loads = re.findall(r"\b(global|flat|buffer)_load_dwordx4\b[^\n]*", body)
     assert loads and not re.search(r"\bflat_load_dwordx4\b", body), "hot loads are flat"
     nt = re.findall(r"global_load_dwordx4[^\n]*\bnt\b", body)
-    assert len(nt) >= 32, "hot loads should be non-temporal global_load_dwordx4"
+    assert len(nt) >= min_nt, "hot loads should be non-temporal global_load_dwordx4"
+    assert len(nt) == len(re.findall(r"global_load_dwordx4", body)), "a hot load without nt"
     assert "scratch_" not in body
 
 
@@ -190,16 +197,20 @@ def test_contraction_checker_sees_a_contraction():
 def test_reduce_family_is_the_shipped_set(tmp_path):
     """r05: the reduce kernel family holds only the
     shipped variants — U x B in {1x8, 1x16, 2x8, 2x16, 4x8}, deep x weighted,
-    POL 5 for the reduce and POL 3 for chain segments: 36 instances."""
+    POL 5 for the reduce and POL 3 for chain segments: 36 instances; plus the
+    client-loop instances (PIPE 1: U = 2, B = 8 / 16, unweighted, not deep,
+    POL 5): 38."""
     names = set()
     for co in _code_objects(LIBS[0], tmp_path):
         names |= {k for k in _kernels(co) if "reduce_kernel" in k}
-    pat = re.compile(r"reduce_kernelILi(\d)ELi(\d+)ELb([01])ELb([01])ELi(\d+)ELb([01])E")
+    pat = re.compile(r"reduce_kernelILi(\d)ELi(\d+)ELb([01])ELb([01])ELi(\d+)ELb([01])ELi(\d)E")
     got = set()
     for k in names:
         m = pat.search(k)
         assert m, k
         got.add(tuple(int(x) for x in m.groups()))
-    want = {(u, b, d, w, 3 if c else 5, c) for u, b in ((1, 8), (1, 16), (2, 8), (2, 16), (4, 8))
+    want = {(u, b, d, w, 3 if c else 5, c, 0)
+            for u, b in ((1, 8), (1, 16), (2, 8), (2, 16), (4, 8))
             for d in (0, 1) for w in (0, 1) for c in (0, 1) if not (c and (u, b) == (1, 16))}
+    want |= {(2, b, 0, 0, 5, 0, 1) for b in (8, 16)}
     assert got == want, (sorted(got - want), sorted(want - got))
