@@ -1800,16 +1800,17 @@ struct Launch {
 };
 // The next client's loads before the current client's adds
 // (reduce_impl.h pipe2_clients) where it measured faster
-// (profiles/r05_exp_pipe2_*.jsonl, r05_ab_lib_pipe2_*.jsonl): unweighted
-// calls of 2..7 or 17..63 clients (inline pointers) on the full 2048-float
-// tiles of launches of three or more rounds of resident workgroups (partial
-// tiles — tensor ends, the halved tail of a table re-cut for the round count
-// — keep the batch form).  Not the 1024-float table, not weighted calls, not
+// (profiles/r05_exp_pipe2_*.jsonl, r05_ab_lib_pipe2_*.jsonl): calls of 2..7
+// or 17..63 clients (inline pointers), mean or weighted, on the full
+// 2048-float tiles of launches of three or more rounds of resident
+// workgroups (partial tiles — tensor ends, the halved tail of a table re-cut
+// for the round count — keep the batch form).  Not the 1024-float table, not
 // 8..16 clients, not the short launches (resnet110sl N = 25 at two rounds:
 // +0.9 %; sf32 N = 3 at 2.5: +0.8 %).
 int pipe_rule(const fa_plan* plan, const Launch& L, int n, bool weighted) {
   (void)plan;
-  if (weighted || n > kInline || L.vec_u != 2 || L.slots <= 0 || L.nt < 3 * L.slots) return 0;
+  (void)weighted;
+  if (n > kInline || L.vec_u != 2 || L.slots <= 0 || L.nt < 3 * L.slots) return 0;
   return (n >= 2 && n <= 7) || (n >= 17 && n <= 63) ? 1 : 0;
 }
 

@@ -373,7 +373,7 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
 // Full tiles only (partial tiles keep the batch form: measured slower here,
 // and a separate instance that also took them compiled into a two-deep loop,
 // 5-8 % slower — profiles/r05_ab_lib_pipe2_instances.jsonl).
-template <int U, bool DEEP, int POL>
+template <int U, bool DEEP, bool WEIGHTED, int POL>
 __device__ __forceinline__ void pipe2_clients(KArgs& a, Acc<U, DEEP>& A, int n, int64_t start,
                                               const uint32_t (&vl)[U], int lp, int mask) {
   f4 cur[U], nxt[U];
@@ -388,8 +388,14 @@ __device__ __forceinline__ void pipe2_clients(KArgs& a, Acc<U, DEEP>& A, int n, 
 #pragma unroll
       for (int u = 0; u < U; ++u) nxt[u] = ldg4<(POL & 1) != 0>(p, vl[u]);
     }
+    if constexpr (WEIGHTED) {
+      const float wb = a.w[b];
 #pragma unroll
-    for (int u = 0; u < U; ++u) A.l0[u] = add4(A.l0[u], cur[u]);
+      for (int u = 0; u < U; ++u) A.l0[u] = add4(A.l0[u], mul4s(cur[u], wb));
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) A.l0[u] = add4(A.l0[u], cur[u]);
+    }
     promote<U, DEEP>(A, b + 1, lp, mask);
 #pragma unroll
     for (int u = 0; u < U; ++u) cur[u] = nxt[u];
@@ -439,8 +445,8 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
     }
   }
   int b0 = 0;
-  if constexpr (PIPE != 0 && FULL && !CHAIN && !TAB && !WEIGHTED) {
-    pipe2_clients<U, DEEP, POL>(a, A, n, start, vi, lp, mask);
+  if constexpr (PIPE != 0 && FULL && !CHAIN && !TAB) {
+    pipe2_clients<U, DEEP, WEIGHTED, POL>(a, A, n, start, vi, lp, mask);
     b0 = n;
   }
   for (; b0 + B <= n; b0 += B)
@@ -710,7 +716,9 @@ template <int U, int B>
 hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, int pipe,
                     hipStream_t st) {
   if constexpr (U == 2) {
-    if (pipe && !deep && !w) return launch_one<U, B, false, false, 5, false, 1>(a, ntiles, st);
+    if (pipe && !deep)
+      return w ? launch_one<U, B, false, true, 5, false, 1>(a, ntiles, st)
+               : launch_one<U, B, false, false, 5, false, 1>(a, ntiles, st);
   } else {
     (void)pipe;
   }

@@ -318,8 +318,9 @@ def test_round_small_n_every_tile_width(lib, n, weighted, tile):
         assert torch.equal(i[:layout.i64_numel], o64[:layout.i64_numel])
 
 
+@pytest.mark.parametrize("weighted", [False, True])
 @pytest.mark.parametrize("n", [2, 5, 7, 8, 16, 17, 20, 31, 33, 48, 63, 64])
-def test_two_deep_clients_on_the_plain_table(lib, n):
+def test_two_deep_clients_on_the_plain_table(lib, n, weighted):
     """r05: unweighted calls of 2..7 / 17..63 clients run their full
     2048-float tiles through the client loop (reduce_impl.h pipe2_clients,
     the PIPE kernel instances; fedagg.hip pipe_rule) and their partial tiles
@@ -332,17 +333,25 @@ def test_two_deep_clients_on_the_plain_table(lib, n):
     bk = states_to_buckets(layout, states, DEV)
     plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
                     flags=lib.FA_PLAN_GAPS_ARE_PADDING | lib.FA_PLAN_TUNE_NO_BALANCE)
-    want = O.aggregate_state(states)
+    w = O.weights_from_sizes(np.arange(1, n + 1) * 7 + 3) if weighted else None
+    if w is None:
+        want = O.aggregate_state(states)
+    else:
+        want = []
+        for j, (k, v0) in enumerate(states[0]):
+            x = np.stack([np.asarray(st[j][1]) for st in states])
+            want.append((k, O.mean_i64_trunc(x) if x.dtype == np.int64 else O.weighted_sum0(x, w)))
+    wa = None if w is None else (ctypes.c_float * n)(*[float(x) for x in w])
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for fl in (0, lib.FA_F_BCAST):
         o32 = torch.full_like(bk[0][0], np.nan)
         o64 = torch.full_like(bk[0][1], -7)
         lib.check(lib.lib.fa_reduce(plan.handle, lib.ptr_array([b[0].data_ptr() for b in bk]),
-                                    lib.ptr_array([b[1].data_ptr() for b in bk]), n, None,
+                                    lib.ptr_array([b[1].data_ptr() for b in bk]), n, wa,
                                     o32.data_ptr(), o64.data_ptr(), fl, s))
         torch.cuda.synchronize()
         for (k, v), (_, g) in zip(want, buckets_to_state(layout, o32, o64)):
-            assert bits_equal(g, v), (n, fl, k)
+            assert bits_equal(g, v), (n, weighted, fl, k)
     for f, i in bk:   # the round's broadcast (the last call)
         for o, m in layout.segs32:
             assert torch.equal(f[o:o + m].view(torch.int32), o32[o:o + m].view(torch.int32)), o

@@ -29,7 +29,12 @@ CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
          ("cfg2_tgpu", "wrn16_8_c10", 20, 1), ("cfg3_tgpu", "wrnsl16_8_sf4_c10", 5, 2),
          # r05: the client-loop rule's range (17..63 unweighted, plain table)
          ("c10_n17", "wrn16_8_c10", 17, 1), ("c10_n32", "wrn16_8_c10", 32, 1),
-         ("c10_n48", "wrn16_8_c10", 48, 1)]
+         ("c10_n48", "wrn16_8_c10", 48, 1), ("c100_n20", "wrn16_8_c100", 20, 1),
+         ("cfg5", "wrnsl16_8_sf4_c100", 24, 1), ("c10_n2", "wrn16_8_c10", 2, 1),
+         ("c10_n8", "wrn16_8_c10", 8, 1), ("c10_n12", "wrn16_8_c10", 12, 1),
+         ("sf32", "wrnsl16_8_sf32_c100", 3, 6), ("sf16", "wrnsl16_8_sf16_c100", 6, 4),
+         ("cfg2w", "wrn16_8_c10", 20, 1), ("cfg5w", "wrnsl16_8_sf4_c100", 24, 1),
+         ("cfg3w", "wrnsl16_8_sf4_c10", 5, 2)]
 
 
 def load(path):
