@@ -35,7 +35,9 @@ CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
          ("sf32", "wrnsl16_8_sf32_c100", 3, 6), ("sf16", "wrnsl16_8_sf16_c100", 6, 4),
          ("cfg2w", "wrn16_8_c10", 20, 1), ("cfg5w", "wrnsl16_8_sf4_c100", 24, 1),
          ("cfg3w", "wrnsl16_8_sf4_c10", 5, 2), ("c10_n10", "wrn16_8_c10", 10, 1),
-         ("c10_n16", "wrn16_8_c10", 16, 1), ("c10_n12w", "wrn16_8_c10", 12, 1)]
+         ("c10_n16", "wrn16_8_c10", 16, 1), ("c10_n12w", "wrn16_8_c10", 12, 1),
+         ("c10_n64", "wrn16_8_c10", 64, 1), ("c10_n100", "wrn16_8_c10", 100, 1),
+         ("c10_n80w", "wrn16_8_c10", 80, 1), ("c10_n128w", "wrn16_8_c10", 128, 1)]
 
 
 def load(path):
