@@ -359,20 +359,16 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
 // client b: still one client's data in flight per wave, as in the batch
 // form, but the adds, the promotion and the next pointer's scalar load no
 // longer sit between one client's data arriving and the next client's loads
-// leaving.  Measured (profiles/r05_exp_pipe2_*.jsonl, same process): 1.1-1.6 %
-// faster for unweighted calls of 20-48 clients on the plain 2048-float
-// table (cfg2 134.2 vs 135.6 us), equal at 16, 7.5 % SLOWER on the
-// 1024-float table (unweighted N >= 64), slower on tables re-cut for the
-// round count (cfg4's C100 layout 143.6 vs 137.6 us), no better weighted —
-// so the launch takes it only for unweighted calls of 17..63 clients on the
-// plain 2048-float table (fedagg.hip, pipe_rule).  A truly two-deep form
-// (two register sets, the waits for the older client only, vmcnt(U)) is 4 %
-// SLOWER on cfg2 (profiles/r05_ab_lib_pipe2_true_two_deep.jsonl): with two
-// clients per wave in flight the chip reads from twice as many places at
-// once, as the issue-all batch form did (r04).
-// Full tiles only (partial tiles keep the batch form: measured slower here,
-// and a separate instance that also took them compiled into a two-deep loop,
-// 5-8 % slower — profiles/r05_ab_lib_pipe2_instances.jsonl).
+// leaving.  Its own kernel instances (PIPE), full tiles only; the launch
+// rule (fedagg.hip pipe_rule) and the measurements behind it are in DESIGN
+// §4.1: 1.0-1.7 % faster for 2..7 and 17..63 clients, mean or weighted, in
+// launches of three or more rounds (cfg2, cfg3, cfg4, cfg5), slower for
+// 8..12 and 64..128 clients and on short launches.  Partial tiles keep the
+// batch form: an instance that took them too compiled into a truly two-deep
+// loop (waits for the older client only, vmcnt(U)) and ran 5-8 % SLOWER, as
+// did a hand-written two-register-set form (4 %): two clients per wave in
+// flight spread the chip's reads over twice as many places, as the issue-all
+// batch form did in r04 (profiles/r05_ab_lib_pipe2_*.jsonl).
 template <int U, bool DEEP, bool WEIGHTED, int POL>
 __device__ __forceinline__ void pipe2_clients(KArgs& a, Acc<U, DEEP>& A, int n, int64_t start,
                                               const uint32_t (&vl)[U], int lp, int mask) {
@@ -711,7 +707,7 @@ hipError_t launch_chain_ub(const ReduceArgs& a, int ntiles, bool deep, bool w, h
            : launch_one<U, B, false, false, 3, true>(a, ntiles, st);
 }
 // The reduce: nt loads, sc1 result stores (POL 5, st_out).  pipe (fedagg.hip
-// pipe_rule; unweighted, not deep, U = 2 only): the PIPE instances.
+// pipe_rule; not deep, U = 2 only): the PIPE instances.
 template <int U, int B>
 hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, int pipe,
                     hipStream_t st) {
