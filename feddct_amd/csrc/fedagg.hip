@@ -323,7 +323,7 @@ __device__ __forceinline__ f4 tgpu_outer4(KArgs& a, int64_t start, uint32_t v, i
 // b & 3 statically), loads through the same pointer accessor as the default
 // reduce.  Row p goes into accumulator p % 4 in increasing row order, then
 // ((a0 + a1) + a2) + a3 — torch's thread order, per component.
-template <int U, int B, bool FULL>
+template <int U, int B, bool FULL, int PIPE = 0>
 __device__ __forceinline__ void tgpu_wide(KArgs& a, int64_t start, int count, float fac,
                                           bool sum_only) {
   static_assert(B % 4 == 0, "batch must keep the accumulator index static");
@@ -340,6 +340,38 @@ __device__ __forceinline__ void tgpu_wide(KArgs& a, int64_t start, int count, fl
   }
   const int n = a.n;
   int b0 = 0;
+  if constexpr (PIPE != 0 && FULL) {
+    // the client loop (as reduce_impl.h pipe2_clients): row b + 1's loads
+    // before row b's adds; four rows per pass keep row b's accumulator
+    // index (b & 3) static.  The rows' order per accumulator is unchanged.
+    // Same process, r05: cfg2 order 139.9 -> 136.7 us, cfg5 169.9 -> 166.6,
+    // N = 17 / 28 -2.8 / -2.5 %, cfg3 and N = 2..16 -1.3 .. +0.1 %, unlike
+    // the default kernel's rule: both batch sizes take it
+    f4 cur[U], nxt[U];
+    {
+      const float* p = cptr32(a, 0) + start;
+#pragma unroll
+      for (int u = 0; u < U; ++u) cur[u] = ldg4<true>(p, vi[u]);
+    }
+    for (; b0 < n; b0 += 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int b = b0 + k;
+        if (b < n) {
+          if (b + 1 < n) {
+            const float* p = cptr32(a, b + 1) + start;
+#pragma unroll
+            for (int u = 0; u < U; ++u) nxt[u] = ldg4<true>(p, vi[u]);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            acc[k][u] += cur[u];
+            cur[u] = nxt[u];
+          }
+        }
+      }
+    }
+  }
   for (; b0 + B <= n; b0 += B) {
     f4 x[B][U];
 #pragma unroll
@@ -444,7 +476,7 @@ __device__ __forceinline__ float tgpu_inner_vec(const Src& src, int64_t e, int n
 // budget of the parts' values to that S (a runtime switch over S = 1..16 in
 // one kernel needed 300 VGPRs and spilled).  Inner tiles (M == 1) ride in
 // the LS = 0 group; their own field is the lane count exponent.
-template <int LS, int WB = 16>
+template <int LS, int WB = 16, int PIPE = 0>
 __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   (void)args;
   constexpr int S = 1 << LS;
@@ -456,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   const int n = a.n;
   if constexpr (LS == 0) {
     if (base == K_F32_TGPU_W) {
-      if (t.count == 8 * kBlock) tgpu_wide<2, WB, true>(a, t.start, t.count, fac, sum_only);
+      if (t.count == 8 * kBlock) tgpu_wide<2, WB, true, PIPE>(a, t.start, t.count, fac, sum_only);
       else tgpu_wide<2, WB, false>(a, t.start, t.count, fac, sum_only);
       return;
     }
@@ -1400,8 +1432,8 @@ int tgpu_slots(int dev, int batch) {
   if (it != cache.end()) return it->second;
   int occ = 0, cus = 0;
   const hipError_t e =
-      batch == 8 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tgpu_kernel<0, 8>, kBlock, 0)
-                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tgpu_kernel<0>, kBlock, 0);
+      batch == 8 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tgpu_kernel<0, 8, 1>, kBlock, 0)
+                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tgpu_kernel<0, 16, 1>, kBlock, 0);
   if (e != hipSuccess) occ = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 0;
@@ -1998,10 +2030,12 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
       a.ntiles = cnt;
       switch (g) {
         case 0:
+          // the client loop on full tiles at every N (r05,
+          // profiles/r05_ab_lib_tgpu_client_loop.jsonl)
           if (plan->tgpu_batch == 8)
-            hipLaunchKernelGGL((tgpu_kernel<0, 8>), dim3(cnt), dim3(kBlock), 0, st, a);
+            hipLaunchKernelGGL((tgpu_kernel<0, 8, 1>), dim3(cnt), dim3(kBlock), 0, st, a);
           else
-            hipLaunchKernelGGL(tgpu_kernel<0>, dim3(cnt), dim3(kBlock), 0, st, a);
+            hipLaunchKernelGGL((tgpu_kernel<0, 16, 1>), dim3(cnt), dim3(kBlock), 0, st, a);
           break;
         case 1: hipLaunchKernelGGL(tgpu_kernel<1>, dim3(cnt), dim3(kBlock), 0, st, a); break;
         case 2: hipLaunchKernelGGL(tgpu_kernel<2>, dim3(cnt), dim3(kBlock), 0, st, a); break;

@@ -37,7 +37,14 @@ CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
          ("cfg3w", "wrnsl16_8_sf4_c10", 5, 2), ("c10_n10", "wrn16_8_c10", 10, 1),
          ("c10_n16", "wrn16_8_c10", 16, 1), ("c10_n12w", "wrn16_8_c10", 12, 1),
          ("c10_n64", "wrn16_8_c10", 64, 1), ("c10_n100", "wrn16_8_c10", 100, 1),
-         ("c10_n80w", "wrn16_8_c10", 80, 1), ("c10_n128w", "wrn16_8_c10", 128, 1)]
+         ("c10_n80w", "wrn16_8_c10", 80, 1), ("c10_n128w", "wrn16_8_c10", 128, 1),
+         # r05: the client loop in the torch-GPU-order kernel
+         ("c10_n2_tgpu", "wrn16_8_c10", 2, 2), ("c10_n10_tgpu", "wrn16_8_c10", 10, 1),
+         ("c10_n32_tgpu", "wrn16_8_c10", 32, 1), ("c10_n64_tgpu", "wrn16_8_c10", 64, 1),
+         ("cfg5_tgpu", "wrnsl16_8_sf4_c100", 24, 1), ("sf32_tgpu", "wrnsl16_8_sf32_c100", 3, 6),
+         ("c10_n5_tgpu", "wrn16_8_c10", 5, 2), ("c10_n12_tgpu", "wrn16_8_c10", 12, 1),
+         ("c10_n16_tgpu", "wrn16_8_c10", 16, 1), ("c10_n17_tgpu", "wrn16_8_c10", 17, 1),
+         ("c10_n28_tgpu", "wrn16_8_c10", 28, 1), ("c100_n20_tgpu", "wrn16_8_c100", 20, 1)]
 
 
 def load(path):
