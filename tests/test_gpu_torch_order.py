@@ -165,6 +165,24 @@ def test_kernel_matches_torch_gpu_mean(lib, case):
     assert _vs_torch(layout, cl, out32, out64) == []
 
 
+# r05: the S = 1 kernel's full 2048-element tiles run the client loop (four
+# rows per pass, row b into accumulator b % 4): every row count mod 4 and
+# both row batches (8 below N = 16, else 16), full tiles beside partial ones
+LOOP_NS = [2, 3, 4, 5, 6, 7, 8, 9, 11, 15, 16, 17, 18, 19, 21, 27, 31]
+
+
+@pytest.mark.parametrize("n", LOOP_NS)
+def test_client_loop_every_row_count(lib, n):
+    man = {"keys": [{"key": f"w{j}", "shape": [m], "dtype": "float32"}
+                    for j, m in enumerate([2048 * 3, 2048 * 5 + 100, 4096, 2047, 64 * 2048])]}
+    assert all(lib.lib.fa_torch_gpu_config(n, e["shape"][0], None) for e in man["keys"])
+    layout = BucketLayout.from_manifest(man)
+    from feddct_amd.workload import make_clients
+    cl = make_clients(layout, man, range(n), DEV, mode=synth.MODE_ADVERSARIAL)
+    out32, out64 = _gpu_order_reduce(lib, layout, cl)
+    assert _vs_torch(layout, cl, out32, out64) == []
+
+
 # (offset, numel) fp32 segments: 4-aligned keys back to back (one wide run
 # across them), a 4-aligned key behind a gap, unaligned heads and ragged
 # tails (each breaks the run), 0-dim keys, and a 2**24 + 12 key whose factor
