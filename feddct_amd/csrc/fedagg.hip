@@ -414,6 +414,66 @@ __device__ __forceinline__ void tgpu_wide(KArgs& a, int64_t start, int count, fl
   }
 }
 
+// S = 1 or 2 (torch's row split for N >= 32 over the large tensors) over
+// 2048-element tiles with the client loop: rows in slot order, row r into
+// part r % S and that part's accumulator (r / S) % 4 — part y's p-th row
+// (y + S p) into accumulator p % 4, as tgpu_outer4<S> — then each part's
+// ((a0 + a1) + a2) + a3 and, for S = 2, part 0 + part 1.  4 S rows per pass
+// keep the accumulator index static.  The S = 2 launch runs its S = 1 tiles
+// through it too (tgpu_kernel<1>).
+template <int U, int S, bool FULL>
+__device__ __forceinline__ void tgpu_wide_loop(KArgs& a, int64_t start, int count, float fac,
+                                               bool sum_only) {
+  static_assert(S == 1 || S == 2, "row split of the wide loop");
+  constexpr int R = 4 * S;
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  f4 acc[R][U];
+  uint32_t vi[U];
+  bool ok[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    vi[u] = threadIdx.x + u * kBlock;
+    ok[u] = FULL || (int)(4 * vi[u]) < count;
+#pragma unroll
+    for (int k = 0; k < R; ++k) acc[k][u] = z;
+  }
+  const int n = a.n;
+  f4 cur[U], nxt[U];
+  {
+    const float* p = cptr32(a, 0) + start;
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
+  }
+  for (int b0 = 0; b0 < n; b0 += R) {
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int b = b0 + k;
+      if (b < n) {
+        if (b + 1 < n) {
+          const float* p = cptr32(a, b + 1) + start;
+#pragma unroll
+          for (int u = 0; u < U; ++u) nxt[u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
+        }
+        const int ai = (k % S) * 4 + ((k / S) & 3);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          acc[ai][u] += cur[u];
+          cur[u] = nxt[u];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!FULL && !ok[u]) continue;
+    f4 r = ((acc[0][u] + acc[1][u]) + acc[2][u]) + acc[3][u];
+    if constexpr (S == 2) r = r + (((acc[4][u] + acc[5][u]) + acc[6][u]) + acc[7][u]);
+    if (!sum_only)
+      r = f4{__fmul_rn(r.x, fac), __fmul_rn(r.y, fac), __fmul_rn(r.z, fac), __fmul_rn(r.w, fac)};
+    st_out<5>(a.out32, start, vi[u], r);
+  }
+}
+
 // lane value of the inner order; the wave then runs the shuffle tree
 template <class Src>
 __device__ __forceinline__ float tgpu_inner(const Src& src, int64_t e, int n, int bw, int lane) {
@@ -471,11 +531,40 @@ __device__ __forceinline__ float tgpu_inner_vec(const Src& src, int64_t e, int n
   return v;
 }
 
+// A V tile (4 elements per lane) and a scalar tile (one element per lane)
+// of row split S.
+template <int S>
+__device__ __forceinline__ void tgpu_v_tile(KArgs& a, const Tile& t, float fac, bool sum_only) {
+  const uint32_t v = threadIdx.x;
+  if ((int)(v * 4) >= t.count) return;
+  f4 r = tgpu_outer4<S>(a, t.start, v, a.n);
+  if (!sum_only)
+    r = f4{__fmul_rn(r.x, fac), __fmul_rn(r.y, fac), __fmul_rn(r.z, fac), __fmul_rn(r.w, fac)};
+  st_out<5>(a.out32, t.start, v, r);
+}
+template <int S>
+__device__ __forceinline__ void tgpu_scalar_tile(KArgs& a, const Tile& t, float fac,
+                                                 bool sum_only) {
+  const int j = threadIdx.x;
+  if (j >= t.count) return;
+  const int64_t e = t.start + j;
+  if ((t.kind & 0xFF) == K_F32_TGPU) {
+    const float s = tgpu_outer<SrcF32, S>(SrcF32{a, false}, e, a.n);
+    a.out32[e] = sum_only ? s : __fmul_rn(s, fac);
+  } else {
+    a.out64[e] = (int64_t)__fmul_rn(tgpu_outer<SrcI64, S>(SrcI64{a}, e, a.n), fac);
+  }
+}
+
 // One instantiation per row split S = 1 << LS (the plan groups its tiles by
 // S and launches each group): a single S per kernel keeps the register
 // budget of the parts' values to that S (a runtime switch over S = 1..16 in
 // one kernel needed 300 VGPRs and spilled).  Inner tiles (M == 1) ride in
-// the LS = 0 group; their own field is the lane count exponent.
+// the LS = 0 group; their own field is the lane count exponent.  r05: when
+// the S = 2 group is the largest (N >= 32 over the large tensors) the S = 1
+// and S = 4 tiles and the inner tiles ride in its launch (their own S from
+// the tile's field; fa_plan_create_order), so the small groups cost no
+// launch of their own.
 template <int LS, int WB = 16, int PIPE = 0>
 __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   (void)args;
@@ -486,6 +575,7 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
   const int base = t.kind & 0xFF, ls = (t.kind >> 8) & 0xFF;
   const bool sum_only = a.flags & FA_F_SUM_ONLY;
   const int n = a.n;
+  const bool inner = base == K_F32_TGPU_IN || base == K_I64_TGPU_IN;
   if constexpr (LS == 0) {
     if (base == K_F32_TGPU_W) {
       if (t.count == 8 * kBlock) tgpu_wide<2, WB, true, PIPE>(a, t.start, t.count, fac, sum_only);
@@ -493,25 +583,30 @@ __global__ __launch_bounds__(kBlock) void tgpu_kernel(ReduceArgs args) {
       return;
     }
   }
+  if constexpr (LS == 1) {
+    if (base == K_F32_TGPU_W) {
+      if (ls == 0) {
+        if (t.count == 8 * kBlock) tgpu_wide_loop<2, 1, true>(a, t.start, t.count, fac, sum_only);
+        else tgpu_wide_loop<2, 1, false>(a, t.start, t.count, fac, sum_only);
+      } else {
+        if (t.count == 8 * kBlock) tgpu_wide_loop<2, 2, true>(a, t.start, t.count, fac, sum_only);
+        else tgpu_wide_loop<2, 2, false>(a, t.start, t.count, fac, sum_only);
+      }
+      return;
+    }
+    if (!inner && ls != 1) {  // a rider: S = 1 or 4
+      if (base == K_F32_TGPU_V) tgpu_v_tile<4>(a, t, fac, sum_only);
+      else if (ls == 0) tgpu_scalar_tile<1>(a, t, fac, sum_only);
+      else tgpu_scalar_tile<4>(a, t, fac, sum_only);
+      return;
+    }
+  }
   if (base == K_F32_TGPU_V) {
-    const uint32_t v = threadIdx.x;
-    if ((int)(v * 4) >= t.count) return;
-    f4 r = tgpu_outer4<S>(a, t.start, v, n);
-    if (!sum_only)
-      r = f4{__fmul_rn(r.x, fac), __fmul_rn(r.y, fac), __fmul_rn(r.z, fac), __fmul_rn(r.w, fac)};
-    st_out<5>(a.out32, t.start, v, r);
+    tgpu_v_tile<S>(a, t, fac, sum_only);
     return;
   }
   if (base == K_F32_TGPU || base == K_I64_TGPU) {
-    const int j = threadIdx.x;
-    if (j >= t.count) return;
-    const int64_t e = t.start + j;
-    if (base == K_F32_TGPU) {
-      const float s = tgpu_outer<SrcF32, S>(SrcF32{a, false}, e, n);
-      a.out32[e] = sum_only ? s : __fmul_rn(s, fac);
-    } else {
-      a.out64[e] = (int64_t)__fmul_rn(tgpu_outer<SrcI64, S>(SrcI64{a}, e, n), fac);
-    }
+    tgpu_scalar_tile<S>(a, t, fac, sum_only);
     return;
   }
   // inner: one element per wave
@@ -730,6 +825,7 @@ struct fa_plan {
   int order = FA_ORDER_TORCH_CPU;
   int order_n = 0;        // FA_ORDER_TORCH_GPU: the client count it was cut for
   int tgpu_batch = 16;    // ... rows per load batch of its S = 1 tiles (8 for N < 16)
+  size_t tgpu_s2_lds = 0;  // ... the S = 2 launch's LDS reservation (tgpu_s2_lds)
   float* d_fac = nullptr; // ... and its per-tile mean factors
   int tg_lo[6] = {0, 0, 0, 0, 0, 0};  // ... tiles grouped by row split S = 1..16
   // cut from a segment list with FA_PLAN_GAPS_ARE_PADDING: every byte of
@@ -1440,6 +1536,34 @@ int tgpu_slots(int dev, int batch) {
   return cache[key] = occ > 0 && cus > 0 ? occ * cus : 0;
 }
 
+// The dynamic LDS the S = 2 launch reserves (and never uses) so that at most
+// kTgpuS2Resident of its workgroups share a CU.  Measured r05
+// (profiles/r05_ab_lib_tgpu_s2.jsonl, same process) on the kernel before its
+// S = 4 riders (100 VGPRs, five per CU): three per CU 3-4 % faster than five,
+// two 10 % slower (a reservation of exactly a third of the CU's LDS admitted
+// only two: the allocation rounds up).  With the riders' paths it holds 130
+// VGPRs, three per CU by itself; the reservation keeps the measured count if
+// that changes.  The default reduce's 8-client kernels capped the same way
+// ran 20-25 % slower (r05_ab_lib_occupancy_cap.jsonl).  0 when the device
+// cannot say.
+constexpr int kTgpuS2Resident = 3;
+size_t tgpu_s2_lds(int dev) {
+  static std::mutex mu;
+  static std::map<int, size_t> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0;
+  if (hipDeviceGetAttribute(&per_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) !=
+      hipSuccess)
+    per_cu = 0;
+  // per_cu / (resident + 1/2): the allocation granularity may round the
+  // request up, and per_cu / resident exactly would then admit one fewer
+  return cache[dev] =
+             per_cu > 0 ? (size_t)(2 * (int64_t)per_cu / (2 * kTgpuS2Resident + 1)) & ~(size_t)1023
+                        : 0;
+}
+
 // Rows per load batch of the S = 1 tiles for a plan cut for n clients: 8
 // below 16 clients (as the default reduce's 8-client kernel; the 8-row form
 // holds 102 VGPRs against 164, five workgroups per CU against three):
@@ -1568,9 +1692,10 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
       const int64_t head = std::min<int64_t>((4 - g.offset % 4) % 4, g.numel);
       const int64_t body = (g.numel - head) / 4 * 4;
       // S = 1: 2048-element tiles, the default reduce's load shape (r02:
-      // 151.9 us on cfg2 with the 1024-element form)
-      const bool wide = S == 1;
-      if (wide && head == 0 && body > 0) {
+      // 151.9 us on cfg2 with the 1024-element form); S = 2 too since r05
+      // (tgpu_wide_loop), per key
+      const bool wide = S <= 2;
+      if (S == 1 && head == 0 && body > 0) {
         const bool extend = run_s >= 0 && run_f == f &&
                             (run_e == g.offset ||
                              ((flags & FA_PLAN_GAPS_ARE_PADDING) && run_e <= g.offset));
@@ -1600,16 +1725,33 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
   flush();
   rc = check_disjoint(t, "torch-GPU order planner");
   if (rc) return rc;
-  // group the tiles by row split (inner tiles with S = 1): one launch each
+  // group the tiles by row split (inner tiles with S = 1): one launch each.
+  // r05: when the S = 2 group holds the most tiles, the S = 1, S = 4 and
+  // inner tiles ride in its launch, first (tgpu_kernel<1>; the small groups'
+  // own launches cost 10-13 us of latency each at N = 32..127).  With the
+  // S = 2 tiles wide, same process against the build before
+  // (profiles/r05_ab_lib_tgpu_s2.jsonl): N = 32 / 48 / 64 / 100 / 127
+  // -10.0 / -10.2 / -12.2 / -10.6 / -7.8 %, C100 N = 64 / 128 -11.6 / -6.0 %
+  // (0.83-0.85 of 8 TB/s); S = 1 riders only: 1-3 points less
   {
     std::vector<int> grp(t.size());
+    int cnt[5] = {0, 0, 0, 0, 0};
     for (size_t i = 0; i < t.size(); ++i) {
       const int b = t[i].kind & 0xFF;
       grp[i] = (b == K_F32_TGPU_IN || b == K_I64_TGPU_IN) ? 0 : (t[i].kind >> 8) & 0xFF;
+      cnt[grp[i]]++;
+    }
+    const bool ride = cnt[1] > 0 && cnt[1] >= cnt[0] && cnt[1] >= cnt[2];
+    // sort key: launch group, riders before the group's own tiles
+    std::vector<int> key(t.size());
+    for (size_t i = 0; i < t.size(); ++i) {
+      const bool rider = ride && (grp[i] == 0 || grp[i] == 2);
+      if (rider) grp[i] = 1;
+      key[i] = 2 * grp[i] + (rider ? 0 : 1);
     }
     std::vector<size_t> ord(t.size());
     for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
-    std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return grp[x] < grp[y]; });
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return key[x] < key[y]; });
     std::vector<Tile> t2;
     std::vector<float> f2;
     for (size_t i : ord) {
@@ -1642,6 +1784,7 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
   p->tgpu_batch = tgpu_batch_for(n);
   for (const Tile& x : t) (kind_is64(x.kind) ? p->has64 : p->has32) = true;
   hipError_t e = hipGetDevice(&p->device);
+  if (e == hipSuccess) p->tgpu_s2_lds = tgpu_s2_lds(p->device);
   if (e == hipSuccess && !t.empty()) {
     e = hipMalloc(&p->d_tiles, t.size() * sizeof(Tile));
     if (e == hipSuccess)
@@ -2037,7 +2180,9 @@ int fa_reduce_tab(const fa_plan* plan, const float* const* c32, const int64_t* c
           else
             hipLaunchKernelGGL((tgpu_kernel<0, 16, 1>), dim3(cnt), dim3(kBlock), 0, st, a);
           break;
-        case 1: hipLaunchKernelGGL(tgpu_kernel<1>, dim3(cnt), dim3(kBlock), 0, st, a); break;
+        case 1:
+          hipLaunchKernelGGL(tgpu_kernel<1>, dim3(cnt), dim3(kBlock), plan->tgpu_s2_lds, st, a);
+          break;
         case 2: hipLaunchKernelGGL(tgpu_kernel<2>, dim3(cnt), dim3(kBlock), 0, st, a); break;
         case 3: hipLaunchKernelGGL(tgpu_kernel<3>, dim3(cnt), dim3(kBlock), 0, st, a); break;
         default: hipLaunchKernelGGL(tgpu_kernel<4>, dim3(cnt), dim3(kBlock), 0, st, a); break;

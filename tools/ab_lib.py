@@ -44,7 +44,10 @@ CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
          ("cfg5_tgpu", "wrnsl16_8_sf4_c100", 24, 1), ("sf32_tgpu", "wrnsl16_8_sf32_c100", 3, 6),
          ("c10_n5_tgpu", "wrn16_8_c10", 5, 2), ("c10_n12_tgpu", "wrn16_8_c10", 12, 1),
          ("c10_n16_tgpu", "wrn16_8_c10", 16, 1), ("c10_n17_tgpu", "wrn16_8_c10", 17, 1),
-         ("c10_n28_tgpu", "wrn16_8_c10", 28, 1), ("c100_n20_tgpu", "wrn16_8_c100", 20, 1)]
+         ("c10_n28_tgpu", "wrn16_8_c10", 28, 1), ("c100_n20_tgpu", "wrn16_8_c100", 20, 1),
+         ("c10_n48_tgpu", "wrn16_8_c10", 48, 1), ("c10_n100_tgpu", "wrn16_8_c10", 100, 1),
+         ("c10_n127_tgpu", "wrn16_8_c10", 127, 1), ("c100_n64_tgpu", "wrn16_8_c100", 64, 1),
+         ("c100_n128_tgpu", "wrn16_8_c100", 128, 1)]
 
 
 def load(path):
