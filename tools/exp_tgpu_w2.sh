@@ -1,7 +1,7 @@
 # Experiment record (r05): the torch-GPU-order S = 2 group (N >= 32) as
 # 2048-element client-loop tiles with the small groups riding in its launch,
 # against the build before it (tools/libfedagg_before_tgpu_w2.so, not kept);
-# r1 = S = 1 riders only (tools/libfedagg_tgpu_r1.so), r14 = S = 1 and S = 4
+# r1 = S = 1 riders only (tools/libfedagg_tgpu_r1.so, not kept), r14 = S = 1 and S = 4
 # riders (the tree's build); results in profiles/r05_ab_lib_tgpu_s2.jsonl
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
