@@ -344,12 +344,16 @@ __device__ __forceinline__ void tgpu_wide(KArgs& a, int64_t start, int count, fl
     // the client loop (as reduce_impl.h pipe2_clients): row b + 1's loads
     // before row b's adds; four rows per pass keep row b's accumulator
     // index (b & 3) static.  The rows' order per accumulator is unchanged.
+    // Pointers through scalar loads only (sptr32): cptr32's table arm is a
+    // vector load, and the compiler then waited for the current row's data
+    // before issuing the next row's loads (ISA read; same process -0.3 ..
+    // -0.9 % on cfg2 / cfg3 / cfg5, profiles/r05_ab_lib_tgpu_sptr.jsonl).
     // Same process, r05: cfg2 order 139.9 -> 136.7 us, cfg5 169.9 -> 166.6,
     // N = 17 / 28 -2.8 / -2.5 %, cfg3 and N = 2..16 -1.3 .. +0.1 %, unlike
     // the default kernel's rule: both batch sizes take it
     f4 cur[U], nxt[U];
     {
-      const float* p = cptr32(a, 0) + start;
+      const float* p = sptr32(a, 0) + start;
 #pragma unroll
       for (int u = 0; u < U; ++u) cur[u] = ldg4<true>(p, vi[u]);
     }
@@ -359,7 +363,7 @@ __device__ __forceinline__ void tgpu_wide(KArgs& a, int64_t start, int count, fl
         const int b = b0 + k;
         if (b < n) {
           if (b + 1 < n) {
-            const float* p = cptr32(a, b + 1) + start;
+            const float* p = sptr32(a, b + 1) + start;
 #pragma unroll
             for (int u = 0; u < U; ++u) nxt[u] = ldg4<true>(p, vi[u]);
           }
@@ -440,7 +444,7 @@ __device__ __forceinline__ void tgpu_wide_loop(KArgs& a, int64_t start, int coun
   const int n = a.n;
   f4 cur[U], nxt[U];
   {
-    const float* p = cptr32(a, 0) + start;
+    const float* p = sptr32(a, 0) + start;
 #pragma unroll
     for (int u = 0; u < U; ++u) cur[u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
   }
@@ -450,7 +454,7 @@ __device__ __forceinline__ void tgpu_wide_loop(KArgs& a, int64_t start, int coun
       const int b = b0 + k;
       if (b < n) {
         if (b + 1 < n) {
-          const float* p = cptr32(a, b + 1) + start;
+          const float* p = sptr32(a, b + 1) + start;
 #pragma unroll
           for (int u = 0; u < U; ++u) nxt[u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
         }
