@@ -7,7 +7,9 @@ is called (fa_plan_create, fa_reduce, fa_synth_fill_*).
 
     python tools/ab_lib.py LIB_A LIB_B [ROUNDS] [CASES]
     AB_SLAB=1: each client set carved from one slab (feddct_amd/slab.py), as
-    the product places them; AB_FLAGS=1: whole rounds (FA_F_BCAST)
+    the product places them; AB_FLAGS=1: whole rounds (FA_F_BCAST);
+    AB_PFLAGS_B=<int>: plan flags ORed into LIB_B's plans (e.g. 8 =
+    FA_PLAN_TUNE_BATCH16), so one library can be A/B'd against itself
 """
 import ctypes
 import json
@@ -85,6 +87,7 @@ def layout_of(stem):
 
 SLAB = os.environ.get("AB_SLAB", "0") == "1"   # clients carved from one slab (slab.py)
 FLAGS = int(os.environ.get("AB_FLAGS", "0"))   # fa_reduce flags (1: FA_F_BCAST, the round)
+PFLAGS_B = int(os.environ.get("AB_PFLAGS_B", "0"))   # extra plan flags for LIB_B
 
 
 def fill(lib, lay, parts, c, dev):
@@ -137,16 +140,17 @@ def main():
                 ctx.__exit__(None, None, None)
             sets.append((cl, torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])))
         plans = []
-        for lib in libs:
+        for k, lib in enumerate(libs):
+            g = G | (PFLAGS_B if k == 1 else 0)
             a32, n32 = segs(lay.segs32)
             a64, n64 = segs(lay.segs64)
             h = _P()
             if name.endswith("_tgpu"):
                 ok(lib, lib.fa_plan_create_order(a32, n32, lay.f32_numel, a64, n64, lay.i64_numel,
-                                                 n, 1, G, ctypes.byref(h)), "plan")
+                                                 n, 1, g, ctypes.byref(h)), "plan")
             else:
                 ok(lib, lib.fa_plan_create(a32, n32, lay.f32_numel, a64, n64, lay.i64_numel, 0,
-                                           G, ctypes.byref(h)), "plan")
+                                           g, ctypes.byref(h)), "plan")
             plans.append(h)
         ptrs = [((_P * n)(*[c[0].data_ptr() for c in cl]), (_P * n)(*[c[1].data_ptr() for c in cl]),
                  o32, o64) for cl, o32, o64 in sets]
