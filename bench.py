@@ -1681,6 +1681,21 @@ def main():
                 extra["torch_gpu_order_mode"] = torch_gpu_order_mode(layout, clients)
             except Exception as e:  # noqa: BLE001
                 extra["torch_gpu_order_mode"] = {"error": repr(e)}
+            # the same at N = 32, where torch splits the large tensors' rows
+            # in two (S = 2), beside the default order's time
+            try:
+                more = make_clients(layout, manifest, range(first + N_CLIENTS, first + 32), dev)
+                c32 = clients + more
+                m32 = torch_gpu_order_mode(layout, c32)
+                d32, d64 = torch.zeros_like(out32), torch.zeros_like(out64)
+                td, _ = timed_launches(Reducer(layout, c32, d32, d64), 20, 3)
+                m32["default_order_us"] = round(td * 1e6, 1)
+                m32["n"] = 32
+                extra["torch_gpu_order_mode_n32"] = m32
+                del more, c32, d32, d64
+                torch.cuda.empty_cache()
+            except Exception as e:  # noqa: BLE001
+                extra["torch_gpu_order_mode_n32"] = {"error": repr(e)}
             # the round with its broadcast (FA_F_BCAST: reduce launch + broadcast
             # launch over the same tiles), N*B read + (N+1)*B written — after
             # every measurement that needs the clients' own values
