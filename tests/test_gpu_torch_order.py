@@ -141,13 +141,19 @@ def test_row_split_kernels_match_torch_gpu_mean(lib, n):
     assert _vs_torch(layout, cl, out32, out64) == []
 
 
-@pytest.mark.parametrize("case", ["cfg2", "cfg3", "cfg5", "small_adversarial"])
+# r05: c10_n32 / c100_n64 — torch splits the large tensors' rows in two
+# (S = 2, 2048-element client-loop tiles) and the S = 1, S = 4 and inner
+# tiles ride in that launch (fa_plan_create_order)
+@pytest.mark.parametrize("case", ["cfg2", "cfg3", "cfg5", "small_adversarial", "c10_n32",
+                                  "c100_n64"])
 def test_kernel_matches_torch_gpu_mean(lib, case):
     from feddct_amd.workload import joint_manifest, make_clients
-    if case == "cfg2":
-        man = load_manifest("wrn16_8_c10")
+    if case in ("cfg2", "c10_n32", "c100_n64"):
+        stem, n = {"cfg2": ("wrn16_8_c10", 20), "c10_n32": ("wrn16_8_c10", 32),
+                   "c100_n64": ("wrn16_8_c100", 64)}[case]
+        man = load_manifest(stem)
         layout = BucketLayout.from_manifest(man)
-        cl = make_clients(layout, man, range(20), DEV)
+        cl = make_clients(layout, man, range(n), DEV)
     elif case in ("cfg3", "cfg5"):
         tag, n = ("c10", 5) if case == "cfg3" else ("c100", 24)
         mm = load_manifest(f"wrnsl16_8_sf4_{tag}_main")
