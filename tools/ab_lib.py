@@ -49,7 +49,11 @@ CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
          ("c10_n28_tgpu", "wrn16_8_c10", 28, 1), ("c100_n20_tgpu", "wrn16_8_c100", 20, 1),
          ("c10_n48_tgpu", "wrn16_8_c10", 48, 1), ("c10_n100_tgpu", "wrn16_8_c10", 100, 1),
          ("c10_n127_tgpu", "wrn16_8_c10", 127, 1), ("c100_n64_tgpu", "wrn16_8_c100", 64, 1),
-         ("c100_n128_tgpu", "wrn16_8_c100", 128, 1)]
+         ("c100_n128_tgpu", "wrn16_8_c100", 128, 1),
+         # r05: the N <= 3 table (every column in the vector runs)
+         ("sf32w", "wrnsl16_8_sf32_c100", 3, 6), ("c10_n3", "wrn16_8_c10", 3, 2),
+         ("r110_n2", "resnet110sl_sf4_c100", 2, 6), ("r110_n3", "resnet110sl_sf4_c100", 3, 6),
+         ("sf16_n3", "wrnsl16_8_sf16_c100", 3, 6)]
 
 
 def load(path):
