@@ -772,12 +772,16 @@ def cfg5_sharded(dev, world, rank, group, steps, ncomm=None, chain_chunks=16):
 
     out = {"slots": n, "slots_per_gpu": hi - lo, "algorithmic_bytes": nbytes}
 
-    def mode(name, make, root, k, exact):
+    def mode(name, make, root, k, exact, model=None):
         try:
             b32, b64 = torch.zeros_like(o32), torch.zeros_like(o64)
             t = tmax(make(b32, b64), k, 2)
             r = {"ms": round(t * 1e3, 4), "GBps": round(nbytes / t / 1e9, 2),
                  "result_on": f"rank {root}"}
+            if model is not None:
+                from feddct_amd import comm as Cm
+                r["model_us"] = round(Cm.round_model(model[0], lay, counts, nchunks=model[1],
+                                                     root=root)["model_us"], 1)
             if exact:
                 r["bit_exact_vs_reference_digest"] = exact_on(root, b32, b64)
             out[name] = r
@@ -785,23 +789,27 @@ def cfg5_sharded(dev, world, rank, group, steps, ncomm=None, chain_chunks=16):
         except Exception as e:  # noqa: BLE001
             out[name] = {"error": repr(e)}
             return None
+    counts = [b - a for a, b in (shard_range(n, world, r) for r in range(world))]
     if ncomm is not None:
+        from feddct_amd import comm as Cm
         from feddct_amd.comm import (NativeAggregator, NativeChainedAggregator,
-                                     NativeStripedAggregator)
-        # the default entry (r05: exact; it picks the chained round at 8 x 3)
-        counts = [b - a for a, b in (shard_range(n, world, r) for r in range(world))]
+                                     NativeStripedAggregator, multi_select)
+        # the default entry (r06: the cost model's exact form and chunk count
+        # — the link-parallel striped round at 8 x 3; r05: chained)
         droot = max(r for r in range(world) if counts[r] > 0)
+        form, fk, _ = multi_select(counts, layout=lay, detail=True)
         mode("default_native", lambda b32, b64: NativeAggregator(
             lay, l32, l64, n, b32, b64, ncomm, final="reduce", root=droot).step, droot, steps,
-            True)
-        from feddct_amd.comm import multi_select
+            True, model=(Cm.MODE_IDS[form], fk))
         if "default_native" in out and "ms" in out["default_native"]:
-            out["default_native"]["form"] = multi_select(counts)
+            out["default_native"].update(form=form, nchunks=fk)
         mode("chained_native", lambda b32, b64: NativeChainedAggregator(
             lay, l32, l64, n, b32, b64, ncomm, nchunks=chain_chunks, final="reduce",
-            root=last).step, last, steps, True)
-        mode("e2_native", lambda b32, b64: NativeStripedAggregator(
-            lay, l32, l64, n, b32, b64, ncomm, final="reduce").step, 0, max(2, steps // 4), True)
+            root=last).step, last, steps, True, model=(Cm.FA_MODE_CHAINED, chain_chunks))
+        for k in (1, 4):
+            mode(f"striped_native_c{k}", lambda b32, b64, k=k: NativeStripedAggregator(
+                lay, l32, l64, n, b32, b64, ncomm, final="reduce", root=last,
+                nchunks=k).step, last, max(2, steps // 2), True, model=(Cm.FA_MODE_STRIPED, k))
     mode("chained_torch_distributed", lambda b32, b64: (lambda a: lambda: a.step(l32, l64))(
         ChainAggregator(lay, n, b32, b64, group=group, final="reduce", root=last,
                         nchunks=chain_chunks)), last, max(2, steps // 2), True)
@@ -1341,7 +1349,13 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
     def phase(name):
         return PhaseDeadline(name, deadline_s, abort_run)
 
-    def run_mode(name, make, root, exact_class, steps=None, warm=None):
+    counts = [N_CLIENTS] * world
+
+    def run_mode(name, make, root, exact_class, steps=None, warm=None, model=None):
+        """``model``: (FA_MODE_*, nchunks) of a native form — its modelled
+        time (fa_round_model, the same root) goes beside the measured one,
+        and one extra round runs profiled (fa_comm_set_profile: the exchange
+        and the kernels on each stream, r06 VERDICT r05 next 4)."""
         log(f"[rank {rank}] {name}")
         try:
             with phase(name):
@@ -1349,6 +1363,21 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
                 fn = make(o32, o64)
                 t = tmax(fn, steps or args.steps, args.warmup if warm is None else warm)
             modes[name] = {"t": t, "root": root, "out": (o32, o64), "exact_class": exact_class}
+            if model is not None and ncomm is not None:
+                from feddct_amd import comm as Cm
+                modes[name]["model_us"] = round(Cm.round_model(
+                    model[0], layout, counts, nchunks=model[1], root=root)["model_us"], 1)
+                plan = getattr(getattr(fn, "__self__", None), "plan", None)
+                if plan is not None and world > 1:
+                    with phase(name + " (profiled)"):
+                        ncomm.set_profile(True)
+                        try:
+                            fn()
+                            modes[name]["profile"] = Cm.plan_profile(plan)
+                        finally:
+                            ncomm.set_profile(False)
+                        torch.cuda.synchronize()
+                        dist.barrier(group=group)
         except Exception as e:  # noqa: BLE001  (reported in the line, every rank alike)
             modes[name] = {"error": repr(e)}
 
@@ -1360,28 +1389,38 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
         except Exception as e:  # noqa: BLE001
             extra["native_comm_error"] = repr(e)
     if ncomm is not None:
+        from feddct_amd import comm as Cm
         from feddct_amd.comm import (FA_XCHG_RS_GATHER, NativeAggregator,
                                      NativeBlockedAggregator, NativeChainedAggregator,
                                      NativeShardedAggregator, NativeStripedAggregator,
                                      multi_select)
-        # the DEFAULT entry first (r05: exact; the form it picks for these
-        # counts is in the name)
-        form = multi_select([N_CLIENTS] * world)
-        droot = 0 if form == "blocked" else last
+        extra["multi_env"] = multi_env(ncomm, world)
+        # the DEFAULT entry first (r06: the exact form and chunk count the
+        # cost model picks for these counts on this layout, result on the
+        # last rank — the model's root; the form is in the name)
+        form, fk, fus = multi_select(counts, layout=layout, detail=True)
+        droot = last
+        extra["default_choice"] = {"form": form, "nchunks": fk, "model_us": round(fus, 1)}
         run_mode(f"default={form}/native", lambda o32, o64: NativeAggregator(
             layout, l32, l64, n_total, o32, o64, ncomm, final="reduce", root=droot).step,
-            droot, True)
+            droot, True, model=(Cm.MODE_IDS[form], fk))
         run_mode("blocked/native", lambda o32, o64: NativeBlockedAggregator(
-            layout, l32, l64, n_total, o32, o64, ncomm, final="reduce", root=0).step, 0, True)
+            layout, l32, l64, n_total, o32, o64, ncomm, final="reduce", root=0).step, 0, True,
+            model=(Cm.FA_MODE_BLOCKED, 1))
         run_mode("blocked/native/allreduce", lambda o32, o64: NativeBlockedAggregator(
             layout, l32, l64, n_total, o32, o64, ncomm, final="allreduce").step, -1, True,
-            steps=max(5, args.steps // 2))
-        run_mode("chained/native", lambda o32, o64: NativeChainedAggregator(
-            layout, l32, l64, n_total, o32, o64, ncomm, nchunks=args.chain_chunks,
-            final="reduce", root=last).step, last, True)
+            steps=max(5, args.steps // 2), model=(Cm.FA_MODE_BLOCKED, 1))
+        # the chained round's chunk count and the striped round's, swept
+        # (the model picks them; the first multi-GPU run checks it)
+        for k in (4, 8, 16, 32):
+            run_mode(f"chained/native/c{k}", lambda o32, o64, k=k: NativeChainedAggregator(
+                layout, l32, l64, n_total, o32, o64, ncomm, nchunks=k, final="reduce",
+                root=last).step, last, True, steps=max(5, args.steps // 4),
+                model=(Cm.FA_MODE_CHAINED, k))
         run_mode("chained/native/allreduce", lambda o32, o64: NativeChainedAggregator(
             layout, l32, l64, n_total, o32, o64, ncomm, nchunks=args.chain_chunks,
-            final="allreduce").step, -1, True, steps=max(5, args.steps // 2))
+            final="allreduce").step, -1, True, steps=max(5, args.steps // 2),
+            model=(Cm.FA_MODE_CHAINED, args.chain_chunks))
         run_mode("e1/native/reduce", lambda o32, o64: NativeShardedAggregator(
             layout, l32, l64, n_total, o32, o64, ncomm, nchunks=args.chunks,
             final="reduce").step, 0, False)
@@ -1389,9 +1428,11 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
             layout, l32, l64, n_total, o32, o64, ncomm, nchunks=args.chunks, final="reduce",
             exchange=FA_XCHG_RS_GATHER).step, 0, False)
         if not args.no_exact:
-            run_mode("e2/native", lambda o32, o64: NativeStripedAggregator(
-                layout, l32, l64, n_total, o32, o64, ncomm, final="reduce").step, 0, True,
-                steps=max(5, args.steps // 2))
+            for k in (1, 2, 4, 8):
+                run_mode(f"striped/native/c{k}", lambda o32, o64, k=k: NativeStripedAggregator(
+                    layout, l32, l64, n_total, o32, o64, ncomm, final="reduce", root=last,
+                    nchunks=k).step, last, True, steps=max(5, args.steps // 4),
+                    model=(Cm.FA_MODE_STRIPED, k))
     run_mode("chained/torch.distributed", lambda o32, o64: (lambda a: lambda: a.step(l32, l64))(
         ChainAggregator(layout, n_total, o32, o64, group=group, final="reduce", root=last,
                         nchunks=args.chain_chunks)), last, True, steps=max(5, args.steps // 2))
@@ -1440,6 +1481,9 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
             r = {"ms_per_step": round(m["t"] * 1e3, 4),
                  "GBps": round(nbytes_rank * world / m["t"] / 1e9, 2),
                  "result_on": "every rank" if m["root"] < 0 else f"rank {m['root']}"}
+            for k in ("model_us", "profile"):
+                if k in m:
+                    r[k] = m[k]
             if rank == 0:
                 # every element of every key (the padding between keys is no
                 # tensor's and each mode leaves it as it likes)
@@ -1492,6 +1536,25 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
         except Exception as e:  # noqa: BLE001
             extra["cfg5_feddct_c100_n24_sharded"] = {"error": repr(e)}
     return best_t, t_kernel, ncomm
+
+def multi_env(ncomm, world):
+    """What the first real multi-GPU run needs to be read (VERDICT r05 next
+    4): the RCCL / NCCL / HSA / HIP environment of this process, the
+    communicator's rank count as RCCL reports it, and which devices this
+    process sees can access each other's memory (hipDeviceCanAccessPeer)."""
+    from feddct_amd import comm as Cm
+    env = {k: v for k, v in sorted(os.environ.items())
+           if k.startswith(("RCCL_", "NCCL_", "HSA_", "HIP_", "GPU_MAX_HW_QUEUES"))}
+    n, r, d = ncomm.info()
+    ndev = torch.cuda.device_count()
+    peer = [[1 if i == j else int(torch.cuda.can_device_access_peer(i, j)) for j in range(ndev)]
+            for i in range(ndev)]
+    return {"env": env, "comm_count": n, "comm_rank": r, "comm_device": d, "world": world,
+            "visible_devices": ndev, "peer_access": peer,
+            "model_constants": {"link_GBps": Cm.MODEL_LINK_GBPS, "hbm_GBps": Cm.MODEL_HBM_GBPS,
+                                "group_us": Cm.MODEL_GROUP_US,
+                                "kernel_us": Cm.MODEL_KERNEL_US}}
+
 
 def build_line(args, world, nbytes_rank, bytes_per_client, t_step, t_kernel, extra):
     """The one JSON line (bench contract) from the measured times + extras."""

@@ -54,7 +54,7 @@ EXPORTS = [
     "fa_prox_grad_ex",
     "fa_read_probe_f32", "fa_write_probe_f32", "fa_tune_prox_store", "fa_tune_prox_cpw", "fa_chain_levels", "fa_reduce_chain", "fa_torch_gpu_config",
     "fa_plan_create_order", "fa_table_bytes", "fa_reduce_tab",
-    "fa_plan_balance_host", "fa_plan_launch_shape",
+    "fa_plan_balance_host", "fa_plan_launch_shape", "fa_plan_launch_form",
 ]
 
 
@@ -108,6 +108,8 @@ def _load():
         "fa_table_bytes": (ctypes.c_size_t, [_I]),
         "fa_plan_balance_host": (_I, [_P, _I, _I, _I, _I, _P, _I]),
         "fa_plan_launch_shape": (_I, [_P, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+        "fa_plan_launch_form": (_I, [_P, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
+                                     ctypes.POINTER(_I)]),
         "fa_reduce_tab": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, ctypes.c_uint, _P]),
         "fa_mean_f32": (_I, [_P, _I, _I64, _P, _P, _I, _P]),
         "fa_weighted_f32": (_I, [_P, _P, _I, _I64, _P, _P, _I, _P]),
@@ -247,6 +249,14 @@ class Plan:
         check(lib.fa_plan_launch_shape(self.handle, int(n), int(bool(weighted)), ctypes.byref(nt),
                                        ctypes.byref(sl)), "fa_plan_launch_shape")
         return nt.value, sl.value
+
+    def launch_form(self, n, weighted=False):
+        """(tile width in floats, clients per load batch, pipe) of the kernel a
+        plain fa_reduce call with n clients runs (pipe 1: the client loop)."""
+        te, b, p = _I(), _I(), _I()
+        check(lib.fa_plan_launch_form(self.handle, int(n), int(bool(weighted)), ctypes.byref(te),
+                                      ctypes.byref(b), ctypes.byref(p)), "fa_plan_launch_form")
+        return te.value, b.value, p.value
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -724,7 +724,9 @@ __global__ __launch_bounds__(kBlock) void write_probe_kernel(BcastArgs a, int64_
   if (v >= nv) return;
   const uint32_t b = (uint32_t)(4 * v) ^ seed;
   const f4 x = {probe_val(b), probe_val(b + 1), probe_val(b + 2), probe_val(b + 3)};
-  for (int c = c0; c < c1; ++c) st_bc(a.dst[c], (uint32_t)v, x);
+  // based at the part's start, as bcast_flat2_kernel: the buffer offset is
+  // 32-bit, so a bucket-based offset would wrap past 2^28 float4s
+  for (int c = c0; c < c1; ++c) st_bc(a.dst[c] + 4 * (int64_t)p * kBlock, threadIdx.x, x);
 }
 
 // Read-only probe in the reduce's own shape (grid = 0 in fa_read_probe_f32):
@@ -1750,6 +1752,12 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
     std::vector<int> key(t.size());
     for (size_t i = 0; i < t.size(); ++i) {
       const bool rider = ride && (grp[i] == 0 || grp[i] == 2);
+      // tgpu_kernel<1> reduces every vector (V) rider with the S = 4 path: S = 1
+      // keys never make V tiles (wide = S <= 2 above); refuse a table that
+      // would, rather than reduce it in the wrong order
+      if (rider && (t[i].kind & 0xFF) == K_F32_TGPU_V && ((t[i].kind >> 8) & 0xFF) != 2)
+        return set_err(FA_E_INVAL, "torch-GPU order planner: a vector rider of row split %d",
+                       1 << ((t[i].kind >> 8) & 0xFF));
       if (rider) grp[i] = 1;
       key[i] = 2 * grp[i] + (rider ? 0 : 1);
     }
@@ -2060,6 +2068,23 @@ int fa_plan_launch_shape(const fa_plan* plan, int n, int weighted, int* ntiles, 
   *slots = L.slots ? L.slots
                    : call_slots(plan->device, n, L.vec_u, weighted != 0,
                                 plan->flags & ~FA_PLAN_TUNE_NO_BALANCE);
+  return FA_OK;
+}
+
+int fa_plan_launch_form(const fa_plan* plan, int n, int weighted, int* tile_elems, int* batch,
+                        int* pipe) {
+  if (!plan || !tile_elems || !batch || !pipe || n < 1)
+    return set_err(FA_E_INVAL, "fa_plan_launch_form: bad arguments");
+  if (plan->order == FA_ORDER_TORCH_GPU) {
+    *tile_elems = 0;
+    *batch = 0;
+    *pipe = 0;
+    return FA_OK;
+  }
+  const Launch L = select_launch(plan, n, weighted != 0, 0);
+  *tile_elems = 4 * kBlock * L.vec_u;
+  *batch = L.batch;
+  *pipe = pipe_rule(plan, L, n, weighted != 0);
   return FA_OK;
 }
 

@@ -66,6 +66,7 @@ struct fa_comm {
   int nranks = 0, rank = 0, device = 0;
   hipStream_t cs = nullptr;  // communication stream
   bool graphs = false;       // replay rounds from captured HIP graphs (fa_comm_set_graphs)
+  bool profile = false;      // time every group and kernel of a round (fa_comm_set_profile)
 };
 
 namespace {
@@ -111,6 +112,45 @@ __global__ void scatter_f32_kernel(const float* __restrict__ src, const int64_t*
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < width;
        e += (int64_t)gridDim.x * blockDim.x)
     dst[idx[e]] = src[e];
+}
+
+// Weighted striped rounds (r06): local client j's columns [off, off + count)
+// times its weight, the product rounded as the weighted reduce rounds it
+// (__fmul_rn, no contraction), into staging row j.  The receivers reduce
+// these rows with weight 1 (x * 1 == x exactly), their own clients with
+// their weights: the one-GPU weighted order's bits.
+struct ScaleArgs {
+  const float* src[kStackPtrs];
+  float w[kStackPtrs];
+  float* dst;
+  int64_t plane;  // staging row stride (floats)
+  int64_t off, count;
+  int rows;
+  int vec;        // every row's src + off and dst + off 16-B aligned
+};
+__global__ void scale_rows_kernel(ScaleArgs a) {
+  const int r = blockIdx.y;
+  if (r >= a.rows) return;
+  const float* s = a.src[r] + a.off;
+  float* d = a.dst + r * a.plane + a.off;
+  const float w = a.w[r];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t e0 = 0;
+  if (a.vec) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const int64_t nv = a.count / 4;
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv; v += stride) {
+      f4v x = ((const f4v*)s)[v];
+      x.x = __fmul_rn(x.x, w);
+      x.y = __fmul_rn(x.y, w);
+      x.z = __fmul_rn(x.z, w);
+      x.w = __fmul_rn(x.w, w);
+      ((f4v*)d)[v] = x;
+    }
+    e0 = 4 * nv;
+  }
+  for (int64_t e = e0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < a.count; e += stride)
+    d[e] = __fmul_rn(s[e], w);
 }
 
 // Blocked mode: an owner's fold of the block sums of its column stripe, in
@@ -300,25 +340,10 @@ struct Sched {
   void next() { ++step; }
 };
 
-// Round-robin pairing of the ranks (circle method): round t's partner of
-// rank r, or -1 (the odd rank out).  Every pair meets in exactly one round,
-// and within a pair the lower rank sends first, so a transport that
-// serialises a rank's sends and receives (gloo) cannot deadlock.
-int partner(int nranks, int r, int t) {
-  const int m = nranks % 2 ? nranks + 1 : nranks;  // even, with a dummy rank m-1
-  if (m < 2) return -1;
-  const int k = m - 1;                             // rounds t = 0..k-1
-  int q = -1;
-  if (r == k) {
-    for (int i = 0; i < k; ++i)
-      if ((2 * i) % k == t % k) q = i;             // the i with 2i == t (mod k)
-  } else if ((2 * r) % k == t % k) {
-    q = k;
-  } else {
-    q = ((t - r) % k + k) % k;                     // pairs i + j == t (mod k)
-  }
-  return q >= nranks ? -1 : q;
-}
+// The striped round's default column chunks per stripe (fa_stripe_plan_create,
+// nchunks 0): the chunk c + 1 exchange overlaps chunk c's stripe reduce and
+// the chunk c - 1 results; fa_multi_select_layout picks the count by the model.
+constexpr int kStripeChunks = 4;
 
 // The int64 keys (num_batches_tracked) of every client, gathered raw and
 // reduced exactly by the result ranks; with `tails`, the fp32 scalar columns
@@ -378,54 +403,74 @@ void sched_sharded(const Geo& g, const std::vector<std::pair<int64_t, int64_t>>&
   sched_raw_gather(S, g, 0, false, result);
 }
 
-// e2: column stripes.
-void sched_striped(const Geo& g, const std::vector<int64_t>& lo, int root, Sched* S) {
+// e2: column stripes, cut into column chunks; every peer in one group per
+// chunk (r06, VERDICT r05 next 1: r02-r05 ran one RCCL group per partner, so
+// a rank used one of its xGMI links at a time).  clo[r][c .. c+1]: chunk c of
+// rank r's stripe.  Step 2 + j carries, in ONE group, chunk j's client
+// exchange with every peer and the finished chunk j - 2 to the result ranks,
+// and — on the caller's stream, concurrent with that group — the stripe
+// reduce of chunk j - 1, whose rows arrived in the previous step's group
+// (the executor starts a compute-stream kernel that reads exchanged data
+// after the exchanges of the steps BEFORE its own: reads_exchanged below).
+// Per pair, the sender posts its client rows then its result chunk and the
+// receiver its receives in the same order (RCCL matches a pair's sends and
+// receives in posting order).  Weighted: the rows sent are the local
+// clients' pre-multiplied values (FA_X_K_SCALE into WSTAGE, step 0).
+void sched_striped(const Geo& g, const std::vector<std::vector<int64_t>>& clo, int root,
+                   bool weighted, Sched* S) {
   const int me = g.rank, W = g.nranks;
+  const int C = (int)clo[0].size() - 1;
   const bool result = root < 0 || root == me;
-  const int64_t Lme = lo[me + 1] - lo[me];
-  // 1. every client's values for stripe r go to rank r, one partner per round
-  const int rounds = W % 2 ? W : W - 1;
-  for (int t = 0; t < rounds; ++t) {
-    const int r = partner(W, me, t);
-    if (r < 0 || r == me) continue;
-    const int64_t Lr = lo[r + 1] - lo[r];
-    auto sends = [&]() {
-      if (Lr > 0)
-        for (int j = 0; j < g.n_local; ++j)
-          S->add(FA_X_SEND, r, FA_B_CLIENT, j, FA_B_NONE, -1, lo[r], Lr);
-    };
-    auto recvs = [&]() {
-      if (Lme > 0)
-        for (int k = 0; k < g.counts[r]; ++k)
-          S->add(FA_X_RECV, r, FA_B_NONE, -1, FA_B_RECV, g.first[r] + k, lo[me], Lme);
-    };
-    if (me < r) { sends(); recvs(); } else { recvs(); sends(); }
-    S->next();
+  const bool i64 = !g.t64.empty();
+  auto len = [&](int r, int c) { return clo[r][c + 1] - clo[r][c]; };
+  // step 0: the int64 keys stacked; weighted: the local clients' values
+  // outside this rank's stripe (what the peers receive) pre-multiplied
+  if (i64 && g.n_local > 0)
+    S->add(FA_X_K_STACK, -1, FA_B_CLIENT, -1, FA_B_STACK, -1, 0, 0, -1, g.lo_slot, g.n_local);
+  const int64_t mlo = clo[me][0], mhi = clo[me][C];
+  if (weighted && g.n_local > 0) {
+    if (mlo > 0)
+      S->add(FA_X_K_SCALE, -1, FA_B_CLIENT, -1, FA_B_WSTAGE, -1, 0, mlo, -1, 0, g.n_local);
+    if (mhi < g.f32_numel)
+      S->add(FA_X_K_SCALE, -1, FA_B_CLIENT, -1, FA_B_WSTAGE, -1, mhi, g.f32_numel - mhi, -1, 0,
+             g.n_local);
   }
   S->next();
-  // 2. the stripe over all n_total clients, exact order
-  if (Lme > 0)
-    S->add(FA_X_K_STRIPE, -1, FA_B_RECV, -1, FA_B_STRIPE, -1, lo[me], Lme, me, 0, g.n_total);
+  // step 1: the int64 keys of every rank (a few bytes)
+  if (i64)
+    S->add(FA_X_ALLGATHER, -1, FA_B_STACK, 1, FA_B_GATHER, 1, 0, (int64_t)g.nmax * g.i64_numel);
   S->next();
-  // 3. the finished stripes to the result ranks, pairwise again
-  for (int t = 0; t < rounds; ++t) {
-    const int r = partner(W, me, t);
-    if (r < 0 || r == me) continue;
-    const int64_t Lr = lo[r + 1] - lo[r];
-    const bool r_result = root < 0 || root == r;
-    auto sends = [&]() {
-      if (Lme > 0 && r_result) S->add(FA_X_SEND, r, FA_B_STRIPE, -1, FA_B_NONE, -1, lo[me], Lme);
-    };
-    auto recvs = [&]() {
-      if (Lr > 0 && result) S->add(FA_X_RECV, r, FA_B_NONE, -1, FA_B_OUT, -1, lo[r], Lr);
-    };
-    if (me < r) { sends(); recvs(); } else { recvs(); sends(); }
+  const int src = weighted ? FA_B_WSTAGE : FA_B_CLIENT;
+  for (int j = 0; j <= C + 1; ++j) {
+    for (int q = 1; q < W; ++q) {  // peers in a rotated order: rank me + q first
+      const int r = (me + q) % W;
+      if (j < C) {
+        if (len(r, j) > 0)
+          for (int k = 0; k < g.n_local; ++k)
+            S->add(FA_X_SEND, r, src, k, FA_B_NONE, -1, clo[r][j], len(r, j), j);
+        if (len(me, j) > 0)
+          for (int k = 0; k < g.counts[r]; ++k)
+            S->add(FA_X_RECV, r, FA_B_NONE, -1, FA_B_RECV, g.first[r] + k, clo[me][j],
+                   len(me, j), j);
+      }
+      const int c = j - 2;
+      if (c >= 0 && c < C) {
+        if (len(me, c) > 0 && (root < 0 || root == r))
+          S->add(FA_X_SEND, r, result ? FA_B_OUT : FA_B_STRIPE, -1, FA_B_NONE, -1, clo[me][c],
+                 len(me, c), c);
+        if (len(r, c) > 0 && result)
+          S->add(FA_X_RECV, r, FA_B_NONE, -1, FA_B_OUT, -1, clo[r][c], len(r, c), c);
+      }
+    }
+    const int k = j - 1;
+    if (k >= 0 && k < C && len(me, k) > 0)
+      S->add(FA_X_K_STRIPE, -1, FA_B_RECV, -1, result ? FA_B_OUT : FA_B_STRIPE, -1, clo[me][k],
+             len(me, k), k, 0, g.n_total);
     S->next();
   }
+  if (i64 && result)
+    S->add(FA_X_K_TAILS, -1, FA_B_GATHER, -1, FA_B_OUT, -1, 0, 0, -1, 0, g.n_total);
   S->next();
-  if (result && Lme > 0) S->add(FA_X_K_COPY, -1, FA_B_STRIPE, -1, FA_B_OUT, -1, lo[me], Lme);
-  S->next();
-  sched_raw_gather(S, g, 0, false, result);
 }
 
 // Chained: state hops rank to rank, chunk by chunk.
@@ -810,6 +855,7 @@ int make_comm(ncclComm_t nc, int device, fa_comm** out) {
 struct fa_round_plan {
   int mode = 0;  // FA_MODE_*
   int xchg = 0;
+  int req_chunks = 0;       // the column chunk count the plan was built for
   fa_comm* comm = nullptr;  // (may be destroyed before the plan: never read in free_round)
   int device = -1;          // the comm's device, for free_round
   Geo g;
@@ -817,12 +863,16 @@ struct fa_round_plan {
   std::vector<fa_plan*> chunk;
   std::vector<std::pair<int64_t, int64_t>> range;
   float* partial = nullptr;  // e1 partial sums (f32_numel)
-  // e2
+  // e2 (r06: every stripe cut into nchunks column chunks; `chunk` holds this
+  // rank's chunk plans, NULL for an empty chunk)
   std::vector<int64_t> lo;   // nranks + 1 stripe bounds
-  fa_plan* stripe = nullptr;
+  std::vector<std::vector<int64_t>> clo;  // per rank: nchunks + 1 chunk bounds
+  int nchunks = 0;
   int64_t row = 0;           // receive row stride (floats)
   float* recv = nullptr;     // n_total rows
-  float* sbuf = nullptr;     // the reduced stripe
+  float* sbuf = nullptr;     // the reduced stripe (a rank that is not a result rank)
+  float* wstage = nullptr;   // weighted rounds: n_local pre-multiplied buckets
+  std::vector<float> wfull;  // weighted rounds: the stripe kernel's n_total weights
   // chained
   ChainGeo cg;
   float* state = nullptr;    // nplanes * plane floats
@@ -847,7 +897,7 @@ struct fa_round_plan {
   int64_t* i64_gather = nullptr;
   std::vector<const float*> t32_rows;
   std::vector<const int64_t*> i64_rows;
-  std::vector<hipEvent_t> ev;  // start, compute-joins (ring), done
+  std::vector<hipEvent_t> ev;  // start, compute join, done, comm join
   std::map<std::pair<int, int>, std::vector<fa_xfer>> sched;  // (root, weighted) -> ops
   // captured rounds (one process per GPU): the whole schedule of one
   // (root, weights, buffers) call as a HIP graph, replayed by one launch;
@@ -865,6 +915,17 @@ struct fa_round_plan {
   // slots, one fa_reduce call on this plan (no chunks, planes, copies or
   // empty exchanges)
   fa_plan* single = nullptr;
+  // fa_comm_set_profile (r06): event pairs around every group (on the
+  // communication stream) and kernel (on its stream) of the last round, and
+  // around the whole round on the caller's stream
+  struct ProfEv {
+    hipEvent_t a = nullptr, b = nullptr;
+    int kind = 0;   // 0 exchange group, 1 kernel on the comm stream, 2 on the caller's
+  };
+  std::vector<ProfEv> prof;
+  size_t nprof = 0;
+  hipEvent_t prof_t0 = nullptr, prof_t1 = nullptr;
+  bool prof_valid = false;
 };
 
 namespace {
@@ -875,16 +936,21 @@ void free_round(fa_round_plan* p) {
   if (p->device >= 0) (void)hipSetDevice(p->device);
   for (fa_plan* c : p->chunk) fa_plan_destroy(c);
   fa_plan_destroy(p->single);
-  fa_plan_destroy(p->stripe);
   fa_plan_destroy(p->plan64);
   fa_plan_destroy(p->plan_t32);
   void* bufs[] = {p->partial,   p->recv,       p->sbuf,    p->state,     p->fin,
                   p->tidx,      p->t32_stack,  p->t32_gather, p->t32_out, p->i64_stack,
                   p->i64_gather, p->pin,       p->tailp,   p->cont,      p->bsum,
-                  p->blk,       p->relay};
+                  p->blk,       p->relay,      p->wstage};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+  for (auto& pe : p->prof) {
+    if (pe.a) (void)hipEventDestroy(pe.a);
+    if (pe.b) (void)hipEventDestroy(pe.b);
+  }
+  if (p->prof_t0) (void)hipEventDestroy(p->prof_t0);
+  if (p->prof_t1) (void)hipEventDestroy(p->prof_t1);
   for (auto& gr : p->graphs) {
     if (gr.exec) (void)hipGraphExecDestroy(gr.exec);
     if (gr.graph) (void)hipGraphDestroy(gr.graph);
@@ -903,10 +969,25 @@ int build_round(fa_round_plan* p, int nchunks, std::vector<fa_tile_desc>* vec_ou
   if (p->mode == FA_MODE_SHARDED) {
     shard_ranges(g, nchunks, cut_out, &p->range);
   } else if (p->mode == FA_MODE_STRIPED) {
+    // stripes, then each stripe's tiles cut into nchunks column chunks
     std::vector<size_t> cut;
     cut_tiles(g.t32, g.nranks, &cut);
     p->lo = cut_bounds(g.t32, cut, g.f32_numel);
-    *cut_out = cut;
+    p->nchunks = nchunks;
+    p->clo.assign(g.nranks, std::vector<int64_t>());
+    cut_out->clear();
+    for (int r = 0; r < g.nranks; ++r) {
+      const std::vector<fa_tile_desc> sub(g.t32.begin() + cut[r], g.t32.begin() + cut[r + 1]);
+      std::vector<size_t> sc;
+      cut_tiles(sub, nchunks, &sc);
+      std::vector<int64_t>& b = p->clo[r];
+      b.assign(nchunks + 1, p->lo[r + 1]);
+      b[0] = p->lo[r];
+      for (int c = 1; c < nchunks; ++c)
+        if (sc[c] < sub.size()) b[c] = sub[sc[c]].start;
+      if (r == g.rank)   // this rank's chunk c = tiles [cut_out[c], cut_out[c + 1])
+        for (size_t c = 0; c <= (size_t)nchunks; ++c) cut_out->push_back(cut[r] + sc[c]);
+    }
   } else if (p->mode == FA_MODE_CHAINED) {
     chain_geo(g, nchunks, &p->cg, vec_out, cut_out, tails_out, tidx_out);
     p->range = p->cg.range;
@@ -930,7 +1011,7 @@ int make_round(fa_comm* comm, int mode, const fa_seg* seg32, int nseg32, int64_t
   if (!out) return set_err(FA_E_INVAL, "%s: out is NULL", who);
   *out = nullptr;
   if (!comm || !counts) return set_err(FA_E_INVAL, "%s: NULL comm/counts", who);
-  if (nchunks == 0) nchunks = 8;
+  if (nchunks == 0) nchunks = mode == FA_MODE_STRIPED ? kStripeChunks : 8;
   if (nchunks < 1 || nchunks > FA_COMM_MAX_CHUNKS)
     return set_err(FA_E_INVAL, "%s: nchunks=%d", who, nchunks);
   if (xchg != FA_XCHG_REDUCE && xchg != FA_XCHG_RS_GATHER)
@@ -938,6 +1019,7 @@ int make_round(fa_comm* comm, int mode, const fa_seg* seg32, int nseg32, int64_t
   fa_round_plan* p = new fa_round_plan();
   p->mode = mode;
   p->xchg = xchg;
+  p->req_chunks = nchunks;
   p->comm = comm;
   p->device = comm->device;
   int rc = make_geo(comm->nranks, comm->rank, counts, seg32, nseg32, f32_numel, seg64, nseg64,
@@ -986,16 +1068,24 @@ int make_round(fa_comm* comm, int mode, const fa_seg* seg32, int nseg32, int64_t
   } else if (mode == FA_MODE_STRIPED) {
     const int me = g.rank;
     const int64_t L = p->lo[me + 1] - p->lo[me];
-    if (cut[me] < cut[me + 1]) {
-      rc = fa_plan_create_from_tiles(g.t32.data() + cut[me], (int)(cut[me + 1] - cut[me]),
-                                     f32_numel, i64_numel, 0, flags, &p->stripe);
-      if (rc) return fail(rc);
+    // cut: this rank's chunk c = tiles [cut[c], cut[c + 1]) (build_round)
+    for (int c = 0; c < p->nchunks; ++c) {
+      fa_plan* sub = nullptr;
+      if (cut[c] < cut[c + 1]) {
+        rc = fa_plan_create_from_tiles(g.t32.data() + cut[c], (int)(cut[c + 1] - cut[c]),
+                                       f32_numel, i64_numel, 0, flags, &sub);
+        if (rc) return fail(rc);
+      }
+      p->chunk.push_back(sub);
+    }
+    if (L > 0) {
       // one row per client slot, 256-B aligned; the stripe starts on a
       // 64-float boundary, so (row - lo) keeps the 16-B alignment
       p->row = (L + 63) / 64 * 64;
       if ((rc = alloc((void**)&p->recv, (size_t)g.n_total * p->row * 4, false))) return fail(rc);
       if ((rc = alloc((void**)&p->sbuf, (size_t)p->row * 4, true))) return fail(rc);
     }
+    p->plane = (f32_numel + 63) / 64 * 64;   // WSTAGE row stride (allocated by a weighted round)
   } else {
     for (size_t c = 0; c + 1 < cut.size(); ++c) {
       fa_plan* sub = nullptr;
@@ -1057,7 +1147,7 @@ int make_round(fa_comm* comm, int mode, const fa_seg* seg32, int nseg32, int64_t
       for (int j = 0; j < g.counts[r]; ++j)
         p->i64_rows.push_back(p->i64_gather + ((size_t)r * g.nmax + j) * i64_numel);
   }
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 4; ++i) {   // start, compute join, done, comm join (striped)
     hipEvent_t e;
     he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
     if (he != hipSuccess) return fail(set_err(FA_E_HIP, "%s: %s", who, hipGetErrorString(he)));
@@ -1073,7 +1163,7 @@ const std::vector<fa_xfer>& schedule(fa_round_plan* p, int root, bool weighted) 
   if (it != p->sched.end()) return it->second;
   Sched S;
   if (p->mode == FA_MODE_SHARDED) sched_sharded(p->g, p->range, p->xchg, root, weighted, &S);
-  else if (p->mode == FA_MODE_STRIPED) sched_striped(p->g, p->lo, root, &S);
+  else if (p->mode == FA_MODE_STRIPED) sched_striped(p->g, p->clo, root, weighted, &S);
   else if (p->mode == FA_MODE_CHAINED) sched_chained(p->g, p->cg, root, &S);
   else sched_blocked(p->g, p->cg, p->bg, root, &S);
   return p->sched[key] = S.ops;
@@ -1126,6 +1216,7 @@ void* addr(Local& L, int buf, int index, int64_t off) {
     case FA_B_BSUM: return p->bsum + (size_t)index * p->plane + off;
     case FA_B_BLK: return p->blk + (size_t)index * p->bg.row + (off - p->bg.slo[p->g.rank]);
     case FA_B_RELAY: return p->relay + (size_t)index * p->bg.row + (off - p->bg.slo[p->g.rank]);
+    case FA_B_WSTAGE: return p->wstage + (size_t)index * p->plane + off;
     default: return nullptr;
   }
 }
@@ -1137,11 +1228,22 @@ bool on_comm_stream(const fa_xfer& x) {
     case FA_X_K_ZERO:
     case FA_X_K_STACK:
     case FA_X_K_PART:                                // (the zero planes of PIN only)
-    case FA_X_K_BLOCK: return false;                 // read local inputs only
+    case FA_X_K_BLOCK:
+    case FA_X_K_SCALE: return false;                 // read local inputs only
+    case FA_X_K_STRIPE: return false;                // reads_exchanged: joined below
     case FA_X_K_CHAIN: return x.src == FA_B_STATE;   // after the state's hop
     default: return true;                            // read exchanged data
   }
 }
+
+// A compute-stream kernel that reads data exchanged in EARLIER steps (r06:
+// the striped round's chunk reduce, beside the next chunk's exchange).  The
+// executor records the communication stream's position at the start of the
+// step — after the previous steps' groups, before this step's — and the
+// caller's stream waits for it before the kernel, so the kernel overlaps
+// this step's group.  A schedule must not give such a kernel data its own
+// step's group writes (tests/schedsim.py checks it).
+bool reads_exchanged(const fa_xfer& x) { return x.op == FA_X_K_STRIPE; }
 
 // Buffers that kernels on the caller's (compute) stream write: partial sums,
 // stacked raw columns, the blocked mode's outgoing partial and local block
@@ -1153,7 +1255,8 @@ bool on_comm_stream(const fa_xfer& x) {
 // kernel reads or writes (received planes and stripes are comm-side only).
 bool user_written(int b) {
   return b == FA_B_PARTIAL || b == FA_B_STACK || b == FA_B_TAILP || b == FA_B_BSUM ||
-         b == FA_B_STATE || b == FA_B_OUT || b == FA_B_FIN;
+         b == FA_B_STATE || b == FA_B_OUT || b == FA_B_FIN || b == FA_B_STRIPE ||
+         b == FA_B_WSTAGE;
 }
 bool needs_compute(const fa_xfer& x) { return user_written(x.src); }
 
@@ -1251,13 +1354,46 @@ int issue_local(Local& L, const fa_xfer& x, hipStream_t s) {
       }
       return FA_OK;
     case FA_X_K_STRIPE: {
+      // chunk x.chunk of this rank's stripe over all n_total clients: the
+      // local clients from their buckets, the others from their receive
+      // rows; written straight into the result bucket on a result rank
+      fa_plan* cp = p->chunk[x.chunk];
+      if (!cp) return FA_OK;
       L.src.assign(p->g.n_total, nullptr);
       for (int k = 0; k < g.n_total; ++k)
         L.src[k] = p->recv + (size_t)k * p->row - p->lo[g.rank];  // element e at [e - lo]
       for (int j = 0; j < g.n_local; ++j) L.src[g.lo_slot + j] = io->c32[j];
+      const float* w = nullptr;
+      if (io->weights) {   // received rows come pre-multiplied: weight 1
+        p->wfull.assign(g.n_total, 1.0f);
+        for (int j = 0; j < g.n_local; ++j) p->wfull[g.lo_slot + j] = io->weights[j];
+        w = p->wfull.data();
+      }
       void* tab = g.n_total > FA_INLINE_CLIENTS ? take_table(L) : nullptr;
-      return fa_reduce_tab(p->stripe, L.src.data(), nullptr, g.n_total, nullptr, tab,
-                           p->sbuf - p->lo[g.rank], nullptr, 0, s);
+      float* out = x.dst == FA_B_OUT ? io->out32 : p->sbuf - p->lo[g.rank];
+      return fa_reduce_tab(cp, L.src.data(), nullptr, g.n_total, w, tab, out, nullptr, 0, s);
+    }
+    case FA_X_K_SCALE: {
+      for (int j0 = 0; j0 < x.nrows; j0 += kStackPtrs) {
+        ScaleArgs a;
+        memset(&a, 0, sizeof a);
+        a.rows = std::min(kStackPtrs, x.nrows - j0);
+        bool al = ((uintptr_t)(p->wstage + x.offset) & 15u) == 0 && (p->plane & 3) == 0;
+        for (int j = 0; j < a.rows; ++j) {
+          a.src[j] = io->c32[j0 + j];
+          a.w[j] = io->weights[j0 + j];
+          al = al && ((uintptr_t)(io->c32[j0 + j] + x.offset) & 15u) == 0;
+        }
+        a.dst = p->wstage + (size_t)j0 * p->plane;
+        a.plane = p->plane;
+        a.off = x.offset;
+        a.count = x.count;
+        a.vec = al ? 1 : 0;
+        const int gx = (int)std::min<int64_t>(1024, (x.count / 4 + 255) / 256 + 1);
+        hipLaunchKernelGGL(scale_rows_kernel, dim3(gx, a.rows), dim3(256), 0, s, a);
+        FA_HIP_TRY(hipGetLastError());
+      }
+      return FA_OK;
     }
     case FA_X_K_CHAIN: {
       fa_chain ch;
@@ -1350,6 +1486,19 @@ int issue_local(Local& L, const fa_xfer& x, hipStream_t s) {
   }
 }
 
+// The next profiling event pair of a plan's round (fa_comm_set_profile).
+int prof_pair(fa_round_plan* p, int kind, fa_round_plan::ProfEv** out) {
+  if (p->nprof == p->prof.size()) {
+    fa_round_plan::ProfEv e;
+    FA_HIP_TRY(hipEventCreate(&e.a));
+    FA_HIP_TRY(hipEventCreate(&e.b));
+    p->prof.push_back(e);
+  }
+  *out = &p->prof[p->nprof++];
+  (*out)->kind = kind;
+  return FA_OK;
+}
+
 // Walk the local GPUs' schedules step by step: one RCCL group per step over
 // every local GPU's exchanges, then the step's kernels.
 int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_xfer>*>& scheds) {
@@ -1358,6 +1507,13 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
   for (size_t d = 0; d < nl; ++d) {
     fa_round_plan* p = locals[d].p;
     FA_HIP_TRY(hipSetDevice(p->comm->device));
+    if (p->comm->profile) {
+      if (!p->prof_t0) FA_HIP_TRY(hipEventCreate(&p->prof_t0));
+      if (!p->prof_t1) FA_HIP_TRY(hipEventCreate(&p->prof_t1));
+      p->nprof = 0;
+      p->prof_valid = false;
+      FA_HIP_TRY(hipEventRecord(p->prof_t0, locals[d].user));
+    }
     // the inputs are ready on the caller's stream
     FA_HIP_TRY(hipEventRecord(p->ev[0], locals[d].user));
     FA_HIP_TRY(hipStreamWaitEvent(p->comm->cs, p->ev[0], 0));
@@ -1366,7 +1522,7 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
   int step = 0;
   for (;;) {
     bool any = false, comm = false;
-    std::vector<char> join(nl, 0);
+    std::vector<char> join(nl, 0), xread(nl, 0);
     for (size_t d = 0; d < nl; ++d) {
       const std::vector<fa_xfer>& o = *scheds[d];
       for (size_t i = pos[d]; i < o.size() && o[i].step == step; ++i) {
@@ -1375,10 +1531,18 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
           comm = true;
           join[d] |= needs_compute(o[i]);
         }
+        xread[d] |= reads_exchanged(o[i]);
       }
       if (pos[d] < o.size()) any = true;
     }
     if (!any) break;
+    // the communication stream's position before this step's group: what a
+    // compute-stream kernel reading earlier steps' exchanges waits for
+    for (size_t d = 0; d < nl; ++d) {
+      if (!xread[d]) continue;
+      FA_HIP_TRY(hipSetDevice(locals[d].p->comm->device));
+      FA_HIP_TRY(hipEventRecord(locals[d].p->ev[3], locals[d].p->comm->cs));
+    }
     // comm stream joins the compute stream before this step's exchanges when
     // one of them reads compute-stream output
     if (comm) {
@@ -1389,6 +1553,19 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
         FA_HIP_TRY(hipEventRecord(L.p->ev[1], L.user));
         FA_HIP_TRY(hipStreamWaitEvent(L.p->comm->cs, L.p->ev[1], 0));
         L.comp_dirty = false;
+      }
+      std::vector<fa_round_plan::ProfEv*> gev(nl, nullptr);
+      for (size_t d = 0; d < nl; ++d) {
+        fa_round_plan* p = locals[d].p;
+        if (!p->comm->profile) continue;
+        bool has = false;
+        for (size_t i = pos[d]; i < scheds[d]->size() && (*scheds[d])[i].step == step; ++i)
+          has |= is_comm((*scheds[d])[i].op);
+        if (!has) continue;
+        FA_HIP_TRY(hipSetDevice(p->comm->device));
+        const int rc = prof_pair(p, 0, &gev[d]);
+        if (rc) return rc;
+        FA_HIP_TRY(hipEventRecord(gev[d]->a, p->comm->cs));
       }
       NCCL_TRY(ncclGroupStart());
       for (size_t d = 0; d < nl; ++d) {
@@ -1404,6 +1581,11 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
         }
       }
       NCCL_TRY(ncclGroupEnd());
+      for (size_t d = 0; d < nl; ++d) {
+        if (!gev[d]) continue;
+        FA_HIP_TRY(hipSetDevice(locals[d].p->comm->device));
+        FA_HIP_TRY(hipEventRecord(gev[d]->b, locals[d].p->comm->cs));
+      }
     }
     for (size_t d = 0; d < nl; ++d) {
       Local& L = locals[d];
@@ -1418,8 +1600,17 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
           FA_HIP_TRY(hipStreamWaitEvent(L.p->comm->cs, L.p->ev[1], 0));
           L.comp_dirty = false;
         }
-        const int rc = issue_local(L, x, cs ? L.p->comm->cs : L.user);
+        if (!cs && reads_exchanged(x)) FA_HIP_TRY(hipStreamWaitEvent(L.user, L.p->ev[3], 0));
+        const hipStream_t ks = cs ? L.p->comm->cs : L.user;
+        fa_round_plan::ProfEv* kev = nullptr;
+        if (L.p->comm->profile) {
+          const int prc = prof_pair(L.p, cs ? 1 : 2, &kev);
+          if (prc) return prc;
+          FA_HIP_TRY(hipEventRecord(kev->a, ks));
+        }
+        const int rc = issue_local(L, x, ks);
         if (rc) return rc;
+        if (kev) FA_HIP_TRY(hipEventRecord(kev->b, ks));
         if (!cs) L.comp_dirty = true;
       }
     }
@@ -1431,6 +1622,10 @@ int execute(std::vector<Local>& locals, const std::vector<const std::vector<fa_x
     FA_HIP_TRY(hipSetDevice(L.p->comm->device));
     FA_HIP_TRY(hipEventRecord(L.p->ev[2], L.p->comm->cs));
     FA_HIP_TRY(hipStreamWaitEvent(L.user, L.p->ev[2], 0));
+    if (L.p->comm->profile) {
+      FA_HIP_TRY(hipEventRecord(L.p->prof_t1, L.user));
+      L.p->prof_valid = true;
+    }
   }
   return FA_OK;
 }
@@ -1582,8 +1777,6 @@ int run_round(fa_round_plan* const* plans, int nlocal, const fa_shard_io* io, in
     if (root >= p->comm->nranks) return set_err(FA_E_INVAL, "%s: root=%d", who, root);
     if ((io[d].weights != nullptr) != weighted)
       return set_err(FA_E_INVAL, "%s: weights on some GPUs only", who);
-    if (weighted && mode == FA_MODE_STRIPED)
-      return set_err(FA_E_INVAL, "%s: the striped mode takes no weights", who);
     const Geo& g = p->g;
     const bool result = root < 0 || root == g.rank;
     if (g.n_local > 0 && !io[d].c32)
@@ -1603,6 +1796,14 @@ int run_round(fa_round_plan* const* plans, int nlocal, const fa_shard_io* io, in
       return fa_reduce(p->single, io[d].c32, io[d].c64, g.n_total, io[d].weights, io[d].out32,
                        io[d].out64, 0, io[d].stream);
     }
+    if (weighted && mode == FA_MODE_STRIPED && !p->wstage && g.n_local > 0) {
+      // the first weighted round: the staging buckets of the pre-multiplied
+      // client rows (before any capture: no allocation inside a graph)
+      DeviceGuard dg2;
+      FA_HIP_TRY(hipSetDevice(p->device));
+      const int rc = alloc((void**)&p->wstage, (size_t)g.n_local * p->plane * 4, false);
+      if (rc) return rc;
+    }
     Local L;
     L.p = p;
     L.io = &io[d];
@@ -1612,11 +1813,285 @@ int run_round(fa_round_plan* const* plans, int nlocal, const fa_shard_io* io, in
     scheds.push_back(&schedule(p, root, weighted));
   }
   DeviceGuard dg;
-  if (nlocal == 1 && plans[0]->comm->graphs && !plans[0]->graph_failed) {
+  if (nlocal == 1 && plans[0]->comm->graphs && !plans[0]->graph_failed &&
+      !plans[0]->comm->profile) {
     int rc = FA_OK;
     if (replay_graph(locals[0], *scheds[0], root, weighted, &rc)) return rc;
   }
   return execute(locals, scheds);
+}
+
+// ============================================================ cost model ==
+// (r06; fedagg_comm.h fa_round_model.)  Every
+// rank's schedule replayed in virtual time under the executor's stream rules
+// (execute above): per rank the communication stream (tc) and the caller's
+// stream (tu).  tests/roundmodel.py restates it and checks it against this.
+inline double us_link(double bytes) { return bytes / (FA_MODEL_LINK_GBPS * 1e3); }
+inline double us_hbm(double bytes) { return bytes / (FA_MODEL_HBM_GBPS * 1e3); }
+
+int popc(unsigned v) { return __builtin_popcount(v); }
+
+// HBM bytes a kernel op reads and writes (the columns it covers; count 0 =
+// the vector columns, V elements); the scalar-column stacks and their
+// reductions are a few KB and cost only their launch.
+double kernel_bytes(const fa_xfer& x, int n_total, int64_t V) {
+  const double b = 4.0 * (double)(x.count > 0 ? x.count : V);
+  switch (x.op) {
+    case FA_X_K_SUM:
+    case FA_X_K_STRIPE:
+    case FA_X_K_FOLD:
+    case FA_X_K_PART:
+    case FA_X_K_BLOCK: return (x.nrows + 1) * b;
+    case FA_X_K_CONT: return (x.nrows + 2) * b;
+    case FA_X_K_CHAIN: {
+      const int lin = x.src == FA_B_STATE ? popc(fa_chain_levels(x.row0, n_total)) : 0;
+      const int lout = x.dst == FA_B_STATE ? popc(fa_chain_levels(x.row0 + x.nrows, n_total)) : 1;
+      return (x.nrows + lin + std::max(lout, 1)) * b;
+    }
+    case FA_X_K_COPY: return x.dst == FA_B_BLK ? 0.0 : 2 * b;
+    case FA_X_K_DIV: return 2 * b;
+    case FA_X_K_ZERO: return b;
+    case FA_X_K_SCALE: return 2.0 * x.nrows * b;
+    default: return 0.0;   // K_STACK, K_TAILS
+  }
+}
+
+double elem_bytes(const fa_xfer& x) {
+  const int buf = x.op == FA_X_RECV ? x.dst : x.src;
+  const int idx = x.op == FA_X_RECV ? x.dst_index : x.src_index;
+  return dtype_of(buf, idx) == ncclInt64 ? 8.0 : 4.0;
+}
+
+// A collective's bytes on each link direction of a rank (ring algorithms).
+double coll_link_bytes(const fa_xfer& x, int W) {
+  const double es = elem_bytes(x), n = (double)x.count * es;
+  switch (x.op) {
+    case FA_X_ALLGATHER:
+      return x.src == FA_B_PARTIAL ? n * (W - 1) / W : n * (W - 1);
+    case FA_X_BCAST: return n;
+    case FA_X_ALLREDUCE: return 2.0 * n * (W - 1) / W;
+    default: return n * (W - 1) / W;   // REDUCE, REDUCE_SCATTER, GATHER
+  }
+}
+
+int model_schedules(const std::vector<std::vector<fa_xfer>>& sch, int n_total, int64_t V,
+                    fa_round_cost* out) {
+  const int W = (int)sch.size();
+  std::vector<size_t> pos(W, 0);
+  std::vector<char> posted(W, 0);
+  std::vector<double> tc(W, 0.0), tu(W, 0.0), post(W, 0.0), ev3(W, 0.0);
+  std::vector<double> hbm(W, 0.0);
+  std::vector<std::vector<double>> lout(W, std::vector<double>(W, 0.0)),
+      lin(W, std::vector<double>(W, 0.0));
+  std::vector<int> groups(W, 0);
+  // p2p matching: the post times of each channel's sends / receives in order
+  std::map<std::pair<int, int>, std::vector<double>> sendt, recvt;
+  std::map<uint64_t, std::vector<double>> collt;
+  std::vector<uint64_t> cseq(W, 0);
+  struct Pend {
+    std::vector<std::pair<int, size_t>> p2p;  // (op index, channel position)
+    std::vector<uint64_t> coll;
+  };
+  std::vector<Pend> pend(W);
+  int steps = 0;
+  for (;;) {
+    bool progress = false, done = true;
+    for (int r = 0; r < W; ++r) {
+      const std::vector<fa_xfer>& o = sch[r];
+      if (pos[r] >= o.size()) continue;
+      done = false;
+      const int step = o[pos[r]].step;
+      size_t e = pos[r];
+      while (e < o.size() && o[e].step == step) ++e;
+      steps = std::max(steps, step + 1);
+      if (!posted[r]) {
+        ev3[r] = tc[r];
+        bool join = false, comm = false;
+        for (size_t i = pos[r]; i < e; ++i)
+          if (is_comm(o[i].op)) {
+            comm = true;
+            join |= needs_compute(o[i]);
+          }
+        if (join) tc[r] = std::max(tc[r], tu[r]);
+        post[r] = tc[r];
+        pend[r] = Pend();
+        for (size_t i = pos[r]; i < e; ++i) {
+          const fa_xfer& x = o[i];
+          if (x.op == FA_X_SEND) {
+            auto& v = sendt[{r, x.peer}];
+            pend[r].p2p.push_back({(int)i, v.size()});
+            v.push_back(post[r]);
+          } else if (x.op == FA_X_RECV) {
+            auto& v = recvt[{x.peer, r}];
+            pend[r].p2p.push_back({(int)i, v.size()});
+            v.push_back(post[r]);
+          } else if (is_comm(x.op)) {
+            const uint64_t q = cseq[r]++;
+            auto& v = collt[q];
+            if (v.empty()) v.assign(W, -1.0);
+            v[r] = post[r];
+            pend[r].coll.push_back(q);
+          }
+        }
+        if (comm) ++groups[r];
+        posted[r] = 1;
+        progress = true;
+      }
+      // complete once every peer has posted the matching operations
+      double start = post[r];
+      bool ok = true;
+      for (const auto& pe : pend[r].p2p) {
+        const fa_xfer& x = o[pe.first];
+        const auto& v = x.op == FA_X_SEND ? recvt[{r, x.peer}] : sendt[{x.peer, r}];
+        if (v.size() <= pe.second) {
+          ok = false;
+          break;
+        }
+        start = std::max(start, v[pe.second]);
+      }
+      for (uint64_t q : pend[r].coll) {
+        if (!ok) break;
+        for (double t : collt[q]) {
+          if (t < 0) {
+            ok = false;
+            break;
+          }
+          start = std::max(start, t);
+        }
+      }
+      if (!ok) continue;
+      // the group
+      std::vector<double> go(W, 0.0), gi(W, 0.0);
+      double ghbm = 0.0, gcoll = 0.0;
+      bool comm = false;
+      for (size_t i = pos[r]; i < e; ++i) {
+        const fa_xfer& x = o[i];
+        if (!is_comm(x.op)) continue;
+        comm = true;
+        if (x.op == FA_X_SEND || x.op == FA_X_RECV) {
+          const double b = (double)x.count * elem_bytes(x);
+          (x.op == FA_X_SEND ? go : gi)[x.peer] += b;
+          (x.op == FA_X_SEND ? lout : lin)[r][x.peer] += b;
+          ghbm += b;
+        } else {
+          const double b = coll_link_bytes(x, W);
+          gcoll += b;
+          ghbm += 2.0 * b;
+        }
+      }
+      if (comm) {
+        double link = gcoll;
+        for (int q = 0; q < W; ++q) link = std::max(link, std::max(go[q], gi[q]));
+        tc[r] = start + FA_MODEL_GROUP_US + std::max(us_link(link), us_hbm(ghbm));
+        hbm[r] += ghbm;
+      }
+      // the kernels
+      for (size_t i = pos[r]; i < e; ++i) {
+        const fa_xfer& x = o[i];
+        if (is_comm(x.op)) continue;
+        const double kb = kernel_bytes(x, n_total, V);
+        const double dur = FA_MODEL_KERNEL_US + us_hbm(kb);
+        hbm[r] += kb;
+        if (on_comm_stream(x)) {
+          if (needs_compute(x)) tc[r] = std::max(tc[r], tu[r]);
+          tc[r] += dur;
+        } else {
+          if (reads_exchanged(x)) tu[r] = std::max(tu[r], ev3[r]);
+          tu[r] += dur;
+        }
+      }
+      pos[r] = e;
+      posted[r] = 0;
+      progress = true;
+    }
+    if (done) break;
+    if (!progress) return set_err(FA_E_INVAL, "fa_round_model: the schedules deadlock");
+  }
+  fa_round_cost c{};
+  for (int r = 0; r < W; ++r) {
+    c.model_us = std::max(c.model_us, std::max(tc[r], tu[r]));
+    c.hbm_bytes_max = std::max(c.hbm_bytes_max, hbm[r]);
+    for (int q = 0; q < W; ++q)
+      c.link_bytes_max = std::max(c.link_bytes_max, std::max(lout[r][q], lin[r][q]));
+    c.groups = std::max(c.groups, groups[r]);
+  }
+  c.steps = steps;
+  *out = c;
+  return FA_OK;
+}
+
+// Every rank's schedule of a form (host only), from one geometry.
+int all_schedules(const Geo& base, int mode, int nchunks, int xchg, int root, bool weighted,
+                  std::vector<std::vector<fa_xfer>>* sch, int64_t* V) {
+  sch->assign(base.nranks, {});
+  *V = 0;
+  for (const fa_tile_desc& t : base.t32)
+    if (t.kind == 0) *V += t.count;
+  for (int r = 0; r < base.nranks; ++r) {
+    fa_round_plan p;
+    p.mode = mode;
+    p.xchg = xchg;
+    p.req_chunks = nchunks;
+    p.g = base;
+    p.g.rank = r;
+    p.g.n_local = base.counts[r];
+    p.g.lo_slot = base.first[r];
+    std::vector<fa_tile_desc> vec, tails;
+    std::vector<size_t> cut;
+    std::vector<int64_t> tidx;
+    const int rc = build_round(&p, nchunks, &vec, &cut, &tails, &tidx);
+    if (rc) return rc;
+    (*sch)[r] = schedule(&p, root, weighted);
+  }
+  return FA_OK;
+}
+
+// The default entry's choice (fa_multi_select_layout): the exact form and
+// chunk count with the lowest modelled time; ties keep the earlier candidate
+// (blocked, then chained, then striped, fewer chunks first).
+int select_form(const Geo& base, unsigned mflags, int* mode, int* nchunks, double* us) {
+  if (mflags & FA_MULTI_REASSOCIATE) {
+    *mode = FA_MODE_SHARDED;
+    *nchunks = 8;
+    if (us) *us = -1.0;
+    return FA_OK;
+  }
+  if (base.nranks == 1) {   // every form is the plain reduction (make_round)
+    *mode = first_wide_block(1, base.counts.data(), nullptr, nullptr) < 0 ? FA_MODE_BLOCKED
+                                                                         : FA_MODE_CHAINED;
+    *nchunks = 1;
+    if (us) *us = -1.0;
+    return FA_OK;
+  }
+  int root = -1;
+  if (!(mflags & FA_MULTI_ROOT_ALL))
+    for (int r = 0; r < base.nranks; ++r)
+      if (base.counts[r] > 0) root = r;
+  struct Cand {
+    int mode, nchunks;
+  };
+  std::vector<Cand> cand;
+  if (first_wide_block(base.nranks, base.counts.data(), nullptr, nullptr) < 0)
+    cand.push_back({FA_MODE_BLOCKED, 1});
+  for (int c : {4, 8, 16, 32}) cand.push_back({FA_MODE_CHAINED, c});
+  for (int c : {1, 2, 4, 8}) cand.push_back({FA_MODE_STRIPED, c});
+  double best = 0.0;
+  *mode = -1;
+  for (const Cand& k : cand) {
+    std::vector<std::vector<fa_xfer>> sch;
+    int64_t V = 0;
+    int rc = all_schedules(base, k.mode, k.nchunks, FA_XCHG_REDUCE, root, false, &sch, &V);
+    if (rc) return rc;
+    fa_round_cost c{};
+    if ((rc = model_schedules(sch, base.n_total, V, &c))) return rc;
+    if (*mode < 0 || c.model_us < best) {
+      best = c.model_us;
+      *mode = k.mode;
+      *nchunks = k.nchunks;
+    }
+  }
+  if (us) *us = best;
+  return FA_OK;
 }
 
 // fa_mean_f32_multi's shard plans, by (communicator, layout, counts); a
@@ -1701,6 +2176,37 @@ int fa_comm_set_graphs(fa_comm* c, int enable) {
   return FA_OK;
 }
 
+int fa_comm_set_profile(fa_comm* c, int enable) {
+  if (!c) return set_err(FA_E_INVAL, "fa_comm_set_profile: NULL comm");
+  c->profile = enable != 0;
+  return FA_OK;
+}
+
+int fa_round_plan_profile(const void* plan, fa_round_profile* out) {
+  if (!plan || !out) return set_err(FA_E_INVAL, "fa_round_plan_profile: NULL argument");
+  const fa_round_plan* p = (const fa_round_plan*)plan;
+  memset(out, 0, sizeof *out);
+  if (!p->prof_valid) return set_err(FA_E_INVAL, "fa_round_plan_profile: no profiled round");
+  DeviceGuard dg;
+  FA_HIP_TRY(hipSetDevice(p->device));
+  FA_HIP_TRY(hipEventSynchronize(p->prof_t1));
+  float ms = 0.f;
+  FA_HIP_TRY(hipEventElapsedTime(&ms, p->prof_t0, p->prof_t1));
+  out->wall_us = 1e3 * ms;
+  for (size_t i = 0; i < p->nprof; ++i) {
+    const fa_round_plan::ProfEv& e = p->prof[i];
+    FA_HIP_TRY(hipEventElapsedTime(&ms, e.a, e.b));
+    if (e.kind == 0) {
+      out->exchange_us += 1e3 * ms;
+      ++out->groups;
+    } else {
+      (e.kind == 1 ? out->comm_kernel_us : out->compute_kernel_us) += 1e3 * ms;
+      ++out->kernels;
+    }
+  }
+  return FA_OK;
+}
+
 int fa_comm_info(const fa_comm* c, int* nranks, int* rank, int* device) {
   if (!c) return set_err(FA_E_INVAL, "fa_comm_info: comm is NULL");
   if (nranks) *nranks = c->nranks;
@@ -1735,27 +2241,34 @@ int fa_reduce_sharded(fa_shard_plan* const* plans, int nlocal, const fa_shard_io
                    "fa_reduce_sharded");
 }
 
-// ======================================================= default (r05) ====
-// The default multi-GPU entry: the exact round the counts allow (blocked if
-// every cascade block lies on at most two ranks, else chained); e1 only on
-// request (FA_MULTI_REASSOCIATE).
+// ================================================ default (r05, r06) ====
+// The default multi-GPU entry: the exact form and chunk count with the lowest
+// modelled time (select_form; r05: blocked if every cascade block lies on at
+// most two ranks, else chained); e1 only on request (FA_MULTI_REASSOCIATE).
+int fa_multi_select_layout(int nranks, const int* counts, const fa_seg* seg32, int nseg32,
+                           int64_t f32_numel, const fa_seg* seg64, int nseg64, int64_t i64_numel,
+                           unsigned flags, unsigned mflags, int* mode, int* nchunks,
+                           double* model_us) {
+  if (!mode || !nchunks) return set_err(FA_E_INVAL, "fa_multi_select: mode/nchunks is NULL");
+  *mode = -1;
+  *nchunks = 0;
+  if (nranks < 1 || !counts) return set_err(FA_E_INVAL, "fa_multi_select: bad arguments");
+  if (mflags & ~(unsigned)(FA_MULTI_REASSOCIATE | FA_MULTI_ROOT_ALL))
+    return set_err(FA_E_INVAL, "fa_multi_select: unknown flags 0x%x", mflags);
+  Geo g;
+  const int rc = make_geo(nranks, 0, counts, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel,
+                          flags, "fa_multi_select", &g);
+  if (rc) return rc;
+  return select_form(g, mflags, mode, nchunks, model_us);
+}
+
 int fa_multi_select(int nranks, const int* counts, unsigned mflags, int* mode) {
   if (!mode) return set_err(FA_E_INVAL, "fa_multi_select: mode is NULL");
-  *mode = -1;
-  if (nranks < 1 || !counts) return set_err(FA_E_INVAL, "fa_multi_select: bad arguments");
-  if (mflags & ~(unsigned)FA_MULTI_REASSOCIATE)
-    return set_err(FA_E_INVAL, "fa_multi_select: unknown flags 0x%x", mflags);
-  int n = 0;
-  for (int r = 0; r < nranks; ++r) {
-    if (counts[r] < 0) return set_err(FA_E_INVAL, "fa_multi_select: counts[%d]=%d", r, counts[r]);
-    n += counts[r];
-  }
-  if (n < 1 || n > FA_MAX_CLIENTS)
-    return set_err(FA_E_RANGE, "fa_multi_select: %d clients in total", n);
-  if (mflags & FA_MULTI_REASSOCIATE) *mode = FA_MODE_SHARDED;
-  else *mode = first_wide_block(nranks, counts, nullptr, nullptr) < 0 ? FA_MODE_BLOCKED
-                                                                      : FA_MODE_CHAINED;
-  return FA_OK;
+  // the nominal layout: one fp32 tensor of 2^24 elements
+  const fa_seg seg{0, (int64_t)1 << 24};
+  int nchunks = 0;
+  return fa_multi_select_layout(nranks, counts, &seg, 1, seg.numel, nullptr, 0, 0,
+                                FA_PLAN_GAPS_ARE_PADDING, mflags, mode, &nchunks, nullptr);
 }
 
 int fa_multi_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
@@ -1764,14 +2277,21 @@ int fa_multi_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t
   if (!out) return set_err(FA_E_INVAL, "fa_multi_plan_create: out is NULL");
   *out = nullptr;
   if (!comm) return set_err(FA_E_INVAL, "fa_multi_plan_create: NULL comm");
-  int mode = -1;
-  int rc = fa_multi_select(comm->nranks, counts, mflags, &mode);
+  int mode = -1, best = 0;
+  int rc = fa_multi_select_layout(comm->nranks, counts, seg32, nseg32, f32_numel, seg64, nseg64,
+                                  i64_numel, flags, mflags, &mode, &best, nullptr);
   if (rc) return rc;
-  if (nchunks == 0) nchunks = mode == FA_MODE_CHAINED ? 16 : 8;
+  if (nchunks == 0) nchunks = best;
   if (mode == FA_MODE_BLOCKED) nchunks = 1;
   return make_round(comm, mode, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, counts,
                     nchunks, FA_XCHG_REDUCE, flags, "fa_multi_plan_create",
                     (fa_round_plan**)out);
+}
+
+int fa_multi_plan_chunks(const fa_multi_plan* plan, int* nchunks) {
+  if (!plan || !nchunks) return set_err(FA_E_INVAL, "fa_multi_plan_chunks: NULL argument");
+  *nchunks = ((const fa_round_plan*)plan)->req_chunks;
+  return FA_OK;
 }
 
 int fa_multi_plan_mode(const fa_multi_plan* plan, int* mode) {
@@ -1834,8 +2354,15 @@ int fa_mean_f32_multi_ex(fa_comm* comm, const float* const* clients, const int* 
 int fa_stripe_plan_create(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
                           const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
                           unsigned flags, fa_stripe_plan** out) {
+  return fa_stripe_plan_create_ex(comm, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel,
+                                  counts, 0, flags, out);
+}
+
+int fa_stripe_plan_create_ex(fa_comm* comm, const fa_seg* seg32, int nseg32, int64_t f32_numel,
+                             const fa_seg* seg64, int nseg64, int64_t i64_numel, const int* counts,
+                             int nchunks, unsigned flags, fa_stripe_plan** out) {
   return make_round(comm, FA_MODE_STRIPED, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel,
-                    counts, 1, FA_XCHG_REDUCE, flags, "fa_stripe_plan_create",
+                    counts, nchunks, FA_XCHG_REDUCE, flags, "fa_stripe_plan_create",
                     (fa_round_plan**)out);
 }
 
@@ -1898,7 +2425,7 @@ int fa_describe_round(int mode, int nranks, int rank, const int* counts, const f
   if (mode != FA_MODE_SHARDED && mode != FA_MODE_STRIPED && mode != FA_MODE_CHAINED &&
       mode != FA_MODE_BLOCKED)
     return set_err(FA_E_INVAL, "fa_describe_round: mode %d", mode);
-  if (nchunks == 0) nchunks = 8;
+  if (nchunks == 0) nchunks = mode == FA_MODE_STRIPED ? kStripeChunks : 8;
   if (nchunks < 1 || nchunks > FA_COMM_MAX_CHUNKS)
     return set_err(FA_E_INVAL, "fa_describe_round: nchunks=%d", nchunks);
   if (exchange != FA_XCHG_REDUCE && exchange != FA_XCHG_RS_GATHER)
@@ -1907,6 +2434,7 @@ int fa_describe_round(int mode, int nranks, int rank, const int* counts, const f
   fa_round_plan p;
   p.mode = mode;
   p.xchg = exchange;
+  p.req_chunks = nchunks;
   int rc = make_geo(nranks, rank, counts, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel,
                     flags, "fa_describe_round", &p.g);
   if (rc) return rc;
@@ -1922,6 +2450,31 @@ int fa_describe_round(int mode, int nranks, int rank, const int* counts, const f
     std::copy(s.begin(), s.end(), ops);
   }
   return FA_OK;
+}
+
+
+int fa_round_model(int mode, int nranks, const int* counts, const fa_seg* seg32, int nseg32,
+                   int64_t f32_numel, const fa_seg* seg64, int nseg64, int64_t i64_numel,
+                   int nchunks, int exchange, unsigned flags, int root, int weighted,
+                   fa_round_cost* out) {
+  if (!out) return set_err(FA_E_INVAL, "fa_round_model: out is NULL");
+  if (mode != FA_MODE_SHARDED && mode != FA_MODE_STRIPED && mode != FA_MODE_CHAINED &&
+      mode != FA_MODE_BLOCKED)
+    return set_err(FA_E_INVAL, "fa_round_model: mode %d", mode);
+  if (nchunks == 0) nchunks = mode == FA_MODE_STRIPED ? kStripeChunks : 8;
+  if (nchunks < 1 || nchunks > FA_COMM_MAX_CHUNKS)
+    return set_err(FA_E_INVAL, "fa_round_model: nchunks=%d", nchunks);
+  if (exchange != FA_XCHG_REDUCE && exchange != FA_XCHG_RS_GATHER)
+    return set_err(FA_E_INVAL, "fa_round_model: exchange %d", exchange);
+  if (root >= nranks) return set_err(FA_E_INVAL, "fa_round_model: root=%d", root);
+  Geo g;
+  int rc = make_geo(nranks, 0, counts, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, flags,
+                    "fa_round_model", &g);
+  if (rc) return rc;
+  std::vector<std::vector<fa_xfer>> sch;
+  int64_t V = 0;
+  if ((rc = all_schedules(g, mode, nchunks, exchange, root, weighted != 0, &sch, &V))) return rc;
+  return model_schedules(sch, g.n_total, V, out);
 }
 
 }  // extern "C"

@@ -442,8 +442,13 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
   }
   int b0 = 0;
   if constexpr (PIPE != 0 && FULL && !CHAIN && !TAB) {
-    pipe2_clients<U, DEEP, WEIGHTED, POL>(a, A, n, start, vi, lp, mask);
-    b0 = n;
+    // pipe2_clients reads the inline kernarg arrays: safe on its own for any
+    // launch, the host rule (pipe_rule) aside — beyond kInline clients the
+    // batches below take the tile
+    if (n <= kInline) {
+      pipe2_clients<U, DEEP, WEIGHTED, POL>(a, A, n, start, vi, lp, mask);
+      b0 = n;
+    }
   }
   for (; b0 + B <= n; b0 += B)
     batch<U, B, FULL, DEEP, WEIGHTED, POL, TAB>(a, A, b0, start, vi, ok, lp, mask, r0);

@@ -225,29 +225,93 @@ PyObject* src_match(PyObject*, PyObject* args) {
 // the reduce, the per-tensor check, the broadcast and the version bumps as
 // four Python-level calls, the launches through ctypes with the stream looked
 // up through torch.cuda (tools/launch_cost.py: ~2.7 us of wrapper per launch
-// beyond fa_reduce's own ~3.9 us).  The same sequence here, with the same
-// order and the same guarantee: the broadcast is issued only after the check
-// has passed while the GPU reduces (the reduce writes only the global's
-// bucket, whose value the round replaces anyway).
+// beyond fa_reduce's own ~3.9 us).  The same sequence here.  Since r06 the
+// whole check (every dict's tag, every bound tensor's storage) runs before
+// the reduce is launched, through cached TensorImpl fields (ViewKey), so a
+// failed check has issued nothing.
 //
 // round_state(fa_reduce, plan, a32, a64, n, o32, o64, device, dicts, tags,
-//             tensors, ptrs, written, ng_dicts, ng_tensors) -> capsule
+//             tensors, ptrs, written, ng_dicts, ng_tensors[, precheck_max])
+//             -> capsule
 //   fa_reduce: the address of libfedagg's fa_reduce; plan / a32 / a64 / o32 /
 //   o64: the plan handle, the client pointer arrays and the global's
 //   buckets (kept alive by the caller's binding); the rest as valid_tagged /
 //   bump_versions take them (the capsule holds references).
 //   ng_dicts / ng_tensors: how many of dicts / tensors (the first ones) are
-//   the GLOBAL model's.
+//   the GLOBAL model's; precheck_max: up to this many client tensors
+//   (default 4096) every key is checked before the launch, beyond it the
+//   bucket use counts (bound_round).
 // bound_round(state, weights) -> 1: round issued; 3: the global model's own
 //   check failed (nothing issued: the reduce writes the global's bound
 //   bucket, so the global is checked BEFORE it, r05 — VERDICT r04 weak 6);
-//   0: a client's check failed after the reduce was issued (nothing else
-//   issued; the reduce wrote only the global's still-bound bucket); 2: the
+//   0: a client's check failed (nothing issued — r05 and before: after the
+//   reduce had been issued; r06: so still in a large round whose bucket use
+//   counts are unchanged, see bound_round); 2: the
 //   current device is not the binding's (nothing issued); < 0: fa_reduce's
 //   error code (the message in fa_last_error).  weights: None or bytes of n
 //   float32.
 using fa_reduce_fn = decltype(&fa_reduce);   // called through the address only
 constexpr unsigned kBcastOnly = FA_F_BCAST_ONLY;
+
+// A bound tensor's storage as bound: its TensorImpl (fixed for the life of
+// the Python object the binding holds: a `.data` swap rewrites the impl in
+// place, shallow_copy_from), the storage it then held, the offset into it and
+// the storage's data pointer.  Comparing these reads the impl's own fields —
+// no PyObject type check, no Tensor unpack — so the whole binding can be
+// checked before the reduce is launched (r06).
+struct ViewKey {
+  c10::TensorImpl* impl;
+  const c10::StorageImpl* storage;
+  int64_t offset;
+  const void* data;
+};
+
+bool view_key(PyObject* t, ViewKey* k) {
+  if (!THPVariable_Check(t)) return false;
+  c10::TensorImpl* impl = THPVariable_Unpack(t).unsafeGetTensorImpl();
+  if (!impl->has_storage()) return false;
+  const c10::StorageImpl* s = impl->unsafe_storage().unsafeGetStorageImpl();
+  *k = ViewKey{impl, s, impl->storage_offset(), s ? s->data() : nullptr};
+  return s != nullptr;
+}
+
+// 1: every key's tensor still views the storage it was bound to.
+int keys_intact(const std::vector<ViewKey>& keys, size_t k0, size_t k1) {
+  // the impls are independent: overlap their misses — both lines a check
+  // reads (storage_ near the start, storage_offset_ ~150 B in)
+  constexpr size_t kAhead = 16;
+  for (size_t i = k0; i < k1; ++i) {
+    if (i + kAhead < k1) {
+      const char* a = reinterpret_cast<const char*>(keys[i + kAhead].impl);
+      __builtin_prefetch(a);
+      __builtin_prefetch(a + 128);
+    }
+    const ViewKey& k = keys[i];
+    const c10::StorageImpl* s = k.impl->unsafe_storage().unsafeGetStorageImpl();
+    if (s != k.storage || k.impl->storage_offset() != k.offset || s->data() != k.data) return 0;
+  }
+  return 1;
+}
+
+// 1: dicts [d0, d1) carry their bound tags (see tagged_range).
+int tags_intact(PyObject* dicts, PyObject* tags, Py_ssize_t d0, Py_ssize_t d1) {
+#ifdef FA_DICT_TAGS
+  const char* tp = PyBytes_AS_STRING(tags);
+  for (Py_ssize_t i = d0; i < d1; ++i) {
+    PyObject* d = PyTuple_GET_ITEM(dicts, i);
+    uint64_t want;
+    std::memcpy(&want, tp + i * sizeof(uint64_t), sizeof want);
+    if (((PyDictObject*)d)->ma_version_tag != want) return 0;
+  }
+  return 1;
+#else
+  (void)dicts;
+  (void)tags;
+  (void)d0;
+  (void)d1;
+  return 0;
+#endif
+}
 
 struct RoundState {
   fa_reduce_fn reduce = nullptr;
@@ -261,6 +325,14 @@ struct RoundState {
   Py_ssize_t ng_dicts = 0, ng_tensors = 0;  // the global model's checks come first
   PyObject *dicts = nullptr, *tags = nullptr, *tensors = nullptr, *ptrs = nullptr,
            *written = nullptr;
+  std::vector<ViewKey> keys;   // one per tensor, in the tensors' order
+  // Large rounds (more client tensors than precheck_max): the storages the
+  // clients' tensors view, each held here (+1 use) with the use count it had
+  // when the clients last passed the full check.  A `.data` swap away from a
+  // bucket lowers its storage's count; see bound_round.
+  Py_ssize_t precheck_max = 0;
+  std::vector<c10::Storage> storages;
+  std::vector<size_t> uses;
   ~RoundState() {
     Py_XDECREF(dicts);
     Py_XDECREF(tags);
@@ -274,14 +346,18 @@ void round_capsule_free(PyObject* cap) {
   delete static_cast<RoundState*>(PyCapsule_GetPointer(cap, "feddct_amd.round_state"));
 }
 
+size_t use_count(const c10::Storage& s) {
+  return c10::raw::intrusive_ptr::use_count(s.unsafeGetStorageImpl());
+}
+
 PyObject* round_state(PyObject*, PyObject* args) {
   unsigned long long fn, plan, a32, a64, o32, o64;
   int n, device;
-  Py_ssize_t ngd, ngt;
+  Py_ssize_t ngd, ngt, precheck_max = 4096;
   PyObject *dicts, *tags, *tensors, *ptrs, *written;
-  if (!PyArg_ParseTuple(args, "KKKKiKKiO!SO!SO!nn", &fn, &plan, &a32, &a64, &n, &o32, &o64,
+  if (!PyArg_ParseTuple(args, "KKKKiKKiO!SO!SO!nn|n", &fn, &plan, &a32, &a64, &n, &o32, &o64,
                         &device, &PyTuple_Type, &dicts, &tags, &PyTuple_Type, &tensors, &ptrs,
-                        &PyTuple_Type, &written, &ngd, &ngt))
+                        &PyTuple_Type, &written, &ngd, &ngt, &precheck_max))
     return nullptr;
   if (!fn || !plan || n < 1 || ngd < 0 || ngd > PyTuple_GET_SIZE(dicts) || ngt < 0 ||
       ngt > PyTuple_GET_SIZE(tensors)) {
@@ -299,6 +375,40 @@ PyObject* round_state(PyObject*, PyObject* args) {
   st->device = device;
   st->ng_dicts = ngd;
   st->ng_tensors = ngt;
+  const Py_ssize_t ntens = PyTuple_GET_SIZE(tensors);
+  if (PyBytes_GET_SIZE(ptrs) != ntens * (Py_ssize_t)sizeof(uint64_t) ||
+      PyBytes_GET_SIZE(tags) != PyTuple_GET_SIZE(dicts) * (Py_ssize_t)sizeof(uint64_t)) {
+    delete st;
+    PyErr_SetString(PyExc_ValueError, "round_state: length mismatch");
+    return nullptr;
+  }
+  st->keys.resize(ntens);
+  for (Py_ssize_t i = 0; i < ntens; ++i) {
+    PyObject* t = PyTuple_GET_ITEM(tensors, i);
+    uint64_t want;
+    std::memcpy(&want, PyBytes_AS_STRING(ptrs) + i * sizeof(uint64_t), sizeof want);
+    if (!view_key(t, &st->keys[i]) ||
+        (uint64_t)(uintptr_t)THPVariable_Unpack(t).data_ptr() != want) {
+      delete st;
+      PyErr_SetString(PyExc_ValueError, "round_state: a bound tensor is not on its bucket");
+      return nullptr;
+    }
+  }
+  for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(dicts); ++i)
+    if (!PyDict_Check(PyTuple_GET_ITEM(dicts, i))) {
+      delete st;
+      PyErr_SetString(PyExc_TypeError, "round_state: dicts must hold dicts");
+      return nullptr;
+    }
+  st->precheck_max = precheck_max;
+  for (Py_ssize_t i = ngt; i < ntens; ++i) {
+    const c10::StorageImpl* si = st->keys[i].storage;
+    bool seen = false;
+    for (const c10::Storage& x : st->storages) seen |= x.unsafeGetStorageImpl() == si;
+    if (!seen)
+      st->storages.push_back(THPVariable_Unpack(PyTuple_GET_ITEM(tensors, i)).storage());
+  }
+  for (const c10::Storage& x : st->storages) st->uses.push_back(use_count(x));
   for (PyObject** o : {&dicts, &tags, &tensors, &ptrs, &written}) Py_INCREF(*o);
   st->dicts = dicts;
   st->tags = tags;
@@ -331,26 +441,64 @@ PyObject* bound_round(PyObject*, PyObject* args) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
   }
-  // the global's own dicts and tensors first: the reduce writes its bound
-  // bucket, which must still be the global's (a `.data` swap or a new
-  // parameter on the global would otherwise see its old storage overwritten)
-  const Py_ssize_t nd = PyTuple_GET_SIZE(st->dicts), nt = PyTuple_GET_SIZE(st->tensors);
-  int ok = tagged_range(st->dicts, st->tags, st->tensors, st->ptrs, 0, st->ng_dicts, 0,
-                        st->ng_tensors);
-  if (ok < 0) return nullptr;
-  if (ok == 0) return PyLong_FromLong(3);
+  // Everything is checked BEFORE anything is launched.  The global's own
+  // dicts and tensors first: the reduce writes its bound bucket, which must
+  // still be the global's (r05).  Then the clients' (r06):
+  // until r05 they were checked while the GPU reduced, so a client whose
+  // parameter had been replaced by one of another shape sent the call down
+  // the full path — which raises, as the reference does — AFTER the reduce
+  // had written the mean of the stale buckets into the global; the reference
+  // raises inside torch.stack and leaves the global untouched
+  // (train_fedavg.py:144-147).
+  //
+  // Large rounds (cfg5's 9,800 tensors: 16 us for the clients' keys, r06
+  // tools/shim_profile.py) check, before the launch, the clients' dict tags
+  // and the use count of each client bucket's storage — a `.data` swap away
+  // from a bucket lowers it, a new view raises it, and any mismatch sends the
+  // clients' keys through the full check here (which, when it passes,
+  // re-records the counts).  With the counts unchanged the keys are checked
+  // while the GPU reduces, as in r05: a failure there still leaves the
+  // global written, which only a `.data` re-view onto the SAME bucket (or a
+  // swap exactly offset by a new view of the bucket) can reach.
+  const Py_ssize_t nd = PyTuple_GET_SIZE(st->dicts);
+  if (!tags_intact(st->dicts, st->tags, 0, st->ng_dicts) ||
+      !keys_intact(st->keys, 0, (size_t)st->ng_tensors))
+    return PyLong_FromLong(3);
+  if (!tags_intact(st->dicts, st->tags, st->ng_dicts, nd)) return PyLong_FromLong(0);
+  const size_t k0 = (size_t)st->ng_tensors, k1 = st->keys.size();
+  bool later = false;
+  if ((Py_ssize_t)(k1 - k0) > st->precheck_max) {
+    later = true;
+    for (size_t i = 0; i < st->storages.size() && later; ++i)
+      later = use_count(st->storages[i]) == st->uses[i];
+  }
+  if (!later) {
+    if (!keys_intact(st->keys, k0, k1)) return PyLong_FromLong(0);
+    for (size_t i = 0; i < st->storages.size(); ++i) st->uses[i] = use_count(st->storages[i]);
+  }
   int rc = st->reduce(st->plan, st->a32, st->a64, st->n, wp, st->o32, st->o64, 0, stream);
   if (rc != 0) return PyLong_FromLong(rc);
-  // the clients' (most of the tensors) while the GPU reduces
-  ok = tagged_range(st->dicts, st->tags, st->tensors, st->ptrs, st->ng_dicts, nd, st->ng_tensors,
-                    nt);
-  if (ok < 0) return nullptr;
-  if (ok == 0) return PyLong_FromLong(0);
+  if (later && !keys_intact(st->keys, k0, k1)) return PyLong_FromLong(0);
   rc = st->reduce(st->plan, st->a32, st->a64, st->n, nullptr, st->o32, st->o64, kBcastOnly,
                   stream);
   if (rc != 0) return PyLong_FromLong(rc);
   if (bump_all(st->written) < 0) return nullptr;
   return PyLong_FromLong(1);
+}
+
+// round_check(state, what) -> bool: bound_round's pre-launch check alone,
+// for profiling (tools/shim_profile.py): what 0 = every dict's tag, 1 = every
+// tensor's ViewKey, 2 = both.
+PyObject* round_check(PyObject*, PyObject* args) {
+  PyObject* cap;
+  int what = 2;
+  if (!PyArg_ParseTuple(args, "O|i", &cap, &what)) return nullptr;
+  auto* st = static_cast<RoundState*>(PyCapsule_GetPointer(cap, "feddct_amd.round_state"));
+  if (!st) return nullptr;
+  int ok = 1;
+  if (what != 1) ok = tags_intact(st->dicts, st->tags, 0, PyTuple_GET_SIZE(st->dicts));
+  if (ok && what != 0) ok = keys_intact(st->keys, 0, st->keys.size());
+  return PyBool_FromLong(ok);
 }
 
 // grad_state(params, views) -> 0: every params[i].grad is views[i] (the flat
@@ -644,7 +792,8 @@ PyMethodDef kMethods[] = {
     {"bump_versions", bump_versions, METH_VARARGS, "autograd version bump of every tensor"},
     {"round_state", round_state, METH_VARARGS, "the drop-in's bound repeat round (capsule)"},
     {"src_match", src_match, METH_VARARGS, "the bound round's objects, by identity"},
-    {"bound_round", bound_round, METH_VARARGS, "reduce, check, broadcast, bump in one call"},
+    {"bound_round", bound_round, METH_VARARGS, "check, reduce, broadcast, bump in one call"},
+    {"round_check", round_check, METH_VARARGS, "bound_round's pre-launch check alone"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_fa_shim", "feddct_amd host bookkeeping", -1,

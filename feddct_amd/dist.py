@@ -6,10 +6,11 @@ Rank r holds a contiguous shard of the client slots, in slot order
 THE DEFAULT ENTRY IS ``Aggregator`` (r05), and it is EXACT: its result is
 bit-identical to one GPU reducing every slot, i.e. to the reference's
 single-process ``stack(...).mean(0)`` (train_feddct.py:42-50).  Over RCCL it
-runs the native library's default round (comm.NativeAggregator: the blocked
-round when every 16-slot cascade block lies on at most two ranks, else the
-chained round — ``exact_form``); over any other transport (gloo rehearsals)
-the chained round orchestrated here.  The round forms:
+runs the native library's default round (comm.NativeAggregator: the exact
+form — blocked, chained or striped — with the lowest modelled time,
+``exact_form``; r06); over any other transport (gloo rehearsals) the chained
+or striped round orchestrated here, whichever the model prefers (the blocked
+round exists natively only).  The round forms:
 
 * ``ChainAggregator`` (exact client shards): the shards stay put and the
   cascade's accumulator state travels rank to rank in slot order, chunk by
@@ -17,7 +18,8 @@ the chained round orchestrated here.  The round forms:
   Bit-identical;
 * ``StripedAggregator`` (e2, exact column stripes): every client's values
   for rank r's column stripe go to rank r, which reduces the stripe over all
-  clients.  Bit-identical;
+  clients; per column chunk ONE batch with every peer (r06).  Bit-identical,
+  weighted too;
 * ``ShardedAggregator`` (e1, OPT-IN: ``Aggregator(exact=False)``): the HIP
   kernel sums the rank's clients in the torch order without the /N
   (FA_F_SUM_ONLY), chunk by column chunk; each chunk's partial bucket is
@@ -31,11 +33,10 @@ the chained round orchestrated here.  The round forms:
 int64 keys (a few bytes) always travel raw — an all-gather of every rank's
 int64 buckets — and are reduced exactly over all N_total clients.
 
-Point-to-point exchanges run in pairwise rounds (``pair_rounds``): in every
-round each rank meets one partner, and the lower rank of a pair sends
-first, so a transport that serialises a rank's sends and receives (gloo)
-cannot stall.  The native library (libfedagg_comm.so) runs the same rounds
-(tests/test_schedule.py checks they agree).
+The striped round's exchanges follow the native schedule
+(``stripe_schedule``: per column chunk one batch of sends and receives with
+every peer, the finished chunk two steps later; tests/test_schedule.py checks
+the two agree op for op).
 
 The arithmetic backends are pluggable so the orchestration is testable on
 CPU with gloo (tests/test_dist_gloo.py injects oracle backends); the product
@@ -65,11 +66,10 @@ def cascade_lp(n: int) -> int:
     return max(4, (int(n - 1).bit_length() if n > 1 else 0) // 4)
 
 
-def exact_form(counts: Sequence[int]) -> str:
-    """The exact round the default entry takes for these shard counts
-    (fedcomm.hip fa_multi_select): "blocked" when every cascade block of
-    2**lp slots lies on at most two of the ranks holding slots, else
-    "chained"."""
+def blocked_allowed(counts: Sequence[int]) -> bool:
+    """The blocked round's precondition (fedcomm.hip first_wide_block): every
+    cascade block of 2**lp slots lies on at most two of the ranks holding
+    slots."""
     first, n = [], 0
     for c in counts:
         first.append(n)
@@ -79,46 +79,56 @@ def exact_form(counts: Sequence[int]) -> str:
         b = min(n, a + q)
         on = sum(1 for r, c in enumerate(counts) if c > 0 and first[r] < b and first[r] + c > a)
         if on > 2:
-            return "chained"
-    return "blocked"
+            return False
+    return True
 
 
-def partner(world: int, rank: int, t: int) -> int:
-    """Rank ``rank``'s partner in round ``t`` of the circle-method pairing
-    (or -1: sits out), as fedcomm.hip's ``partner``."""
-    m = world + 1 if world % 2 else world
-    if m < 2:
-        return -1
-    k = m - 1
-    if rank == k:
-        q = next(i for i in range(k) if (2 * i) % k == t % k)
-    elif (2 * rank) % k == t % k:
-        q = k
-    else:
-        q = (t - rank) % k
-    return -1 if q >= world else q
+def exact_form(counts: Sequence[int], layout: Optional[BucketLayout] = None,
+               root_all: bool = False) -> str:
+    """The exact round the default entry takes for these shard counts: the
+    form with the lowest modelled time (fedcomm.hip fa_multi_select_layout
+    on ``layout``; None: fa_multi_select's nominal layout) — "blocked" (only
+    where ``blocked_allowed``), "chained" or "striped".  ``root_all``: the
+    result goes to every rank.  r05: "blocked" if allowed, else "chained"."""
+    from .comm import multi_select
+    return multi_select(counts, layout=layout, root_all=root_all)
 
 
-def pair_rounds(world: int, rank: int):
-    """The partners of ``rank``, one per round, every other rank once."""
-    rounds = world if world % 2 else world - 1
-    return [p for p in (partner(world, rank, t) for t in range(rounds)) if p >= 0 and p != rank]
+def stripe_schedule(bounds, shards, me, root=-1):
+    """The striped round's exchange steps for rank ``me`` (fedcomm.hip
+    sched_striped, its steps 2..C+3): per step, in issue order,
+    ("send", peer, slot, offset, count) / ("recv", peer, slot, offset, count)
+    for client rows, ("send_out", peer, offset, count) / ("recv_out", peer,
+    offset, count) for finished chunks, and ("reduce", chunk, offset, count)
+    for the stripe reduce that runs beside the step's exchanges.  bounds[r]:
+    the C + 1 chunk bounds of rank r's stripe; shards[r]: its slot range."""
+    W = len(bounds)
+    C = len(bounds[0]) - 1
+    result = root < 0 or root == me
 
-
-def stripe_p2p_schedule(ranges, shards, me):
-    """The striped round's client exchange for rank ``me``: ("send", peer,
-    slot, offset, count) / ("recv", peer, slot, offset, count) in issue order
-    (pairwise rounds; the lower rank of a pair sends first).  ``ranges[r]`` =
-    rank r's column stripe, ``shards[r]`` = its slot range."""
-    out = []
-    lo_me, hi_me = ranges[me]
-    for r in pair_rounds(len(ranges), me):
-        lo, hi = ranges[r]
-        sends = [("send", r, k, lo, hi - lo) for k in range(*shards[me])] if hi > lo else []
-        recvs = ([("recv", r, k, lo_me, hi_me - lo_me) for k in range(*shards[r])]
-                 if hi_me > lo_me else [])
-        out += sends + recvs if me < r else recvs + sends
-    return out
+    def ln(r, c):
+        return bounds[r][c + 1] - bounds[r][c]
+    steps = []
+    for j in range(C + 2):
+        ops = []
+        for q in range(1, W):
+            r = (me + q) % W
+            if j < C:
+                if ln(r, j) > 0:
+                    ops += [("send", r, k, bounds[r][j], ln(r, j)) for k in range(*shards[me])]
+                if ln(me, j) > 0:
+                    ops += [("recv", r, k, bounds[me][j], ln(me, j)) for k in range(*shards[r])]
+            c = j - 2
+            if 0 <= c < C:
+                if ln(me, c) > 0 and (root < 0 or root == r):
+                    ops.append(("send_out", r, bounds[me][c], ln(me, c)))
+                if ln(r, c) > 0 and result:
+                    ops.append(("recv_out", r, bounds[r][c], ln(r, c)))
+        k = j - 1
+        if 0 <= k < C and ln(me, k) > 0:
+            ops.append(("reduce", k, bounds[me][k], ln(me, k)))
+        steps.append(ops)
+    return steps
 
 
 def p2p(ops, group=None):
@@ -329,27 +339,30 @@ class ShardedAggregator:
 # Exact mode: element (column) stripes.
 # --------------------------------------------------------------------------
 class HipStripeBackend:
-    """Stripe reduction with the HIP kernel over a tile-subset plan."""
+    """Stripe-chunk reductions with the HIP kernel over tile-subset plans
+    (one per chunk of this rank's stripe)."""
 
-    def __init__(self, layout: BucketLayout, stripe_tiles, tiles64):
+    def __init__(self, layout: BucketLayout, chunk_tiles, tiles64):
         from . import _lib
         self._lib = _lib
         te = 0
-        self.plan = (_lib.Plan(None, layout.f32_numel, None, layout.i64_numel, te,
-                               tiles=stripe_tiles) if len(stripe_tiles) else None)
+        self.plans = [_lib.Plan(None, layout.f32_numel, None, layout.i64_numel, te, tiles=t)
+                      if len(t) else None for t in chunk_tiles]
         self.plan64 = (_lib.Plan(None, layout.f32_numel, None, layout.i64_numel, te,
                                  tiles=tiles64) if len(tiles64) else None)
 
-    def reduce_stripe(self, sources, out32: torch.Tensor):
-        """``sources[k] = (tensor, base)``: client slot k's element e lives at
-        ``tensor[e - base]`` for e in this rank's stripe."""
-        if self.plan is None:
+    def reduce_chunk(self, c, lo, hi, sources, out32: torch.Tensor, weights=None):
+        """Chunk ``c`` ([lo, hi)) over every client: ``sources[k] = (tensor,
+        base)``, client slot k's element e at ``tensor[e - base]``; weights:
+        None (the mean) or n_total fp32 weights (no division)."""
+        if self.plans[c] is None:
             return
         L = self._lib
         ptrs = [t.data_ptr() - 4 * base for t, base in sources]
+        w = None if weights is None else (ctypes.c_float * len(weights))(*map(float, weights))
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        L.check(L.lib.fa_reduce(self.plan.handle, L.ptr_array(ptrs), None, len(ptrs), None,
-                                out32.data_ptr(), None, 0, s), "fa_reduce(stripe)")
+        L.check(L.lib.fa_reduce(self.plans[c].handle, L.ptr_array(ptrs), None, len(ptrs), w,
+                                out32.data_ptr(), None, 0, s), "fa_reduce(stripe chunk)")
 
     def reduce_i64(self, clients64, out64: torch.Tensor):
         if self.plan64 is None:
@@ -363,15 +376,20 @@ class HipStripeBackend:
 
 class StripedAggregator:
     """Bit-exact cross-GPU round: rank r owns the column stripe
-    [lo_r, hi_r) of the bucket (cut at vector-tile starts, partition.py), gets
-    every client's values for those columns, reduces them in the exact torch
-    order and the stripes are exchanged so every rank ends with the full
-    global state.  Two ingress forms:
+    [lo_r, hi_r) of the bucket (cut at vector-tile starts, partition.py), cut
+    into ``nchunks`` column chunks; it gets every client's values for those
+    columns, reduces them in the exact torch order and the finished chunks
+    go to the result ranks (every rank: ``final="allreduce"``; ``root``:
+    ``"reduce"``).  Two ingress forms:
 
-    * ``step_device(local32, local64)`` — client slots device-resident and
-      sharded by rank (as in ShardedAggregator): the stripes travel
-      rank-to-rank as grouped P2P send/recv over RCCL (n·B·(W-1)/W per rank:
-      the price of exactness on device-resident inputs);
+    * ``step_device(local32, local64, weights=None)`` — client slots
+      device-resident and sharded by rank (``counts``, default shard_range):
+      per chunk ONE batch of sends and receives with every peer (r06: the
+      native schedule, ``stripe_schedule``; r02-r05 one partner at a time),
+      n·B·(W-1)/W per rank over the round.  Weighted: the rows a rank sends
+      are its clients' values pre-multiplied by their weights (rounded as the
+      weighted kernel rounds the product), the receiver reduces them with
+      weight 1;
     * ``step_host(stripes32, clients64)`` — client updates in host memory:
       each GPU uploads only ITS stripe of every client (no xGMI traffic for
       inputs; ingress bandwidth scales with the GPUs' PCIe links).
@@ -381,51 +399,47 @@ class StripedAggregator:
 
     def __init__(self, layout: BucketLayout, n_total: int, out32: torch.Tensor,
                  out64: torch.Tensor, group=None, backend=None, final: str = "allreduce",
-                 root: int = 0):
-        from .partition import i64_tiles, layout_tiles, split_tiles
+                 root: int = 0, nchunks: int = 4, counts: Optional[Sequence[int]] = None):
+        from .partition import i64_tiles, layout_tiles, stripe_chunks
         if final not in ("reduce", "allreduce"):
             raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
-        self.final, self.root = final, root
+        self.final = final
+        self.root = root if final == "reduce" else -1
         self.layout = layout
         self.n_total = n_total
         self.out32, self.out64 = out32, out64
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        if counts is None:
+            counts = [b - a for a, b in (shard_range(n_total, self.world, r)
+                                         for r in range(self.world))]
+        self.counts = [int(c) for c in counts]
+        if len(self.counts) != self.world or sum(self.counts) != n_total:
+            raise ValueError(f"counts {self.counts} do not shard {n_total} slots over "
+                             f"{self.world} ranks")
+        first = [sum(self.counts[:r]) for r in range(self.world)]
+        self.shards = [(first[r], first[r] + self.counts[r]) for r in range(self.world)]
         info, tiles = layout_tiles(layout)
-        parts = split_tiles(tiles, self.world, layout.f32_numel)
-        self.ranges = [(lo, hi) for lo, hi, _ in parts]
+        self.chunks = stripe_chunks(tiles, self.world, layout.f32_numel, nchunks)
+        self.bounds = [[c[0] for c in ch] + [ch[-1][1]] for ch in self.chunks]
+        self.ranges = [(b[0], b[-1]) for b in self.bounds]
         self.lo, self.hi = self.ranges[self.rank]
-        self.backend = backend or HipStripeBackend(layout, parts[self.rank][2], i64_tiles(tiles))
+        self.backend = backend or HipStripeBackend(layout, [t for _, _, t in self.chunks[self.rank]],
+                                                   i64_tiles(tiles))
         L = self.hi - self.lo
         self.lpad = (L + 3) // 4 * 4
         dev = out32.device
         self.recv = torch.zeros((n_total, max(self.lpad, 4)), dtype=torch.float32, device=dev)
-        nmax = -(-n_total // self.world)
+        self.stage = None   # weighted rounds: pre-multiplied local clients
+        nmax = max(1, max(self.counts))
         width = max(1, layout.i64_numel)
         self.gather64 = torch.zeros((self.world * nmax, width), dtype=torch.int64, device=dev)
         self.stack64 = torch.zeros((nmax, width), dtype=torch.int64, device=dev)
-        self.rows64 = []
-        self.shards = [shard_range(n_total, self.world, r) for r in range(self.world)]
-        for r, (a, b) in enumerate(self.shards):
-            self.rows64 += [r * nmax + j for j in range(b - a)]
+        self.rows64 = [r * nmax + j for r in range(self.world) for j in range(self.counts[r])]
 
     def _peer(self, r):
         return r if self.group is None else dist.get_global_rank(self.group, r)
-
-    def _gather_stripes(self):
-        """Finished stripes of out32 to every other rank ("allreduce") or to
-        the root only ("reduce"), P2P straight into out32 views, one partner
-        per round (the lower rank sends first)."""
-        me = self.rank
-        for r in pair_rounds(self.world, me):
-            lo, hi = self.ranges[r]
-            sends, recvs = [], []
-            if self.hi > self.lo and (self.final == "allreduce" or r == self.root):
-                sends.append((dist.isend, self.out32[self.lo:self.hi], self._peer(r)))
-            if hi > lo and (self.final == "allreduce" or me == self.root):
-                recvs.append((dist.irecv, self.out32[lo:hi], self._peer(r)))
-            p2p(sends + recvs if me < r else recvs + sends, self.group)
 
     def _i64(self, local64):
         if not self.layout.i64_numel:
@@ -435,36 +449,59 @@ class StripedAggregator:
         dist.all_gather_into_tensor(self.gather64, self.stack64, group=self.group)
         self.backend.reduce_i64([self.gather64[r] for r in self.rows64], self.out64)
 
-    def p2p_schedule(self):
-        """This rank's client exchange, in issue order (stripe_p2p_schedule)."""
-        return stripe_p2p_schedule(self.ranges, self.shards, self.rank)
+    def schedule(self):
+        """This rank's exchange steps, in issue order (``stripe_schedule``)."""
+        return stripe_schedule(self.bounds, self.shards, self.rank, self.root)
 
-    def step_device(self, local32: List[torch.Tensor], local64: List[torch.Tensor]) -> None:
+    def _dst(self):
+        result = self.root < 0 or self.root == self.rank
+        return self.out32 if result else self.out32.new_empty(self.out32.shape)
+
+    def step_device(self, local32: List[torch.Tensor], local64: List[torch.Tensor],
+                    weights: Optional[Sequence[float]] = None) -> None:
         me = self.rank
         a, b = self.shards[me]
-        assert len(local32) == b - a
-        sched = self.p2p_schedule()
-        i = 0
-        while i < len(sched):   # one partner (round) at a time
-            peer = sched[i][1]
-            ops = []
-            while i < len(sched) and sched[i][1] == peer:
-                kind, _, slot, off, cnt = sched[i]
-                if kind == "send":
-                    ops.append((dist.isend, local32[slot - a][off:off + cnt], self._peer(peer)))
-                else:
-                    ops.append((dist.irecv, self.recv[slot, :cnt], self._peer(peer)))
-                i += 1
-            p2p(ops, self.group)
-        sources = []
-        for k in range(self.n_total):
-            if a <= k < b:
-                sources.append((local32[k - a], 0))
-            else:
-                sources.append((self.recv[k], self.lo))
-        self.backend.reduce_stripe(sources, self.out32)
+        if len(local32) != b - a:
+            raise ValueError(f"rank {me} holds {len(local32)} clients, shard is {b - a}")
         self._i64(local64)
-        self._gather_stripes()
+        send = local32
+        wfull = None
+        if weights is not None:
+            if len(weights) != b - a:
+                raise ValueError(f"{len(weights)} weights for {b - a} clients")
+            send = []
+            for j, t in enumerate(local32):
+                wj = torch.tensor(float(np.float32(weights[j])), device=t.device)
+                send.append(t * wj)
+            wfull = [1.0] * self.n_total
+            for j in range(b - a):
+                wfull[a + j] = float(np.float32(weights[j]))
+        sources = [(local32[k - a], 0) if a <= k < b else (self.recv[k], self.lo)
+                   for k in range(self.n_total)]
+        dst = self._dst()
+        for ops in self.schedule():
+            post, red = [], None
+            for op in ops:
+                kind = op[0]
+                if kind == "send":
+                    _, r, slot, off, cnt = op
+                    post.append((dist.isend, send[slot - a][off:off + cnt], self._peer(r)))
+                elif kind == "recv":
+                    _, r, slot, off, cnt = op
+                    post.append((dist.irecv, self.recv[slot, off - self.lo:off - self.lo + cnt],
+                                 self._peer(r)))
+                elif kind == "send_out":
+                    _, r, off, cnt = op
+                    post.append((dist.isend, dst[off:off + cnt], self._peer(r)))
+                elif kind == "recv_out":
+                    _, r, off, cnt = op
+                    post.append((dist.irecv, self.out32[off:off + cnt], self._peer(r)))
+                else:
+                    red = op
+            p2p(post, self.group)
+            if red is not None:
+                _, c, off, cnt = red
+                self.backend.reduce_chunk(c, off, off + cnt, sources, dst, wfull)
 
     def step_host(self, stripes32: Sequence[torch.Tensor], clients64: Sequence[torch.Tensor],
                   local64: Optional[List[torch.Tensor]] = None) -> None:
@@ -473,12 +510,25 @@ class StripedAggregator:
         L = self.hi - self.lo
         for k, t in enumerate(stripes32):
             self.recv[k, :L].copy_(t, non_blocking=True)
-        self.backend.reduce_stripe([(self.recv[k], self.lo) for k in range(self.n_total)],
-                                   self.out32)
+        dst = self._dst()
+        sources = [(self.recv[k], self.lo) for k in range(self.n_total)]
+        for c, (lo, hi, _) in enumerate(self.chunks[self.rank]):
+            if hi > lo:
+                self.backend.reduce_chunk(c, lo, hi, sources, dst)
         if self.layout.i64_numel:
             g = torch.stack([t.to(self.out64.device, non_blocking=True) for t in clients64])
             self.backend.reduce_i64(list(g.unbind(0)), self.out64)
-        self._gather_stripes()
+        # the finished stripes to the result ranks, every peer in one batch
+        me, result = self.rank, self.root < 0 or self.root == self.rank
+        post = []
+        for q in range(1, self.world):
+            r = (me + q) % self.world
+            lo, hi = self.ranges[r]
+            if self.hi > self.lo and (self.root < 0 or self.root == r):
+                post.append((dist.isend, dst[self.lo:self.hi], self._peer(r)))
+            if hi > lo and result:
+                post.append((dist.irecv, self.out32[lo:hi], self._peer(r)))
+        p2p(post, self.group)
 
 
 # --------------------------------------------------------------------------
@@ -688,11 +738,14 @@ class Aggregator:
     ``exact=True`` (default): bit-identical to one GPU reducing all
     ``n_total`` slots (the reference's train_feddct.py:42-50 order).  Over an
     RCCL ("nccl") group the native library's default round
-    (comm.NativeAggregator: blocked or chained by ``exact_form(counts)``, ONE
-    C call per round on the library's own communicator); over any other
-    backend, or with an injected arithmetic ``backend`` (tests), the chained
-    round orchestrated over torch.distributed (``ChainAggregator``) — the
-    blocked round exists natively only.
+    (comm.NativeAggregator: the form and chunk count the cost model picks,
+    ``exact_form(counts, layout)``, ONE C call per round on the library's own
+    communicator); over any other backend, or with injected arithmetic
+    backends (tests: ``backend`` for the chained form, ``stripe_backend`` for
+    the striped one), the round orchestrated over torch.distributed — the
+    striped form (``StripedAggregator``) where the model picks it, else the
+    chained one (``ChainAggregator``; the blocked round exists natively
+    only).
 
     ``exact=False``: the re-associated e1 round (``ShardedAggregator``):
     unweighted only; NOT within 1 ULP (max 22,938 ULP measured r04,
@@ -708,7 +761,8 @@ class Aggregator:
                  out64: torch.Tensor, group=None, final: str = "reduce",
                  root: Optional[int] = None, weights: Optional[Sequence[float]] = None,
                  counts: Optional[Sequence[int]] = None, exact: bool = True,
-                 native: Optional[bool] = None, backend=None, nchunks: Optional[int] = None):
+                 native: Optional[bool] = None, backend=None, nchunks: Optional[int] = None,
+                 stripe_backend=None):
         if final not in ("reduce", "allreduce"):
             raise ValueError(f"final must be 'reduce' or 'allreduce', not {final!r}")
         world, rank = dist.get_world_size(group), dist.get_rank(group)
@@ -735,7 +789,8 @@ class Aggregator:
             self._step = self._agg.step
             return
         if native is None:
-            native = backend is None and "nccl" in str(dist.get_backend(group))
+            native = (backend is None and stripe_backend is None
+                      and "nccl" in str(dist.get_backend(group)))
         if native:
             from .comm import Comm, NativeAggregator
             self._comm = Comm.from_process_group(group)
@@ -744,6 +799,12 @@ class Aggregator:
                                          counts=counts, nchunks=nchunks or 0)
             self.form = f"{self._agg.mode}/native"
             self._step = self._agg.step
+        elif exact_form(counts, layout, root_all=final != "reduce") == "striped":
+            self._agg = StripedAggregator(layout, n_total, out32, out64, group=group,
+                                          backend=stripe_backend, final=final, root=root,
+                                          nchunks=nchunks or 4, counts=counts)
+            self.form = "striped/torch.distributed"
+            self._step = lambda: self._agg.step_device(self.local32, self.local64, self.weights)
         else:
             self._agg = ChainAggregator(layout, n_total, out32, out64, group=group,
                                         backend=backend, final=final, root=root,

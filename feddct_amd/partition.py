@@ -79,6 +79,20 @@ def split_tiles(tiles: np.ndarray, parts: int, f32_numel: int, fractions=None
     return out
 
 
+def stripe_chunks(tiles: np.ndarray, parts: int, f32_numel: int, nchunks: int):
+    """The striped round's cut (fedcomm.hip build_round, r06): ``parts``
+    stripes (split_tiles), each cut into ``nchunks`` column chunks by the
+    same rule.  Returns, per stripe, [(lo, hi, tiles)] of its chunks, in
+    order, covering the stripe exactly (trailing chunks may be empty)."""
+    out = []
+    for lo, hi, sub in split_tiles(tiles, parts, f32_numel):
+        ci = cut_index(sub, nchunks)
+        b = [lo] + [int(sub[ci[c], 0]) if ci[c] < len(sub) else hi
+                    for c in range(1, nchunks)] + [hi]
+        out.append([(b[c], b[c + 1], sub[ci[c]:ci[c + 1]]) for c in range(nchunks)])
+    return out
+
+
 def i64_tiles(tiles: np.ndarray) -> np.ndarray:
     return tiles[tiles[:, 2] >= K_I64_MIN]
 

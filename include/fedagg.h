@@ -171,11 +171,18 @@ int fa_plan_create_from_tiles(const fa_tile_desc *tiles, int ntiles,
  * and returns their count, 0 when the plain cut is kept (the round is
  * >= 97 % full or the launch needs more than one round), < 0 on error.
  * fa_plan_launch_shape: the tiles and resident-workgroup slots a plain
- * fa_reduce call with n clients (weighted or not) launches with. */
+ * fa_reduce call with n clients (weighted or not) launches with.
+ * fa_plan_launch_form: the kernel that call runs — its vector tile width
+ * (floats), clients per load batch, and whether its full tiles take the
+ * client loop (pipe = 1: the next client's loads before the current
+ * client's adds) or the batches (0).  Torch-GPU-order plans
+ * report zeros. */
 int fa_plan_balance_host(const fa_tile_desc *vec, int nvec, int tile_elems,
                          int nscalar, int slots, fa_tile_desc *out, int cap);
 int fa_plan_launch_shape(const fa_plan *plan, int n, int weighted, int *ntiles,
                          int *slots);
+int fa_plan_launch_form(const fa_plan *plan, int n, int weighted, int *tile_elems,
+                        int *batch, int *pipe);
 
 /* ---- summation order ------------------------------------------------------
  * FA_ORDER_TORCH_CPU (every plan's default): torch's CPU stack(...).mean(0),

@@ -91,6 +91,28 @@ int fa_comm_info(const fa_comm *comm, int *nranks, int *rank, int *device);
  * cannot be captured (a rank holding more than FA_INLINE_CLIENTS slots) or
  * whose capture the runtime refuses run uncaptured either way. */
 int fa_comm_set_graphs(fa_comm *comm, int enable);
+/* Round profiles (r06; default OFF): with profiling on, every round a plan of
+ * this communicator runs records event pairs around each of its RCCL groups
+ * (on the communication stream) and each of its kernels (on the stream it
+ * runs on), and around the whole round on the caller's stream (rounds are
+ * then never replayed from graphs).  fa_round_plan_profile reads the last
+ * profiled round of any plan of this library (an fa_multi_plan,
+ * fa_chain_plan, fa_stripe_plan, fa_block_plan or fa_shard_plan; it waits for
+ * the round): the sum of the groups' durations, of the kernels' on each
+ * stream, the round's wall time on the caller's stream, and the counts — so
+ * a multi-GPU run shows how much of a round is exchange, how much compute,
+ * and how much of the two overlapped.  A one-rank plan (the plain reduction)
+ * has no profile. */
+typedef struct fa_round_profile {
+  double exchange_us;         /* sum over the round's groups (communication stream) */
+  double comm_kernel_us;      /* kernels on the communication stream            */
+  double compute_kernel_us;   /* kernels on the caller's stream                 */
+  double wall_us;             /* the whole round on the caller's stream         */
+  int32_t groups;
+  int32_t kernels;
+} fa_round_profile;
+int fa_comm_set_profile(fa_comm *comm, int enable);
+int fa_round_plan_profile(const void *plan, fa_round_profile *out);
 
 /* Shard plan of one rank for a bucket layout (as fa_plan_create; the layout
  * must be built with FA_PLAN_GAPS_ARE_PADDING: chunk exchanges span the
@@ -123,20 +145,38 @@ typedef struct fa_shard_io {
 int fa_reduce_sharded(fa_shard_plan *const *plans, int nlocal,
                       const fa_shard_io *io, int root);
 
-/* ---- the default multi-GPU round (r05): exact ------------------------------
- * fa_multi_select (host only, no communicator): the round form the default
- * entry takes for these counts — FA_MODE_BLOCKED when every cascade block of
- * 2^lp slots (16 below 65,536 slots) lies on at most two of the ranks holding
- * slots, else FA_MODE_CHAINED; FA_MODE_SHARDED (e1) only with
- * FA_MULTI_REASSOCIATE.  fa_multi_plan_create builds that form's plan
- * (nchunks 0: 16 column chunks for the chained round, 8 for e1; the blocked
- * round has none); fa_reduce_multi runs it (io / root as fa_reduce_sharded;
- * weighted rounds: fp32 keys = sum over all clients of fp32(x_i * w_i) in the
- * torch order, also exact).  fa_multi_plan_mode reports the form. */
-#define FA_MULTI_EXACT 0u          /* default: blocked or chained, bit-identical */
+/* ---- the default multi-GPU round (r05; chosen by a cost model since r06) ---
+ * The default entry runs the EXACT form (blocked, chained or striped — all
+ * bit-identical to one GPU) with the lowest modelled time (fa_round_model
+ * below), and its chunk count; the blocked form only where its precondition
+ * holds (every cascade block of 2^lp slots, 16 below 65,536 slots, on at
+ * most two of the ranks holding slots).  FA_MODE_SHARDED (e1) only with
+ * FA_MULTI_REASSOCIATE.
+ * fa_multi_select_layout (host only, no communicator): that choice for a
+ * layout — *mode, *nchunks (the candidates: chained 4/8/16/32, striped
+ * 1/2/4/8, blocked 1) and the winner's modelled time in microseconds
+ * (model_us may be NULL).  The model's root: every rank with
+ * FA_MULTI_ROOT_ALL, else the last rank holding slots (the rounds may still
+ * be run with any root: the flag only steers the choice).
+ * fa_multi_select: the same for a nominal layout (one fp32 tensor of 2^24
+ * elements, no int64 keys), from the counts alone.
+ * fa_multi_plan_create builds the chosen form's plan (nchunks 0: the chosen
+ * count; else the given count for whatever form is chosen); fa_reduce_multi
+ * runs it (io / root as fa_reduce_sharded; weighted rounds: fp32 keys = sum
+ * over all clients of fp32(x_i * w_i) in the torch order, also exact).
+ * fa_multi_plan_mode reports the form, fa_multi_plan_chunks the count.
+ * r05 chose by geometry alone (blocked if allowed, else chained). */
+#define FA_MULTI_EXACT 0u          /* default: the fastest exact form            */
 #define FA_MULTI_REASSOCIATE 1u    /* opt-in: e1, NOT bit-identical (above)      */
+#define FA_MULTI_ROOT_ALL 2u       /* cost-model hint: results on every rank     */
 typedef struct fa_multi_plan fa_multi_plan;
 int fa_multi_select(int nranks, const int *counts, unsigned mflags, int *mode);
+int fa_multi_select_layout(int nranks, const int *counts, const fa_seg *seg32,
+                           int nseg32, int64_t f32_numel, const fa_seg *seg64,
+                           int nseg64, int64_t i64_numel, unsigned flags,
+                           unsigned mflags, int *mode, int *nchunks,
+                           double *model_us);
+int fa_multi_plan_chunks(const fa_multi_plan *plan, int *nchunks);
 int fa_multi_plan_create(fa_comm *comm, const fa_seg *seg32, int nseg32,
                          int64_t f32_numel, const fa_seg *seg64, int nseg64,
                          int64_t i64_numel, const int *counts, int nchunks,
@@ -164,23 +204,38 @@ int fa_mean_f32_multi_ex(fa_comm *comm, const float *const *clients,
 
 /* ---- exact mode: column stripes ----------------------
  * Rank r owns a contiguous column stripe [lo_r, lo_{r+1}) of the bucket (cut
- * before 256-B aligned vector tiles, equal shares of the elements).  A round
- * (fa_reduce_striped):
- *   1. grouped ncclSend/ncclRecv move every client's values for stripe r to
- *      rank r (n_local * (W-1)/W of a bucket out per rank: the price of
- *      exactness on device-resident inputs);
- *   2. each rank reduces its stripe over all n_total clients in the exact
- *      torch order (every tile keeps its column's order);
- *   3. the finished stripes travel to the root (root >= 0) or to every rank;
+ * before 256-B aligned vector tiles, equal shares of the elements), cut in
+ * turn into nchunks column chunks.  A round (fa_reduce_striped), r06:
+ *   1. per chunk c, ONE RCCL group with every peer: each rank sends every
+ *      local client's values for chunk c of every other rank's stripe and
+ *      receives every other rank's clients' values for chunk c of its own
+ *      (n_local * (W-1)/W of a bucket out per rank over the round, spread
+ *      over all W-1 links at once — r02-r05 exchanged with one partner per
+ *      group, one link at a time);
+ *   2. each rank reduces chunk c of its stripe over all n_total clients in
+ *      the exact torch order (every tile keeps its column's order), on the
+ *      caller's stream, while the group of chunk c+1 is in flight;
+ *   3. the finished chunk c travels to the root (root >= 0) or to every rank
+ *      in the group of chunk c+2 (beside that chunk's client exchange);
  *   int64 keys as in e1.  The result is bit-identical to one GPU's
- *   fa_reduce over all clients.  Unweighted only (io.weights must be NULL).
+ *   fa_reduce over all clients.  Weighted rounds (r06): each rank sends its
+ *   clients' values pre-multiplied by their weights, rounded as the weighted
+ *   kernel rounds the product (one staging pass over the columns it sends:
+ *   a plan-owned buffer of n_local buckets, allocated by the first weighted
+ *   round), and reduces its own clients with their weights and the received
+ *   rows with weight 1 — the same bits as one GPU's weighted fa_reduce.
  * Same counts / io conventions as the sharded plan; the plan owns a receive
- * buffer of n_total stripe rows. */
+ * buffer of n_total stripe rows.  fa_stripe_plan_create: nchunks 0 (= 4);
+ * _ex takes it (1..FA_COMM_MAX_CHUNKS, 0 = 4). */
 typedef struct fa_stripe_plan fa_stripe_plan;
 int fa_stripe_plan_create(fa_comm *comm, const fa_seg *seg32, int nseg32,
                           int64_t f32_numel, const fa_seg *seg64, int nseg64,
                           int64_t i64_numel, const int *counts, unsigned flags,
                           fa_stripe_plan **out);
+int fa_stripe_plan_create_ex(fa_comm *comm, const fa_seg *seg32, int nseg32,
+                             int64_t f32_numel, const fa_seg *seg64, int nseg64,
+                             int64_t i64_numel, const int *counts, int nchunks,
+                             unsigned flags, fa_stripe_plan **out);
 int fa_stripe_plan_destroy(fa_stripe_plan *plan);
 int fa_reduce_striped(fa_stripe_plan *const *plans, int nlocal,
                       const fa_shard_io *io, int root);
@@ -284,6 +339,8 @@ int fa_reduce_blocked(fa_block_plan *const *plans, int nlocal,
 #define FA_X_K_CONT 25        /* blocked: continue PIN over rows row0.. -> CONT    */
 #define FA_X_K_BLOCK 26       /* blocked: block sum of local rows -> BSUM[dst_index] */
 #define FA_X_K_FOLD 27        /* blocked: fold BLK[0..nrows) of this stripe       */
+#define FA_X_K_SCALE 28       /* striped, weighted: WSTAGE[j] = fp32(client j * w_j)
+                                 over [offset, +count), local rows 0..nrows-1    */
 
 #define FA_B_NONE 0
 #define FA_B_CLIENT 1         /* local client src_index's fp32 bucket            */
@@ -301,6 +358,7 @@ int fa_reduce_blocked(fa_block_plan *const *plans, int nlocal,
 #define FA_B_BSUM 14          /* blocked: local block sum `index`                */
 #define FA_B_BLK 15           /* blocked: owner's stripe of block `index`        */
 #define FA_B_RELAY 16         /* blocked: owner's relay of rank `index`'s partial */
+#define FA_B_WSTAGE 17        /* striped, weighted: local client `index` pre-multiplied */
 
 typedef struct fa_xfer {
   int32_t step;
@@ -322,6 +380,49 @@ int fa_describe_round(int mode, int nranks, int rank, const int *counts,
                       const fa_seg *seg64, int nseg64, int64_t i64_numel,
                       int nchunks, int exchange, unsigned flags, int root,
                       int weighted, fa_xfer *ops, int cap, int *nops);
+
+/* ---- the round cost model (r06), host only ---------------------------------
+ * Every rank's schedule (fa_describe_round) timed by a discrete-event replay
+ * of the executor's rules: per rank a communication stream and the caller's
+ * (compute) stream; a step's exchanges are one group, posted on the
+ * communication stream once the compute-stream work it reads is done, and
+ * complete when every peer has posted the matching operations; kernels that
+ * read exchanged data run on the stream the executor puts them on, after the
+ * exchanges they read.  Costs:
+ *   a group: FA_MODEL_GROUP_US + max(the largest byte count on any one link
+ *            direction of this rank / FA_MODEL_LINK_GBPS,
+ *            the bytes its DMA moves in and out of HBM / FA_MODEL_HBM_GBPS),
+ *            from the moment the last of its peers posted;
+ *   a kernel: FA_MODEL_KERNEL_US + its HBM bytes / FA_MODEL_HBM_GBPS (reads
+ *            and writes of the op's columns: rows read + planes written);
+ *   collectives: ring traffic ((W-1)/W of the range per link direction, x2
+ *            for an all-reduce, (W-1) x the range for an all-gather of
+ *            per-rank rows; a broadcast the range), in and out of HBM.
+ * The link rate is an assumption of this build until a multi-GPU node has
+ * measured it (MI355X xGMI: 7 links per GPU, a full mesh of 8); the HBM rate
+ * is this chip's measured float4 copy ceiling; the latencies
+ * are round numbers for one RCCL group launch and one kernel launch's ramp
+ * and drain.  bench.py --gpus N prints each form's modelled time beside its
+ * measured time, so the first 8-GPU run checks the model.
+ * fa_round_model: the round's modelled time (max over ranks, us), the
+ * largest byte count on one link direction over the round (any rank, any
+ * peer), the largest per-rank HBM byte count, and the busiest rank's group
+ * count.  Errors as fa_describe_round. */
+#define FA_MODEL_LINK_GBPS 64.0    /* GB/s per xGMI link direction (assumed)   */
+#define FA_MODEL_HBM_GBPS 6500.0   /* GB/s: measured float4 copy ceiling       */
+#define FA_MODEL_GROUP_US 15.0     /* one RCCL group: launch + completion      */
+#define FA_MODEL_KERNEL_US 3.0     /* one kernel: launch gap + ramp / drain    */
+typedef struct fa_round_cost {
+  double model_us;
+  double link_bytes_max;
+  double hbm_bytes_max;
+  int32_t groups;
+  int32_t steps;
+} fa_round_cost;
+int fa_round_model(int mode, int nranks, const int *counts, const fa_seg *seg32,
+                   int nseg32, int64_t f32_numel, const fa_seg *seg64, int nseg64,
+                   int64_t i64_numel, int nchunks, int exchange, unsigned flags,
+                   int root, int weighted, fa_round_cost *out);
 
 #ifdef __cplusplus
 }

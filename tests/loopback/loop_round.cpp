@@ -27,6 +27,9 @@
 // One JSON line per case; exit status 0 iff every case passed.
 // FA_LOOP_DUMP=path: the first result rank's out32 then out64, raw, of the
 // last case.
+// FA_LOOP_PROFILE=1 (threads model): every rank's communicator profiles its
+// round (fa_comm_set_profile) and the line carries rank 0's
+// fa_round_plan_profile.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -127,6 +130,8 @@ struct Rank {
   std::vector<const int64_t*> c64;
   int rc = 0;
   std::string err;
+  fa_round_profile prof{};
+  bool has_prof = false;
 };
 
 int create_plan(const Case& c, const Layout& L, Rank& r) {
@@ -143,9 +148,9 @@ int create_plan(const Case& c, const Layout& L, Rank& r) {
                                 (int)L.s64.size(), L.i64_numel, c.counts.data(), c.nchunks, fl,
                                 (fa_chain_plan**)&r.plan);
   if (c.mode == "striped")
-    return fa_stripe_plan_create(r.comm, L.s32.data(), (int)L.s32.size(), L.f32_numel, s64,
-                                 (int)L.s64.size(), L.i64_numel, c.counts.data(), fl,
-                                 (fa_stripe_plan**)&r.plan);
+    return fa_stripe_plan_create_ex(r.comm, L.s32.data(), (int)L.s32.size(), L.f32_numel, s64,
+                                    (int)L.s64.size(), L.i64_numel, c.counts.data(), c.nchunks,
+                                    fl, (fa_stripe_plan**)&r.plan);
   if (c.mode == "blocked")
     return fa_block_plan_create(r.comm, L.s32.data(), (int)L.s32.size(), L.f32_numel, s64,
                                 (int)L.s64.size(), L.i64_numel, c.counts.data(), fl,
@@ -278,6 +283,8 @@ bool run_case(const Case& c, const Layout& L) {
           k.rc = fa_comm_init_rank(W, r, uid, FA_COMM_UID_BYTES, &k.comm);
           // the loopback pairs sends and receives on the host: never captured
           if (!k.rc) k.rc = fa_comm_set_graphs(k.comm, 0);
+          const bool prof = getenv("FA_LOOP_PROFILE") && atoi(getenv("FA_LOOP_PROFILE"));
+          if (!k.rc && prof) k.rc = fa_comm_set_profile(k.comm, 1);
           if (!k.rc) k.rc = create_plan(c, L, k);
           if (!k.rc) k.rc = hipStreamCreate(&k.st) == hipSuccess ? 0 : -1;
           if (!k.rc) {
@@ -286,6 +293,10 @@ bool run_case(const Case& c, const Layout& L) {
             std::vector<fa_shard_io> io{k.io};
             std::vector<Rank*> rk{&k};
             k.rc = run_round(c, L, rk, plans, io);
+            if (!k.rc && prof && k.plan) {
+              k.rc = fa_round_plan_profile(k.plan, &k.prof);
+              k.has_prof = k.rc == 0;
+            }
           }
           if (k.rc) k.err = fa_last_error();
           if (k.st) (void)hipStreamSynchronize(k.st);
@@ -399,10 +410,18 @@ bool run_case(const Case& c, const Layout& L) {
   }
   const bool ok = !failed && bad32 == 0 && bad64 == 0 && checked > 0;
   if (err.empty()) err = where;
+  char pbuf[256] = "null";
+  if (R[0].has_prof)
+    snprintf(pbuf, sizeof pbuf,
+             "{\"exchange_us\": %.2f, \"comm_kernel_us\": %.2f, \"compute_kernel_us\": %.2f, "
+             "\"wall_us\": %.2f, \"groups\": %d, \"kernels\": %d}",
+             R[0].prof.exchange_us, R[0].prof.comm_kernel_us, R[0].prof.compute_kernel_us,
+             R[0].prof.wall_us, R[0].prof.groups, R[0].prof.kernels);
   printf("{\"case\": \"%s\", \"ok\": %s, \"n\": %d, \"result_ranks\": %lld, \"bad_f32\": %lld, "
-         "\"bad_i64\": %lld, \"check\": \"%s\", \"worst_err_over_bound\": %.4g, \"error\": \"%s\"}\n",
+         "\"bad_i64\": %lld, \"check\": \"%s\", \"worst_err_over_bound\": %.4g, \"error\": \"%s\", "
+         "\"profile\": %s}\n",
          c.text.c_str(), ok ? "true" : "false", n, checked, bad32, bad64,
-         exact ? "bit-exact" : "error bound", worst, err.c_str());
+         exact ? "bit-exact" : "error bound", worst, err.c_str(), pbuf);
   fflush(stdout);
 
   for (int r = 0; r < W; ++r) {

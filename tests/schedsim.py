@@ -16,6 +16,13 @@ So the multi-rank logic of the native library — cut points, peers, offsets,
 receive rows, state planes, roots — is exercised at any world size without
 RCCL or a GPU.  Only the arithmetic of the kernels is substituted, and that
 is pinned by the GPU tests.
+
+r06: the executor's stream rules are checked too.  A compute-stream kernel
+that reads exchanged data (the striped round's chunk reduce, fedcomm.hip
+reads_exchanged) runs concurrently with its own step's group: it must not
+read what that group receives, nor write what that group sends or receives;
+and a step's sends must not read what the same step's kernels write (they
+run after the group).  A violation raises Hazard.
 """
 from __future__ import annotations
 
@@ -31,6 +38,14 @@ COMM = {"SEND", "RECV", "REDUCE", "ALLREDUCE", "REDUCE_SCATTER", "GATHER", "ALLG
 
 class Deadlock(AssertionError):
     pass
+
+
+class Hazard(AssertionError):
+    pass
+
+
+# kernels the executor runs on the caller's (compute) stream
+USER_KERNELS = {"K_SUM", "K_ZERO", "K_STACK", "K_PART", "K_BLOCK", "K_SCALE", "K_STRIPE"}
 
 
 def _column_sum(kind, rows):
@@ -89,7 +104,9 @@ class Sim:
                  "CONT": [np.full(N32, np.nan, F32) for _ in range(4)],
                  "BSUM": defaultdict(lambda: np.full(N32, np.nan, F32)),
                  "BLK": defaultdict(lambda: np.full(N32, np.nan, F32)),
-                 "RELAY": defaultdict(lambda: np.full(N32, np.nan, F32))}
+                 "RELAY": defaultdict(lambda: np.full(N32, np.nan, F32)),
+                 # striped, weighted: pre-multiplied local clients
+                 "WSTAGE": defaultdict(lambda: np.full(N32, np.nan, F32))}
             self.buf.append(b)
 
     # ------------------------------------------------------------ buffers --
@@ -101,7 +118,7 @@ class Sim:
             return b[name][off:off + cnt]
         if name == "RECV":
             return b["RECV"][index][off:off + cnt]
-        if name in ("STATE", "PIN", "TAILP", "CONT", "BSUM", "BLK", "RELAY"):
+        if name in ("STATE", "PIN", "TAILP", "CONT", "BSUM", "BLK", "RELAY", "WSTAGE"):
             return b[name][index][off:off + cnt]
         if name in ("STACK", "GATHER"):
             return b[name][index][off:off + cnt]
@@ -139,15 +156,22 @@ class Sim:
             self._view(r, x["dst"], x["dst_index"], x["offset"], x["count"])[:] = \
                 self._view(r, x["src"], x["src_index"], x["offset"], x["count"])
         elif op == "K_STRIPE":
+            # local clients from their buckets (times their weights), the
+            # others from their receive rows (pre-multiplied when weighted)
             for st, cnt, kind in self._tiles_in(x["offset"], x["count"]):
                 rows = []
                 for s in range(self.n):
                     if self.first[r] <= s < self.first[r] + n_loc:
-                        rows.append(self.c32[s][st:st + cnt])
+                        rows.append(val(s, st, cnt))
                     else:
                         rows.append(b["RECV"][s][st:st + cnt])
-                res = _column_sum(kind, rows)
-                b["STRIPE"][st:st + cnt] = (F32(0) + res) / F32(self.n)
+                res = (F32(0) + _column_sum(kind, rows)).astype(F32)
+                b[x["dst"]][st:st + cnt] = res if wt is not None else res / F32(self.n)
+        elif op == "K_SCALE":
+            off, cnt = x["offset"], x["count"]
+            for j in range(x["nrows"]):
+                s = self.first[r] + j
+                b["WSTAGE"][j][off:off + cnt] = (self.c32[s][off:off + cnt] * wt[s]).astype(F32)
         elif op == "K_CHAIN":
             row0, nr = x["row0"], x["nrows"]
             lin = O.chain_levels(row0, self.n)
@@ -295,6 +319,48 @@ class Sim:
         else:
             raise AssertionError(op)
 
+    # ------------------------------------------------------------ hazards --
+    def _regions_read(self, x):
+        """(buffer, index, lo, hi) a kernel reads, as far as the hazard check
+        needs (exchanged buffers only)."""
+        if x["op"] == "K_STRIPE":
+            return [("RECV", s, x["offset"], x["offset"] + x["count"]) for s in range(self.n)]
+        return []
+
+    def _regions_written(self, x):
+        if x["op"] in COMM or x["dst"] in ("NONE",):
+            return []
+        if x["count"] <= 0:
+            return [(x["dst"], None, 0, 1 << 62)]
+        return [(x["dst"], x["dst_index"] if x["dst"] not in ("OUT", "STRIPE", "FIN", "PARTIAL")
+                 else None, x["offset"], x["offset"] + x["count"])]
+
+    @staticmethod
+    def _overlap(a, b):
+        return a[0] == b[0] and (a[1] is None or b[1] is None or a[1] == b[1]) and \
+            a[2] < b[3] and b[2] < a[3]
+
+    def _hazards(self, r, grp):
+        recv_w = [(x["dst"], x["dst_index"] if x["dst"] not in ("OUT", "STRIPE", "FIN") else None,
+                   x["offset"], x["offset"] + x["count"]) for x in grp if x["op"] == "RECV"]
+        send_r = [(x["src"], x["src_index"] if x["src"] not in ("OUT", "STRIPE", "FIN") else None,
+                   x["offset"], x["offset"] + x["count"]) for x in grp if x["op"] == "SEND"]
+        for x in grp:
+            if x["op"] in COMM:
+                continue
+            wr = self._regions_written(x)
+            for a in wr:            # the step's sends ran before this kernel
+                for b in send_r:
+                    if self._overlap(a, b):
+                        raise Hazard(f"rank {r} step {x['step']}: {x['op']} writes {a} "
+                                     f"which the same step's send {b} reads")
+            if x["op"] in USER_KERNELS:   # concurrent with the step's group
+                for a in self._regions_read(x) + wr:
+                    for b in recv_w:
+                        if self._overlap(a, b):
+                            raise Hazard(f"rank {r} step {x['step']}: {x['op']} touches {a} "
+                                         f"while the same step's group receives {b}")
+
     def run(self, scheds):
         """``scheds[r]``: rank r's op list (comm.describe).  Runs to the end
         or raises Deadlock."""
@@ -367,6 +433,7 @@ class Sim:
                 ok = all((id(e) in matched) if kind == "p2p" else (e in done_coll)
                          for kind, e in posted[r])
                 if ok:
+                    self._hazards(r, grp)
                     for x in grp:
                         if x["op"] not in COMM:
                             self._kernel(r, x)

@@ -89,3 +89,24 @@ def test_parse_smi_reads_clocks_power_and_temperatures():
                   "socket_power_w": 812.0, "junction_c": 46.0, "memory_c": 33.0,
                   "vram_used_pct": 81.0, "serial": "692533015330"}
     assert "error" in bench.parse_smi("no json here")
+
+
+def test_multi_env_fields(monkeypatch):
+    """The N>1 line's environment block: the RCCL /
+    NCCL / HSA / HIP variables of the process, the communicator's view, the
+    peer-access matrix of the visible devices and the cost model's
+    constants — what the first real multi-GPU run needs to be read."""
+    class FakeComm:
+        def info(self):
+            return 8, 3, 3
+    monkeypatch.setenv("NCCL_DEBUG", "WARN")
+    monkeypatch.setenv("RCCL_MSCCL_ENABLE", "0")
+    monkeypatch.setenv("UNRELATED_VAR", "x")
+    e = bench.multi_env(FakeComm(), 8)
+    assert e["env"]["NCCL_DEBUG"] == "WARN" and e["env"]["RCCL_MSCCL_ENABLE"] == "0"
+    assert "UNRELATED_VAR" not in e["env"]
+    assert (e["comm_count"], e["comm_rank"], e["comm_device"], e["world"]) == (8, 3, 3, 8)
+    n = e["visible_devices"]
+    assert len(e["peer_access"]) == n and all(len(row) == n for row in e["peer_access"])
+    mc = e["model_constants"]
+    assert mc["link_GBps"] > 0 and mc["hbm_GBps"] > 0 and mc["group_us"] >= 0

@@ -137,19 +137,22 @@ def test_shard_range_and_chunks():
 
 # ------------------------------------------------ exact striped mode (e2) --
 class OracleStripeBackend:
-    """Per-column oracle over whatever columns a stripe holds: the order a
-    column needs depends only on its position inside its tensor."""
+    """Per-column oracle over whatever columns a stripe chunk holds: the
+    order a column needs depends only on its position inside its tensor.
+    Weighted (n_total weights): the weighted order, no division."""
 
-    def __init__(self, layout, lo, hi):
-        self.layout, self.lo, self.hi = layout, lo, hi
+    def __init__(self, layout, lo=None, hi=None):
+        self.layout = layout
 
-    def reduce_stripe(self, sources, out32):
+    def reduce_chunk(self, c, lo, hi, sources, out32, weights=None):
         n = len(sources)
         for o, M in self.layout.segs32:
-            a, b = max(o, self.lo), min(o + M, self.hi)
+            a, b = max(o, lo), min(o + M, hi)
             if a >= b:
                 continue
             x = np.stack([t[a - base:b - base].numpy() for t, base in sources])
+            if weights is not None:
+                x = (x * np.asarray(weights, np.float32)[:, None]).astype(np.float32)
             body = O.body_len(M)
             res = np.empty(b - a, np.float32)
             for j, e in enumerate(range(a, b)):
@@ -160,7 +163,8 @@ class OracleStripeBackend:
                     s = O.cascade(col)[0]
                 else:
                     s = O.ilp4(col)[0]
-                res[j] = np.float32(np.float32(0) + np.float32(s)) / np.float32(n)
+                s = np.float32(np.float32(0) + np.float32(s))
+                res[j] = s if weights is not None else s / np.float32(n)
             out32[a:b] = torch.from_numpy(res)
 
     def reduce_i64(self, clients64, out):
@@ -169,40 +173,45 @@ class OracleStripeBackend:
             out[o:o + m] = torch.from_numpy(O.mean_i64_trunc(x))
 
 
-def _striped_worker(rank, world, port, n_total, host, q, final="allreduce"):
+def _striped_worker(rank, world, port, n_total, host, q, final="allreduce", weighted=False,
+                    nchunks=4):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from feddct_amd.dist import StripedAggregator
-    from feddct_amd.partition import layout_tiles, split_tiles
     layout = BucketLayout.from_manifest(MAN)
     out32 = torch.full((layout.f32_numel,), float("nan"))
     out64 = torch.zeros(max(1, layout.i64_numel), dtype=torch.int64)
-    info, tiles = layout_tiles(layout)
-    lo, hi, _ = split_tiles(tiles, world, layout.f32_numel)[rank]
-    agg = StripedAggregator(layout, n_total, out32, out64,
-                            backend=OracleStripeBackend(layout, lo, hi), final=final)
+    agg = StripedAggregator(layout, n_total, out32, out64, backend=OracleStripeBackend(layout),
+                            final=final, nchunks=nchunks)
     if host:
+        lo, hi = agg.lo, agg.hi
         allb = [_bucket(layout, synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL))
                 for c in range(n_total)]
         agg.step_host([b[0][lo:hi].clone() for b in allb], [b[1] for b in allb])
     else:
         a, b = shard_range(n_total, world, rank)
         bk = [_bucket(layout, synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL)) for c in range(a, b)]
-        agg.step_device([x[0] for x in bk], [x[1] for x in bk])
+        w = O.weights_from_sizes(np.arange(1, n_total + 1) * 3 + 2) if weighted else None
+        agg.step_device([x[0] for x in bk], [x[1] for x in bk],
+                        None if w is None else w[a:b])
     q.put((rank, out32.numpy().copy(), out64.numpy().copy()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_total,host,final", [(2, 20, False, "allreduce"),
-                                                    (3, 7, False, "allreduce"),
-                                                    (2, 9, True, "allreduce"),
-                                                    (3, 7, False, "reduce")])
-def test_striped_round_is_exact_gloo(world, n_total, host, final):
+@pytest.mark.parametrize("world,n_total,host,final,weighted,nchunks", [
+    (2, 20, False, "allreduce", False, 4), (3, 7, False, "allreduce", False, 2),
+    (2, 9, True, "allreduce", False, 4), (3, 7, False, "reduce", False, 1),
+    (3, 8, False, "reduce", True, 3), (2, 5, False, "allreduce", True, 4)])
+def test_striped_round_is_exact_gloo(world, n_total, host, final, weighted, nchunks):
+    """The Python StripedAggregator over real torch.distributed (gloo), r06:
+    per column chunk one batch with every peer (the native schedule), weighted
+    rounds too — every result rank ends with the single-process bits."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_striped_worker, args=(r, world, port, n_total, host, q, final))
+    procs = [ctx.Process(target=_striped_worker, args=(r, world, port, n_total, host, q, final,
+                                                       weighted, nchunks))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -212,7 +221,14 @@ def test_striped_round_is_exact_gloo(world, n_total, host, final):
         assert p.exitcode == 0
     layout = BucketLayout.from_manifest(MAN)
     states = [synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL) for c in range(n_total)]
-    exact = dict(O.aggregate_state(states))
+    if weighted:
+        w = O.weights_from_sizes(np.arange(1, n_total + 1) * 3 + 2)
+        exact = {}
+        for j, (k, v0) in enumerate(states[0]):
+            x = np.stack([np.asarray(st[j][1]) for st in states])
+            exact[k] = O.mean_i64_trunc(x) if x.dtype == np.int64 else O.weighted_sum0(x, w)
+    else:
+        exact = dict(O.aggregate_state(states))
     for rk, o32, o64 in res:  # every rank (or the root) holds the full, exact state
         if final == "reduce" and rk != 0:
             continue

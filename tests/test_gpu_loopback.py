@@ -69,11 +69,13 @@ def _digest_params(layout, parts):
     return p32, p64
 
 
-def _run(layout, cases, tmp_path, timeout=240, params=None, dump=None):
+def _run(layout, cases, tmp_path, timeout=240, params=None, dump=None, profile=False):
     assert os.path.exists(DRIVER), "tests/loopback/loop_round is not built (run build())"
     lf = str(tmp_path / "layout.txt")
     _write_layout(layout, lf, params)
     env = dict(os.environ, FA_LOOP_TIMEOUT_S="30")
+    if profile:
+        env["FA_LOOP_PROFILE"] = "1"
     if dump:
         env["FA_LOOP_DUMP"] = dump
     p = subprocess.run([DRIVER, lf, *cases], capture_output=True, text=True, timeout=timeout,
@@ -116,6 +118,12 @@ def test_loopback_small_layout_all_modes(tmp_path):
         "striped:3:2,0,3:-1:threads:0:0",
         "striped:8:1,2,1,3,1,1,2,9:5:threads:0:0",
         "striped:4:65,65,65,65:-1:threads:0:0",          # N=260: device pointer tables
+        # r06: every peer in one group per chunk; chunk counts; weighted
+        "striped:8:3,3,3,3,3,3,3,3:7:threads:0:1",
+        "striped:8:3,3,3,3,3,3,3,3:-1:threads:1:3",
+        "striped:5:4,0,2,1,6:2:threads:1:8",
+        "striped:3:2,5,1:-1:threads:1:2",
+        "striped:4:65,65,65,65:0:threads:1:4",           # weighted, N=260
         "sharded:4:65,65,65,65:0:threads:1:4",
         "sharded:2:3,2:0:threads:0:8",
         "sharded:4:5,0,2,1:-1:threads:1:4",
@@ -133,10 +141,9 @@ def test_loopback_small_layout_all_modes(tmp_path):
         "blocked:6:12,9,30,0,14,8:4:threads:0:0",
         "blocked:3:100,156,44:-1:threads:0:0",            # N=300: the fold's level 2
         # r05: the default entry picks the exact form from the counts
-        "multi:8:1,2,1,3,1,1,2,9:-1:threads:0:0",          # -> chained
-        "multi:3:7,0,13:-1:threads:1:0",                   # -> blocked
-        "multi:2:10,10:0:single:0:0",                      # -> blocked, one thread
-        "multi:4:65,65,65,65:3:threads:1:0",               # N=260 -> chained, 4 planes
+        "multi:8:1,2,1,3,1,1,2,9:-1:threads:0:0",
+        "multi:3:7,0,13:-1:threads:1:0",
+        "multi:4:65,65,65,65:3:threads:1:0",               # N=260
         "multi_e1:4:5,0,2,1:-1:threads:1:4",               # opt-in e1: error bound
         "mean_multi:3:4,5,3:2:threads:0:0",                # stateless fp32 form
         "mean_multi:8:3,3,3,3,3,3,3,3:-1:threads:0:0",
@@ -153,6 +160,8 @@ def test_loopback_cfg3_layout(cfg3_layout, tmp_path):
         "chained:3:2,1,2:0:threads:1:4",
         "striped:2:3,2:1:threads:0:0",
         "striped:4:2,1,1,1:-1:threads:0:0",
+        "striped:5:1,1,1,1,1:4:threads:0:4",
+        "striped:5:1,1,1,1,1:-1:threads:1:2",
         "sharded:2:3,2:0:threads:0:8",
         "sharded_rs:4:2,1,1,1:-1:threads:1:8",
         "blocked:2:3,2:0:threads:0:0",
@@ -163,11 +172,15 @@ def test_loopback_cfg3_layout(cfg3_layout, tmp_path):
 
 def test_loopback_cfg5_sharded_chain(tmp_path):
     """BASELINE config 5's shape: 24 FedDCT slots (wrnsl16_8 sf4 C100) over
-    8 ranks of 3 slots, chained to the last rank and to every rank."""
+    8 ranks of 3 slots, chained to the last rank and to every rank, and
+    striped (r06: every peer in one group per chunk) in 1 and 4 chunks,
+    weighted too."""
     mm, pm = load_manifest("wrnsl16_8_sf4_c100_main"), load_manifest("wrnsl16_8_sf4_c100_proxy")
     lay = BucketLayout.from_manifest(joint_manifest([mm, pm]))
     cases = ["chained:8:3,3,3,3,3,3,3,3:7:threads:0:8",
-             "chained:8:3,3,3,3,3,3,3,3:-1:threads:0:8"]
+             "chained:8:3,3,3,3,3,3,3,3:-1:threads:0:8",
+             "striped:8:3,3,3,3,3,3,3,3:-1:threads:0:4",
+             "striped:8:3,3,3,3,3,3,3,3:7:threads:1:1"]
     _run(lay, cases, tmp_path, timeout=300)
 
 
@@ -190,11 +203,12 @@ def test_loopback_cfg5_default_entry_matches_reference_digest(tmp_path):
     rank's main and proxy halves hash to the digests the REFERENCE's own
     server_aggregate produced (tests/golden/digests.json, n24), and equal one
     GPU's reduction bit for bit.  With 3 slots per rank a 16-slot cascade
-    block spans 6 ranks, so the entry must take the chained round."""
+    block spans 6 ranks (no blocked round); r06: the cost model takes the
+    link-parallel striped round (r05: chained)."""
     from feddct_amd import dist
     mm, pm = load_manifest("wrnsl16_8_sf4_c100_main"), load_manifest("wrnsl16_8_sf4_c100_proxy")
     lay = BucketLayout.from_manifest(joint_manifest([mm, pm]))
-    assert dist.exact_form([3] * 8) == "chained"
+    assert dist.exact_form([3] * 8, lay) == "striped"
     params = _digest_params(lay, [(mm, "0."), (pm, "1.")])
     dump = str(tmp_path / "out.bin")
     rows = _run(lay, ["multi:8:3,3,3,3,3,3,3,3:7:threads:0:0"], tmp_path, timeout=300,
@@ -219,7 +233,7 @@ def test_loopback_cfg5_default_entry_matches_reference_digest(tmp_path):
 def test_loopback_default_entry_random_shards(tmp_path):
     """The default entry over seeded random shard shapes (W = 2..8, 0..40
     slots per rank, empty ranks, every root, weighted and not): whatever form
-    it picks (blocked or chained by the counts), the result equals one GPU's
+    and chunk count the cost model picks, the result equals one GPU's
     reduction of all the slots bit for bit."""
     from feddct_amd import dist
     rng = np.random.default_rng(20260518)
@@ -232,8 +246,38 @@ def test_loopback_default_entry_random_shards(tmp_path):
             continue
         holders = [r for r, c in enumerate(counts) if c]
         root = int(rng.choice(holders + [-1]))
-        forms.add(dist.exact_form(counts))
+        forms.add(dist.exact_form(counts, _small_layout(), root_all=root < 0))
         cases.append(f"multi:{w}:{','.join(map(str, counts))}:{root}:threads:"
                      f"{int(rng.random() < 0.5)}:0")
-    assert forms == {"blocked", "chained"}, forms
+    print("forms", sorted(forms))
     _run(_small_layout(), cases, tmp_path, timeout=300)
+
+
+def test_loopback_default_entry_each_form(tmp_path):
+    """The default entry's three exact forms each run at least once on the
+    loopback: shapes the model sends to blocked, to chained and to striped
+    (on a layout where a long chain of small hops loses to the stripes and
+    the blocks win for many slots per rank)."""
+    from feddct_amd import dist
+    lay = BucketLayout([("a", (300000,), "float32"), ("s", (), "float32"),
+                        ("b", (4101,), "float32"), ("n1", (), "int64")])
+    shapes = {"striped": [3] * 8, "blocked": [20] * 4, "chained": [60, 60]}
+    for form, counts in shapes.items():
+        assert dist.exact_form(counts, lay) == form, (form, dist.exact_form(counts, lay))
+    cases = [f"multi:{len(c)}:{','.join(map(str, c))}:{len(c) - 1}:threads:{i % 2}:0"
+             for i, c in enumerate(shapes.values())]
+    _run(lay, cases, tmp_path, timeout=300)
+
+
+def test_loopback_round_profiles(tmp_path):
+    """fa_comm_set_profile / fa_round_plan_profile (r06):
+    a profiled round of each exact form reports its RCCL groups, its kernels
+    and its wall time (rank 0 of the loopback), and stays bit-exact."""
+    cases = ["striped:4:3,3,3,3:-1:threads:0:2", "chained:4:3,3,3,3:3:threads:0:4",
+             "blocked:2:10,10:0:threads:1:0", "multi:8:3,3,3,3,3,3,3,3:7:threads:0:0"]
+    rows = _run(_small_layout(), cases, tmp_path, profile=True)
+    for r in rows:
+        p = r["profile"]
+        assert p is not None, r
+        assert p["groups"] > 0 and p["kernels"] > 0 and p["wall_us"] > 0, r
+        assert p["exchange_us"] > 0, r

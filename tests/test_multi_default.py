@@ -1,9 +1,12 @@
-"""The default multi-GPU entry is exact, on a CPU:
+"""The default multi-GPU entry is exact and picks its
+form by a cost model (r06), on a CPU:
 
-* the form it takes (native fa_multi_select) agrees with the Python rule
-  (dist.exact_form) and with the blocked round's own refusal (block_geo:
-  fa_describe_round of the blocked mode fails exactly where the rule says
-  "chained");
+* the native model (fa_round_model) equals its Python restatement
+  (tests/roundmodel.py) on every form and shard shape tried, and the native
+  choice (fa_multi_select_layout) is the argmin of the restated model over
+  the candidate forms and chunk counts; the blocked form is chosen only
+  where its precondition holds (dist.blocked_allowed = block_geo's own
+  refusal), and the Python rule (dist.exact_form) names the same form;
 * the schedule of the selected form, replayed for all ranks at once
   (tests/schedsim.py, the oracle as arithmetic), gives the single-process
   reference's bits — including BASELINE config 5's 8 x 3 shape;
@@ -23,14 +26,18 @@ import torch.multiprocessing as mp
 
 from feddct_amd import comm as C
 from feddct_amd import synth
-from feddct_amd.dist import exact_form
+import roundmodel as RM
+from feddct_amd.dist import blocked_allowed, exact_form
 from feddct_amd.layout import BucketLayout
 from feddct_amd.partition import layout_tiles
 from oracle import torch_order as O
 from schedsim import Sim
 from test_schedule import MAN, _buckets, _expected, _result_ranks
 
-MODES = {"blocked": C.FA_MODE_BLOCKED, "chained": C.FA_MODE_CHAINED, "e1": C.FA_MODE_SHARDED}
+MODES = {"blocked": C.FA_MODE_BLOCKED, "chained": C.FA_MODE_CHAINED, "e1": C.FA_MODE_SHARDED,
+         "striped": C.FA_MODE_STRIPED}
+CANDIDATES = [("blocked", 1)] + [("chained", k) for k in (4, 8, 16, 32)] + \
+    [("striped", k) for k in (1, 2, 4, 8)]
 
 
 def _random_counts(rng, n):
@@ -43,16 +50,15 @@ def _random_counts(rng, n):
     return out
 
 
-def test_select_matches_python_rule_and_block_geo():
+def test_blocked_precondition_matches_block_geo():
+    """dist.blocked_allowed is exactly where the blocked round's own geometry
+    (block_geo) accepts the counts."""
     rng = random.Random(5)
     layout = BucketLayout.from_manifest(MAN)
     seen = set()
-    for counts in _random_counts(rng, 400) + [[3] * 8, [20] * 8, [24], [1, 23], [16, 16, 1]]:
-        form = C.multi_select(counts)
-        assert form == exact_form(counts), counts
-        assert C.multi_select(counts, exact=False) == "e1"
-        seen.add(form)
-        # the blocked round refuses exactly the counts the rule sends to the chain
+    for counts in _random_counts(rng, 300) + [[3] * 8, [20] * 8, [24], [1, 23], [16, 16, 1]]:
+        allowed = blocked_allowed(counts)
+        seen.add(allowed)
         for r in range(len(counts)):
             try:
                 C.describe(C.FA_MODE_BLOCKED, layout, counts, r)
@@ -60,18 +66,104 @@ def test_select_matches_python_rule_and_block_geo():
             except Exception as e:  # noqa: BLE001
                 assert "more than two" in str(e), e
                 ok = False
-            assert ok == (form == "blocked") or len(counts) == 1, (counts, r)
-    assert seen == {"blocked", "chained"}
+            assert ok == allowed or len(counts) == 1, (counts, r)
+    assert seen == {True, False}
+
+
+def _restated(layout, counts, mode, nchunks, root, weighted=False):
+    _, tiles = layout_tiles(layout)
+    V = int(tiles[tiles[:, 2] == 0][:, 1].sum())
+    scheds = [C.describe(MODES[mode], layout, counts, r, nchunks=nchunks, root=root,
+                         weighted=weighted) for r in range(len(counts))]
+    return RM.model(scheds, sum(counts), V)
+
+
+@pytest.mark.parametrize("counts", [[10, 10], [7, 0, 13], [3] * 8, [1, 1, 1, 17], [20] * 4,
+                                    [2, 30, 2, 0, 0, 1, 3, 2], [5, 6]])
+@pytest.mark.parametrize("root", [-1, "last"])
+def test_native_model_equals_its_restatement(counts, root):
+    """fa_round_model == tests/roundmodel.py on every candidate form, and
+    the native default's choice is the restated model's argmin (blocked only
+    where allowed; ties keep the earlier candidate)."""
+    W = len(counts)
+    root = max(r for r in range(W) if counts[r]) if root == "last" else root
+    layout = BucketLayout.from_manifest(MAN)
+    best = None
+    for mode, k in CANDIDATES + [("striped", 3)]:
+        if mode == "blocked" and not blocked_allowed(counts):
+            continue
+        nat = C.round_model(MODES[mode], layout, counts, nchunks=k, root=root)
+        py = _restated(layout, counts, mode, k, root)
+        for f in ("model_us", "link_bytes_max", "hbm_bytes_max"):
+            assert nat[f] == pytest.approx(py[f], rel=1e-9, abs=1e-9), (mode, k, f, nat, py)
+        assert (nat["groups"], nat["steps"]) == (py["groups"], py["steps"]), (mode, k)
+        if (mode, k) in CANDIDATES and (best is None or py["model_us"] < best[2]):
+            best = (mode, k, py["model_us"])
+    form, k, us = C.multi_select(counts, layout=layout, root_all=root < 0, detail=True)
+    assert (form, k) == best[:2], (form, k, best)
+    assert us == pytest.approx(best[2], rel=1e-9)
+    assert exact_form(counts, layout, root_all=root < 0) == form
+
+
+def test_weighted_striped_model_pays_the_staging():
+    """A weighted striped round stages the clients it sends (K_SCALE): more
+    HBM bytes than the unweighted round, same link bytes."""
+    layout = BucketLayout.from_manifest(MAN)
+    u = C.round_model(C.FA_MODE_STRIPED, layout, [3] * 4, nchunks=2, root=-1)
+    w = C.round_model(C.FA_MODE_STRIPED, layout, [3] * 4, nchunks=2, root=-1, weighted=True)
+    assert w["link_bytes_max"] == u["link_bytes_max"]
+    assert w["hbm_bytes_max"] > u["hbm_bytes_max"]
+    assert w == pytest.approx(_restated(layout, [3] * 4, "striped", 2, -1, weighted=True))
 
 
 def test_select_named_shapes():
-    assert C.multi_select([3] * 8) == "chained"        # cfg5: a block spans 6 ranks
-    assert C.multi_select([20] * 8) == "blocked"       # the bench's N>1 shape
-    assert C.multi_select([10, 10]) == "blocked"
-    assert C.multi_select([7, 0, 13]) == "blocked"     # an empty rank between two
-    assert C.multi_select([1, 1, 1, 17]) == "chained"
+    """BASELINE config 5's shape (8 ranks x 3 FedDCT slots) takes the striped
+    round: one group per chunk over all 7 links against the chained round's
+    one hop at a time; the bench's N>1 shape (8 x 20 wrn16_8 slots) the
+    blocked round.  r05 chose chained for cfg5 by geometry alone."""
+    from feddct_amd.workload import joint_manifest, load_manifest
+    cfg5 = BucketLayout.from_manifest(joint_manifest(
+        [load_manifest("wrnsl16_8_sf4_c100_main"), load_manifest("wrnsl16_8_sf4_c100_proxy")]))
+    wrn = BucketLayout.from_manifest(load_manifest("wrn16_8_c10"))
+    form, k, us = C.multi_select([3] * 8, layout=cfg5, detail=True)
+    assert form == "striped", (form, k, us)
+    ch = min(C.round_model(C.FA_MODE_CHAINED, cfg5, [3] * 8, nchunks=c, root=7)["model_us"]
+             for c in (4, 8, 16, 32))
+    assert us < ch / 2
+    assert C.multi_select([20] * 8, layout=wrn) == "blocked"
+    assert C.multi_select([3] * 8) == "striped"        # the nominal layout
+    assert C.multi_select([20] * 8) == "blocked"
+    assert C.multi_select([3] * 8, exact=False) == "e1"
+    for counts in ([10, 10], [7, 0, 13], [1, 1, 1, 17]):
+        assert C.multi_select(counts) in ("blocked", "chained", "striped")
+        if not blocked_allowed(counts):
+            assert C.multi_select(counts) != "blocked"
     with pytest.raises(Exception):
         C.multi_select([0, 0])
+
+
+def test_cfg5_striped_per_link_bytes():
+    """VERDICT r05 next 1 'done': on cfg5's 8 x 3 shape the striped round's
+    largest per-step byte count on one link is about 1/7 of what the r05
+    pairwise form put on one link per step (all of a peer's share in one
+    group per chunk vs every peer in turn)."""
+    from feddct_amd.workload import joint_manifest, load_manifest
+    cfg5 = BucketLayout.from_manifest(joint_manifest(
+        [load_manifest("wrnsl16_8_sf4_c100_main"), load_manifest("wrnsl16_8_sf4_c100_proxy")]))
+    W, counts = 8, [3] * 8
+    worst_link = worst_total = 0.0
+    for r in range(W):
+        steps = RM.per_step(C.describe(C.FA_MODE_STRIPED, cfg5, counts, r, nchunks=1, root=7), W)
+        for _, link, _ in steps:
+            worst_link = max(worst_link, link)
+        # what the same rank moves over all its links in its busiest step
+        by = {}
+        for x in C.describe(C.FA_MODE_STRIPED, cfg5, counts, r, nchunks=1, root=7):
+            if x["op"] in ("SEND", "RECV") and x["dst"] != "OUT" and x["src"] != "OUT":
+                by[(x["step"], x["op"])] = by.get((x["step"], x["op"]), 0) + 4 * x["count"]
+        worst_total = max([worst_total] + list(by.values()))
+    # one peer's share of a rank's exchange: 1/7 of its whole per-step volume
+    assert worst_link == pytest.approx(worst_total / 7, rel=0.02), (worst_link, worst_total)
 
 
 @pytest.mark.parametrize("counts", [[10, 10], [7, 0, 13], [3, 3, 3, 3, 3, 3, 3, 3],
@@ -81,14 +173,14 @@ def test_select_named_shapes():
 def test_default_form_schedule_is_exact(counts, root, weighted):
     W = len(counts)
     root = W - 1 if root == "last" else root
-    mode = MODES[C.multi_select(counts)]
     layout = BucketLayout.from_manifest(MAN)
+    form, nchunks, _ = C.multi_select(counts, layout=layout, root_all=root < 0, detail=True)
+    mode = MODES[form]
     n = sum(counts)
     states = [synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL) for c in range(n)]
     c32, c64 = _buckets(layout, states)
     w = O.weights_from_sizes(np.arange(1, n + 1) * 5 + 1) if weighted else None
     _, tiles = layout_tiles(layout)
-    nchunks = 16 if mode == C.FA_MODE_CHAINED else 1
     scheds = [C.describe(mode, layout, counts, r, nchunks=nchunks, root=root, weighted=weighted)
               for r in range(W)]
     bufs = Sim(layout, tiles, counts, c32, c64, w, root).run(scheds)
@@ -115,7 +207,7 @@ def _worker(rank, world, port, counts, final, weighted, q):
     from feddct_amd.dist import Aggregator
     from feddct_amd.partition import chain_cut
     from test_dist_gloo import MAN as GMAN
-    from test_dist_gloo import OracleChainBackend, _bucket
+    from test_dist_gloo import OracleChainBackend, OracleStripeBackend, _bucket
     layout = BucketLayout.from_manifest(GMAN)
     n = sum(counts)
     a = sum(counts[:rank])
@@ -128,7 +220,8 @@ def _worker(rank, world, port, counts, final, weighted, q):
     agg = Aggregator(layout, [x[0] for x in bk], [x[1] for x in bk], n, out32, out64,
                      final=final, counts=counts, nchunks=3,
                      weights=None if w is None else w[a:a + counts[rank]],
-                     backend=OracleChainBackend(layout, chunks, compact))
+                     backend=OracleChainBackend(layout, chunks, compact),
+                     stripe_backend=OracleStripeBackend(layout))
     agg.step()
     q.put((rank, agg.form, agg._agg.root, out32.numpy().copy(), out64.numpy().copy()))
     dist.barrier()
@@ -137,11 +230,13 @@ def _worker(rank, world, port, counts, final, weighted, q):
 
 @pytest.mark.parametrize("counts,final,weighted", [([10, 10], "reduce", False),
                                                    ([3, 4, 2], "allreduce", False),
-                                                   ([0, 6, 3], "reduce", True)])
+                                                   ([0, 6, 3], "reduce", True),
+                                                   ([2, 2, 3], "reduce", True)])
 def test_default_aggregator_is_exact_gloo(counts, final, weighted):
     """dist.Aggregator() with no form named: world 2 and 3 over gloo, the
-    reference's bits on every result rank (the root defaults to the last
-    rank holding slots)."""
+    form the cost model picks (chained or striped; the blocked round is
+    native only), the reference's bits on every result rank (the root
+    defaults to the last rank holding slots)."""
     from test_dist_gloo import MAN as GMAN
     world = len(counts)
     ctx = mp.get_context("spawn")
@@ -162,8 +257,10 @@ def test_default_aggregator_is_exact_gloo(counts, final, weighted):
     want = _expected(states, w)
     last = max(r for r in range(world) if counts[r] > 0)
     checked = 0
+    want_form = exact_form(counts, layout, root_all=final != "reduce")
+    want_form = "striped" if want_form == "striped" else "chained"
     for rk, form, root, o32, o64 in res:
-        assert form == "chained/torch.distributed"
+        assert form == f"{want_form}/torch.distributed"
         assert root == (last if final == "reduce" else -1)
         if final == "reduce" and rk != last:
             continue

@@ -22,7 +22,7 @@ from feddct_amd.dist import shard_range
 from feddct_amd.layout import BucketLayout
 from feddct_amd.partition import layout_tiles, split_tiles
 from oracle import torch_order as O
-from schedsim import Deadlock, Sim
+from schedsim import Deadlock, Hazard, Sim
 
 MAN = {"keys": [{"key": f"k{j}", "shape": [m] if m else [], "dtype": "float32"}
                 for j, m in enumerate([100, 4096, 33, 2048 + 8, 7, 0, 5000, 1, 64, 3000])]
@@ -111,17 +111,57 @@ def test_chained_schedule_deep_levels():
     assert planes == set(i for i in range(4) if O.chain_levels(256, 300) & (1 << i))
 
 
-@pytest.mark.parametrize("counts", COUNTS)
+STRIPE_COUNTS = [[9], [10, 10], [7, 0, 13], [0, 5, 1, 14], [4, 9, 0, 2, 5], [1, 2, 3, 4, 5, 6],
+                 [1, 1, 1, 17, 0, 2, 3], [3, 3, 3, 3, 3, 3, 3, 3], [2, 30, 2, 0, 0, 1, 3, 2]]
+
+
+@pytest.mark.parametrize("counts", STRIPE_COUNTS)
 @pytest.mark.parametrize("root", [0, -1, 1])
-def test_striped_schedule_is_exact(counts, root):
+@pytest.mark.parametrize("nchunks", [1, 3])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_striped_schedule_is_exact(counts, root, nchunks, weighted):
+    """r06: the link-parallel striped round (every peer in one group per
+    column chunk, the chunk reduce beside the next chunk's exchange, the
+    finished chunks two steps later), W = 1..8, weighted too: the
+    single-process reference's bits on every result rank, no deadlock, no
+    stream hazard (schedsim)."""
     W = len(counts)
-    layout, states, _, bufs, scheds = _run(C.FA_MODE_STRIPED, counts, root)
-    want = _expected(states, None)
+    if root >= W:
+        pytest.skip("root beyond the world")
+    layout, states, w, bufs, scheds = _run(C.FA_MODE_STRIPED, counts, root, weighted=weighted,
+                                           nchunks=nchunks)
+    want = _expected(states, w)
     for r in _result_ranks(W, root):
         for s in layout.slots:
             src = bufs[r]["OUT64"] if s.kind == "i64" else bufs[r]["OUT"]
             got = src[s.offset:s.offset + s.numel].reshape(s.shape)
             assert got.tobytes() == np.asarray(want[s.key]).tobytes(), (r, s.key)
+
+
+@pytest.mark.parametrize("W", [2, 3, 5, 8])
+def test_striped_groups_are_link_parallel(W):
+    """Every exchange step of the striped round is ONE group holding all the
+    rank's peers (r06, VERDICT r05 next 1: r02-r05 one partner per group), and
+    the round has nchunks + 2 such steps; one stripe reduce per nonempty
+    chunk, each in the step after its rows arrive."""
+    big = {"keys": [{"key": f"b{j}", "shape": [40000 + 7 * j], "dtype": "float32"}
+                    for j in range(12)]}
+    layout = BucketLayout.from_manifest(big)
+    counts = [3] * W
+    for r in range(W):
+        ops = C.describe(C.FA_MODE_STRIPED, layout, counts, r, nchunks=4, root=-1)
+        by_step = {}
+        for x in ops:
+            if x["op"] in ("SEND", "RECV") and (x["src"] == "CLIENT" or x["dst"] == "RECV"):
+                by_step.setdefault(x["step"], set()).add(x["peer"])
+        assert by_step and all(v == set(range(W)) - {r} for v in by_step.values()), by_step
+        recv_step = {}
+        for x in ops:
+            if x["op"] == "RECV" and x["dst"] == "RECV":
+                recv_step[x["chunk"]] = x["step"]
+        for x in ops:
+            if x["op"] == "K_STRIPE":
+                assert x["step"] == recv_step[x["chunk"]] + 1
 
 
 @pytest.mark.parametrize("counts", COUNTS)
@@ -149,36 +189,43 @@ def test_sharded_schedule(counts, exchange, root, weighted):
 
 
 @pytest.mark.parametrize("W", [2, 3, 4, 5, 6, 7, 8])
-def test_striped_cuts_and_peers_match_python(W):
-    """The native stripe bounds are partition.split_tiles', the shards are
-    dist.shard_range's, and the native send/receive lists are exactly the
-    Python StripedAggregator's (same pairwise rounds)."""
-    from feddct_amd.dist import stripe_p2p_schedule
+@pytest.mark.parametrize("root", [-1, 0])
+def test_striped_cuts_and_peers_match_python(W, root):
+    """The native stripe bounds are partition.split_tiles', its chunk bounds
+    partition.stripe_chunks', the shards dist.shard_range's, and the native
+    exchange and reduce steps are exactly the Python StripedAggregator's
+    (dist.stripe_schedule), op for op and step for step."""
+    from feddct_amd.dist import stripe_schedule
+    from feddct_amd.partition import stripe_chunks
     layout = BucketLayout.from_manifest(MAN)
     n = 3 * W + 2
     counts = [b - a for a, b in (shard_range(n, W, r) for r in range(W))]
     _, tiles = layout_tiles(layout)
     parts = split_tiles(tiles, W, layout.f32_numel)
+    chunks = stripe_chunks(tiles, W, layout.f32_numel, 3)
+    bounds = [[c[0] for c in ch] + [ch[-1][1]] for ch in chunks]
+    assert [(b[0], b[-1]) for b in bounds] == [p[:2] for p in parts]
+    shards = [shard_range(n, W, q) for q in range(W)]
     for r in range(W):
-        ops = C.describe(C.FA_MODE_STRIPED, layout, counts, r, root=-1)
-        sends = [(x["peer"], sum(counts[:r]) + x["src_index"], x["offset"], x["count"])
-                 for x in ops if x["op"] == "SEND" and x["src"] == "CLIENT"]
-        recvs = [(x["peer"], x["dst_index"], x["offset"], x["count"])
-                 for x in ops if x["op"] == "RECV" and x["dst"] == "RECV"]
-        for peer, slot, off, cnt in sends:
-            assert (off, off + cnt) == parts[peer][:2]
-        for peer, slot, off, cnt in recvs:
-            assert (off, off + cnt) == parts[r][:2]
-            a, b = shard_range(n, W, peer)
-            assert a <= slot < b
-        py = stripe_p2p_schedule([p[:2] for p in parts], [shard_range(n, W, q) for q in range(W)],
-                                 r)
-        native = [("send", x["peer"], sum(counts[:r]) + x["src_index"], x["offset"], x["count"])
-                  if x["op"] == "SEND" else
-                  ("recv", x["peer"], x["dst_index"], x["offset"], x["count"])
-                  for x in ops if x["op"] in ("SEND", "RECV") and
-                  (x["src"] == "CLIENT" or x["dst"] == "RECV")]
-        assert native == py
+        ops = C.describe(C.FA_MODE_STRIPED, layout, counts, r, nchunks=3, root=root)
+        native = {}
+        for x in ops:
+            if x["op"] == "SEND" and x["src"] == "CLIENT":
+                t = ("send", x["peer"], sum(counts[:r]) + x["src_index"], x["offset"], x["count"])
+            elif x["op"] == "RECV" and x["dst"] == "RECV":
+                t = ("recv", x["peer"], x["dst_index"], x["offset"], x["count"])
+            elif x["op"] == "SEND":
+                t = ("send_out", x["peer"], x["offset"], x["count"])
+            elif x["op"] == "RECV" and x["dst"] == "OUT":
+                t = ("recv_out", x["peer"], x["offset"], x["count"])
+            elif x["op"] == "K_STRIPE":
+                t = ("reduce", x["chunk"], x["offset"], x["count"])
+            else:
+                continue
+            native.setdefault(x["step"], []).append(t)
+        py = stripe_schedule(bounds, shards, r, root)
+        assert [native.get(k + 2, []) for k in range(len(py))] == py
+        assert all(2 <= k <= len(py) + 1 for k in native), sorted(native)
 
 
 @pytest.mark.parametrize("W", [2, 3, 5, 8])
@@ -217,6 +264,26 @@ def test_describe_errors():
         C.describe(C.FA_MODE_CHAINED, layout, [1, 1], 0, root=2)
     with pytest.raises(_lib.FedaggError, match="clients in total"):
         C.describe(C.FA_MODE_CHAINED, layout, [0, 0], 0)
+
+
+def test_stream_hazard_is_detected():
+    """The replay's stream rules: a compute-stream chunk reduce placed in the
+    same step as the group that receives its rows is reported (the executor
+    would run the two concurrently)."""
+    layout = BucketLayout.from_manifest(MAN)
+    counts = [2, 2]
+    states = [synth.gen_state(MAN, c, synth.MODE_ADVERSARIAL) for c in range(4)]
+    c32, c64 = _buckets(layout, states)
+    _, tiles = layout_tiles(layout)
+    scheds = [C.describe(C.FA_MODE_STRIPED, layout, counts, r, nchunks=2, root=-1)
+              for r in range(2)]
+    for o in scheds:
+        for x in o:
+            if x["op"] == "K_STRIPE":
+                x["step"] -= 1   # beside its own rows' receives
+        o.sort(key=lambda x: x["step"])
+    with pytest.raises(Hazard):
+        Sim(layout, tiles, counts, c32, c64, None, -1).run(scheds)
 
 
 def test_deadlock_is_detected():

@@ -1,32 +1,36 @@
-"""Algorithmic bytes of each native multi-GPU round form, per rank (r04,
-VERDICT r03 next 2): what every rank's own kernels read and write in HBM,
-what its DMA engines move for the exchanges, and what crosses each xGMI link
-— from the schedule the executor issues (fa_describe_round, host only, no
-GPU), against the plain single-GPU reduce of the rank's own clients
-((n_local + 1) * F * 4 bytes).  These are the per-rank local floors of the
-weak-scaling curve that one GPU cannot measure.
+"""Bytes and modelled time of each native multi-GPU round form, per rank
+(r04; r06: per step, and the cost model) — from the schedule the executor
+issues (fa_describe_round, host only, no GPU).
 
-Byte model per op (fp32 elements of the rank's bucket, F = f32_numel,
-V = elements in vector tiles, the cascade region):
-  K_SUM / K_PART / K_BLOCK   nrows rows of the op's range read, one plane written
-  K_CONT                     + the incoming partial plane read
-  K_CHAIN                    + the state planes read and written (fa_chain_levels)
-  K_FOLD                     nrows stripe pieces read, one stripe written
-  K_STRIPE                   n_total receive rows read, one stripe written
-  K_COPY into BLK            0 (the executor binds the fold's piece in place)
-  K_COPY otherwise           read + write; K_DIV read + write; K_ZERO write
-  SEND / RECV                the range over the link to/from `peer`, read /
-                             written in HBM by the DMA
-  collectives                ring traffic: (W-1)/W of the range per link
-                             direction (x2 for all-reduce), in and out of HBM
-Scalar columns (ILP-4 tails, M == 1, int64: < 0.1 % of the bytes) are left
-out.  Usage: round_bytes.py [LAYOUT] [SLOTS_PER_RANK] [W ...]"""
+Per form and world size one JSON line:
+  * max_rank_hbm_bytes / over_plain_reduce: what the busiest rank's kernels
+    and DMA read and write in HBM, against the plain single-GPU reduce of the
+    rank's own clients ((n_local + 1) * F * 4 bytes);
+  * max_link_bytes: the largest byte count on one link direction over the
+    round (any rank, any peer) — what one xGMI link carries;
+  * max_step_link_bytes: the largest byte count on one link direction in ONE
+    step (one RCCL group) of any rank;
+  * serialized_link_bytes: per rank the sum over its steps of the step's
+    largest per-link byte count (the link-bound time of the round x the link
+    rate), max over ranks; pairwise_serialized_link_bytes: the same had every
+    peer been exchanged with in a step of its own, one link at a time (r02-r05's
+    striped round) — the sum over peers of max(bytes out, bytes in);
+  * groups: RCCL groups on the busiest rank;
+  * model_us: fa_round_model's time (include/fedagg_comm.h: link rate
+    FA_MODEL_LINK_GBPS per direction, HBM FA_MODEL_HBM_GBPS, a fixed cost per
+    group and per kernel; the stream rules of the executor);
+  * chosen: the (form, chunks) the default entry takes for this shape.
+The byte model per op is tests/roundmodel.py's (kernel_bytes,
+coll_link_bytes), the same as the native model's.
+Usage: round_bytes.py [LAYOUT] [SLOTS_PER_RANK] [W ...]"""
 import json
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import roundmodel as RM  # noqa: E402
 from feddct_amd import _lib  # noqa: E402
 from feddct_amd import comm as C  # noqa: E402
 from feddct_amd.layout import BucketLayout  # noqa: E402
@@ -41,51 +45,14 @@ def layout_of(name):
     return BucketLayout.from_manifest(load_manifest(name))
 
 
-def rank_bytes(ops, F, V, n_total, W):
-    hbm = link_out = link_in = 0
-    per_peer = {}
-    for o in ops:
-        op, cnt = o["op"], o["count"]
-        rng = cnt if cnt > 0 else V
-        b = 4 * rng
-        if op in ("K_SUM", "K_PART", "K_BLOCK"):
-            hbm += o["nrows"] * b + b
-        elif op == "K_CONT":
-            hbm += o["nrows"] * b + 2 * b
-        elif op == "K_CHAIN":
-            lv_in = bin(_lib.lib.fa_chain_levels(o["row0"], n_total)).count("1")
-            lv_out = bin(_lib.lib.fa_chain_levels(o["row0"] + o["nrows"], n_total)).count("1")
-            hbm += o["nrows"] * b + (lv_in + max(lv_out, 1)) * b
-        elif op == "K_FOLD":
-            hbm += o["nrows"] * b + b
-        elif op == "K_STRIPE":
-            hbm += n_total * b + b
-        elif op == "K_COPY":
-            hbm += 0 if o["dst"] == "BLK" else 2 * b
-        elif op == "K_DIV":
-            hbm += 2 * b
-        elif op == "K_ZERO":
-            hbm += b
-        elif op == "SEND":
-            hbm += b
-            link_out += b
-            per_peer[o["peer"]] = per_peer.get(o["peer"], 0) + b
-        elif op == "RECV":
-            hbm += b
-            link_in += b
-        elif op in ("REDUCE", "REDUCE_SCATTER", "GATHER", "BCAST", "ALLGATHER"):
-            if o["src"] in ("STACK",) or o["dst"] in ("GATHER",):
-                continue   # scalar columns: negligible
-            t = b * (W - 1) / W
-            hbm += 2 * t
-            link_out += t
-            link_in += t
-        elif op == "ALLREDUCE":
-            t = 2 * b * (W - 1) / W
-            hbm += 2 * t
-            link_out += t
-            link_in += t
-    return hbm, link_out, link_in, max(per_peer.values()) if per_peer else 0
+FORMS = [("blocked", C.FA_MODE_BLOCKED, {}),
+         ("chained_4", C.FA_MODE_CHAINED, {"nchunks": 4}),
+         ("chained_16", C.FA_MODE_CHAINED, {"nchunks": 16}),
+         ("striped_1", C.FA_MODE_STRIPED, {"nchunks": 1}),
+         ("striped_4", C.FA_MODE_STRIPED, {"nchunks": 4}),
+         ("sharded_reduce", C.FA_MODE_SHARDED, {"nchunks": 8}),
+         ("sharded_rs_gather", C.FA_MODE_SHARDED,
+          {"nchunks": 8, "exchange": C.FA_XCHG_RS_GATHER})]
 
 
 def main():
@@ -93,34 +60,41 @@ def main():
     spr = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     ws = [int(x) for x in sys.argv[3:]] or [2, 4, 8]
     lay = layout_of(name)
-    info, tiles = _lib.build_tiles_host(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel)
-    F, V = int(lay.f32_numel), int(info["cascade_elems"])
-    forms = [("blocked", C.FA_MODE_BLOCKED, {}), ("chained_1", C.FA_MODE_CHAINED, {"nchunks": 1}),
-             ("chained_16", C.FA_MODE_CHAINED, {"nchunks": 16}),
-             ("striped", C.FA_MODE_STRIPED, {}),
-             ("sharded_reduce", C.FA_MODE_SHARDED, {"nchunks": 8}),
-             ("sharded_rs_gather", C.FA_MODE_SHARDED,
-              {"nchunks": 8, "exchange": C.FA_XCHG_RS_GATHER})]
+    F = int(lay.f32_numel)
     for W in ws:
         counts = [spr] * W
-        n_total = spr * W
         plain = (spr + 1) * F * 4
-        for fname, mode, kw in forms:
-            root = W - 1 if mode == C.FA_MODE_CHAINED else 0
+        root = W - 1
+        chosen = C.multi_select(counts, layout=lay, detail=True)
+        for fname, mode, kw in FORMS:
             try:
-                per = [rank_bytes(C.describe(mode, lay, counts, r, root=root, **kw), F, V,
-                                  n_total, W) for r in range(W)]
+                m = C.round_model(mode, lay, counts, root=root, **kw)
+                scheds = [C.describe(mode, lay, counts, r, root=root, **kw) for r in range(W)]
+                steps = [RM.per_step(o, W) for o in scheds]
+                step_link = max(link for st in steps for _, link, _ in st)
+                serial = max(sum(link for _, link, _ in st) for st in steps)
+                pair = max(pairwise(o, W) for o in scheds)
             except _lib.FedaggError as e:
                 print(json.dumps({"layout": name, "W": W, "form": fname, "error": str(e)}))
                 continue
-            hb = max(p[0] for p in per)
             print(json.dumps({
-                "layout": name, "W": W, "slots_per_rank": spr, "form": fname,
-                "max_rank_hbm_bytes": int(hb), "over_plain_reduce": round(hb / plain, 3),
-                "max_rank_link_out_bytes": int(max(p[1] for p in per)),
-                "max_rank_link_in_bytes": int(max(p[2] for p in per)),
-                "max_bytes_to_one_peer": int(max(p[3] for p in per)),
-                "bucket_bytes": F * 4}), flush=True)
+                "layout": name, "W": W, "slots_per_rank": spr, "form": fname, "root": root,
+                "max_rank_hbm_bytes": int(m["hbm_bytes_max"]),
+                "over_plain_reduce": round(m["hbm_bytes_max"] / plain, 3),
+                "max_link_bytes": int(m["link_bytes_max"]),
+                "max_step_link_bytes": int(step_link), "serialized_link_bytes": int(serial),
+                "pairwise_serialized_link_bytes": int(pair),
+                "groups": m["groups"], "model_us": round(m["model_us"], 1),
+                "chosen": list(chosen[:2]), "bucket_bytes": F * 4}), flush=True)
+
+
+def pairwise(ops, W):
+    """Bytes one rank would serialize exchanging with one peer at a time."""
+    out, inn = [0.0] * W, [0.0] * W
+    for x in ops:
+        if x["op"] in ("SEND", "RECV"):
+            (out if x["op"] == "SEND" else inn)[x["peer"]] += x["count"] * RM.elem_bytes(x)
+    return sum(max(a, b) for a, b in zip(out, inn))
 
 
 if __name__ == "__main__":

@@ -9,7 +9,10 @@ fa_reduce), the per-tensor check that runs while the GPU reduces
 launch call, the version bumps (these five: the r04 Python form of the fast
 path), native_call (the same sequence as one _fa_shim.bound_round call, the
 drop-in's form), the wall of a whole drop-in call with its sync, and the GPU
-time of the round alone (its two launches back to back).  Usage: shim_profile.py [REPS]"""
+time of the round alone (its two launches back to back).  r06: check_tags /
+check_keys / check_all — the native pre-launch check alone (_fa_shim.round_check:
+the dicts' version tags, the tensors' cached TensorImpl storage fields, both).
+Usage: shim_profile.py [REPS]"""
 import json
 import os
 import sys
@@ -57,6 +60,13 @@ def phases(call, reps):
         for k, a, b in (("same_modules", t0, t1), ("launch_reduce", t1, t2),
                         ("views_intact", t2, t3), ("launch_bcast", t3, t4), ("bump", t4, t5)):
             ph[k].append((b - a) * 1e6)
+    # r06: bound_round's pre-launch check alone (dict tags / tensor ViewKeys / both)
+    for what, key in ((0, "check_tags"), (1, "check_keys"), (2, "check_all")):
+        ph[key] = []
+        for _ in range(reps if rb.native is not None else 0):
+            t0 = time.perf_counter()
+            assert _fa_shim.round_check(rb.native, what)
+            ph[key].append((time.perf_counter() - t0) * 1e6)
     # the same round as one C call (the drop-in's path since r04 session 3)
     ph["native_call"] = []
     for _ in range(reps if rb.native is not None else 0):
