@@ -667,7 +667,7 @@ __global__ __launch_bounds__(kBlock) void bcast_kernel(BcastArgs a, int64_t nume
 
 // Streaming copy (the roofline's calibration): one 16-B non-temporal load and
 // store per lane, one 256-lane tile per workgroup, no loop — the fastest of
-// the copy forms measured (tools/copylab.hip, profiles/r02_copylab.jsonl:
+// the copy forms measured (tools/archive/copylab.hip, profiles/r02_copylab.jsonl:
 // 6.62-6.66 TB/s on 1 GiB, against 5.0 TB/s for a grid-stride loop with one
 // float4 per lane and 4.4-5.2 TB/s with four in flight per lane).
 __global__ __launch_bounds__(kBlock) void copy_kernel(const float* __restrict__ src,
@@ -733,7 +733,7 @@ __global__ __launch_bounds__(kBlock) void write_probe_kernel(BcastArgs a, int64_
 // one tile of 2 x 1024 floats per workgroup, 2 independent 16-B
 // non-temporal loads per lane, no loop, and no store unless the tile's sum
 // hits a sentinel value (so nothing but the reads reaches HBM).  The lab's
-// fastest read-only form (tools/bwlab.hip one_stream_read_only_U2: 7.0-7.1
+// fastest read-only form (tools/archive/bwlab.hip one_stream_read_only_U2: 7.0-7.1
 // TB/s, profiles/r01_bwlab.jsonl) — the read ceiling of a box, which the
 // reduce (95 % reads) is compared with; the grid-stride form above runs
 // ~10 % slower.
@@ -1935,7 +1935,7 @@ namespace {
 // otherwise (bcast_group2_kernel).  Scalar pointer loads, client groups of
 // <= kBcastGroupMax = 24, 1024-float parts, destination stores sc1 nt.
 // Measured inside the round, same process, after the reduce's result stores
-// became sc1 (tools/exp_round2.py, profiles/r04_exp_round2_bcast_forms.jsonl):
+// became sc1 (tools/archive/exp_round2.py, profiles/r04_exp_round2_bcast_forms.jsonl):
 // groups of <= 24 vs <= 10 cfg2 283.7 / 282.4 vs 284.9 / 285.0 us, cfg5 (24
 // slots: one group vs three) 350.0 vs 363.5 us, the small layouts equal; and
 // one source fetch instead of one per group (PMC: broadcast traffic 1.0012

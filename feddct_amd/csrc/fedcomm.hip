@@ -2471,6 +2471,16 @@ int fa_round_model(int mode, int nranks, const int* counts, const fa_seg* seg32,
   int rc = make_geo(nranks, 0, counts, seg32, nseg32, f32_numel, seg64, nseg64, i64_numel, flags,
                     "fa_round_model", &g);
   if (rc) return rc;
+  if (nranks == 1) {
+    // one rank: every form is the plain reduction (make_round), one kernel
+    // reading n_total buckets and writing one
+    fa_round_cost c{};
+    c.hbm_bytes_max = (double)(g.n_total + 1) * (4.0 * (double)f32_numel + 8.0 * (double)i64_numel);
+    c.model_us = FA_MODEL_KERNEL_US + us_hbm(c.hbm_bytes_max);
+    c.steps = 1;
+    *out = c;
+    return FA_OK;
+  }
   std::vector<std::vector<fa_xfer>> sch;
   int64_t V = 0;
   if ((rc = all_schedules(g, mode, nchunks, exchange, root, weighted != 0, &sch, &V))) return rc;

@@ -407,7 +407,8 @@ int fa_describe_round(int mode, int nranks, int rank, const int *counts,
  * fa_round_model: the round's modelled time (max over ranks, us), the
  * largest byte count on one link direction over the round (any rank, any
  * peer), the largest per-rank HBM byte count, and the busiest rank's group
- * count.  Errors as fa_describe_round. */
+ * count.  One rank: the plain reduction every form becomes (one kernel over
+ * n_total + 1 buckets).  Errors as fa_describe_round. */
 #define FA_MODEL_LINK_GBPS 64.0    /* GB/s per xGMI link direction (assumed)   */
 #define FA_MODEL_HBM_GBPS 6500.0   /* GB/s: measured float4 copy ceiling       */
 #define FA_MODEL_GROUP_US 15.0     /* one RCCL group: launch + completion      */

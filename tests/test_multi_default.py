@@ -270,3 +270,14 @@ def test_default_aggregator_is_exact_gloo(counts, final, weighted):
             got = src[s.offset:s.offset + s.numel].reshape(s.shape)
             assert got.tobytes() == np.asarray(want[s.key]).tobytes(), (rk, s.key)
     assert checked == (1 if final == "reduce" else world)
+
+
+def test_one_rank_model_is_the_plain_reduction():
+    """With one rank every form is the single-GPU reduction (make_round): the
+    model prices exactly that kernel, whatever form is named."""
+    layout = BucketLayout.from_manifest(MAN)
+    want = RM.KERNEL_US + 21 * (4.0 * layout.f32_numel + 8.0 * layout.i64_numel) / (
+        RM.HBM_GBPS * 1e3)
+    for mode in ("blocked", "chained", "striped"):
+        m = C.round_model(MODES[mode], layout, [20], nchunks=4, root=0)
+        assert m["model_us"] == pytest.approx(want) and m["groups"] == 0
