@@ -13,9 +13,10 @@
  * (and the stateless fa_mean_f32_multi) run a round whose result is
  * bit-identical to one GPU's fa_reduce over all slots, i.e. to the
  * reference's single-process stack(...).mean(0) (train_feddct.py:42-50):
- * the blocked round when every cascade block of 16 slots lies on at most two
- * ranks, else the chained round (fa_multi_select names the choice, host
- * only).  The re-associated e1 round (partial sums + an RCCL sum,
+ * r06, the exact form — blocked (only when every cascade block of 16 slots
+ * lies on at most two ranks), chained or striped — and chunk count with the
+ * lowest time in the cost model below (fa_round_model; fa_multi_select_layout
+ * names the choice, host only; r05 chose blocked-else-chained by geometry).  The re-associated e1 round (partial sums + an RCCL sum,
  * fa_reduce_sharded below) is opt-in (FA_MULTI_REASSOCIATE, or its own
  * plan type): it is NOT within the north_star's 1 ULP — measured r04 on
  * 2 x 20 wrn16_8 clients (profiles/r04_final_bench_n2_gloo_rehearsal.json):

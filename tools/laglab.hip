@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void lagged_k(Args a) {
   if (j < 0 || j >= a.ntiles) return;
   if (threadIdx.x == 0) {
     int ok = 0;
-    for (int it = 0; it < (1 << 22); ++it) {  // bounded: the launch always drains
+    for (int it = 0; it < (1 << 16); ++it) {  // bounded: the launch always drains
       const unsigned f = __builtin_amdgcn_raw_buffer_load_b32(rsrc(a.flags), 4 * j, 0, 16);
       if (f == a.epoch) {
         ok = 1;
@@ -172,7 +172,84 @@ __global__ __launch_bounds__(256) void persist_k(Args a) {
   for (int j = w - a.ntiles; j < a.ntiles; j += a.lag) {
     if (threadIdx.x == 0) {
       int ok = 0;
-      for (int it = 0; it < (1 << 22); ++it) {
+      for (int it = 0; it < (1 << 16); ++it) {
+        const unsigned f = __builtin_amdgcn_raw_buffer_load_b32(rsrc(a.flags), 4 * j, 0, 16);
+        if (f == a.epoch) {
+          ok = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (!ok) atomicAdd(a.err, 1u);
+      go = ok;
+    }
+    __syncthreads();
+    if (go) bcast_tile(a, j);
+    __syncthreads();
+  }
+}
+
+// r06: the publish deferred by one tile.  R persistent
+// reducers (blocks 0..R-1) take tiles w, w + R, ...; after storing tile t's
+// result a reducer issues tile t + R's FIRST client's loads, then waits only
+// until the older operations — tile t's result stores — have completed
+// (vmcnt(2): the two new loads may stay in flight), then a bare workgroup
+// barrier (no fence: a workgroup-scope release would wait for the new loads
+// too) and one lane publishes tile t's flag sc1.  P broadcasters (blocks R ..
+// R+P-1) poll the flags in tile order as persist_k does.  So each reducer
+// keeps the chip's reads going while its stores drain, instead of idling for
+// the stores' write-through latency (the r05 bisect: +1.4 us per round of
+// resident workgroups).
+__device__ __forceinline__ void reduce_tile_from(const Args& a, int t, f4 x0, f4 x1) {
+  const int v0 = threadIdx.x, v1 = threadIdx.x + 256;
+  f4 s0 = x0, s1 = x1;   // client 0's values, loaded ahead
+  for (int i = 1; i < a.n; ++i) {
+    const float* b = a.c[i] + (size_t)t * kTile;
+    const f4 y0 = ld_nt(b, v0), y1 = ld_nt(b, v1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s0 += y0;
+    s1 += y1;
+  }
+  const float fn = (float)a.n;
+  s0 = f4{s0.x / fn, s0.y / fn, s0.z / fn, s0.w / fn};
+  s1 = f4{s1.x / fn, s1.y / fn, s1.z / fn, s1.w / fn};
+  float* o = a.out + (size_t)t * kTile;
+  st_sc1(o, v0, s0);
+  st_sc1(o, v1, s1);
+}
+
+__global__ __launch_bounds__(256) void defer_k(Args a, int R) {
+  const int w = blockIdx.x;
+  __shared__ int go;
+  const int v0 = threadIdx.x, v1 = threadIdx.x + 256;
+  if (w < R) {
+    int t = w;
+    if (t >= a.ntiles) return;
+    f4 x0 = ld_nt(a.c[0] + (size_t)t * kTile, v0), x1 = ld_nt(a.c[0] + (size_t)t * kTile, v1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (;;) {
+      reduce_tile_from(a, t, x0, x1);
+      const int nt = t + R;
+      if (nt < a.ntiles) {
+        x0 = ld_nt(a.c[0] + (size_t)nt * kTile, v0);
+        x1 = ld_nt(a.c[0] + (size_t)nt * kTile, v1);
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // the stores, not the new loads
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      if (threadIdx.x == 0)
+        __builtin_amdgcn_raw_buffer_store_b32(a.epoch, rsrc(a.flags), 4 * t, 0, 16);
+      if (nt >= a.ntiles) return;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the next tile's first loads
+      t = nt;
+    }
+  }
+  const int P = gridDim.x - R;
+  for (int j = w - R; j < a.ntiles; j += P) {
+    if (threadIdx.x == 0) {
+      int ok = 0;
+      for (int it = 0; it < (1 << 16); ++it) {
         const unsigned f = __builtin_amdgcn_raw_buffer_load_b32(rsrc(a.flags), 4 * j, 0, 16);
         if (f == a.epoch) {
           ok = 1;
@@ -256,13 +333,19 @@ int main(int argc, char** argv) {
     };
     std::vector<V> vs = {{"lab_reduce", -3},       {"lab_bcast", -4},
                          {"lab_two_launches", -1}, {"product_round", -2},
-                         {"lag_split_grid", T},    {"lag_4096", 4096},
-                         {"lag_2048", 2048},       {"lag_1024", 1024},
-                         {"lag_512", 512},         {"persist_full", -10},
-                         {"persist_half", -11},    {"persist_quarter", -12}};
+                         {"lag_split_grid", T},    {"lag_1024", 1024},
+                         {"persist_quarter", -12},
+                         // r06: the publish deferred by one tile (defer_k),
+                         // P = slots / 4, 8, 16 broadcasters
+                         {"defer_P4", -20},        {"defer_P8", -21},
+                         {"defer_P16", -22}};
     int occ = 0, cus = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(persist_k),
                                                     256, 0));
+    int occ_d = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_d, reinterpret_cast<const void*>(defer_k),
+                                                    256, 0));
+    occ = std::min(occ, occ_d);
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     const int slots = occ * cus;
     int ctr = 0;
@@ -277,6 +360,11 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(bcast_k, dim3(T), dim3(256), 0, 0, a);
       } else if (v.lag == -2) {
         FA(fa_reduce(plan, a.c, nullptr, L.n, nullptr, a.out, nullptr, FA_F_BCAST, nullptr));
+      } else if (v.lag <= -20) {
+        const int P = std::max(1, slots / (v.lag == -20 ? 4 : v.lag == -21 ? 8 : 16));
+        const int R = std::max(1, slots - P);
+        a.epoch = ++epoch;
+        hipLaunchKernelGGL(defer_k, dim3(R + P), dim3(256), 0, 0, a, R);
       } else if (v.lag <= -10) {
         const int P = std::max(1, std::min(T, v.lag == -10 ? slots - 1
                                               : v.lag == -11 ? slots / 2 : slots / 4));
@@ -324,6 +412,18 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(got.data(), i < L.n ? a.c[i] : a.out, B, hipMemcpyDeviceToHost));
         same = memcmp(got.data(), want.data(), B) == 0;
       }
+      // and the deferred-publish round
+      hipLaunchKernelGGL(hash_fill, dim3(4096), dim3(256), 0, 0, slab[0],
+                         (int64_t)(L.n + 1) * L.floats, 77u);
+      a.epoch = ++epoch;
+      const int P = std::max(1, slots / 8);
+      hipLaunchKernelGGL(defer_k, dim3(std::max(1, slots - P) + P), dim3(256), 0, 0, a,
+                         std::max(1, slots - P));
+      CK(hipDeviceSynchronize());
+      for (int i = 0; i <= L.n && same; ++i) {
+        CK(hipMemcpy(got.data(), i < L.n ? a.c[i] : a.out, B, hipMemcpyDeviceToHost));
+        same = memcmp(got.data(), want.data(), B) == 0;
+      }
     }
     for (size_t k = 0; k < vs.size(); ++k) {
       std::vector<float> t = ts[k];
@@ -332,9 +432,9 @@ int main(int argc, char** argv) {
       const double bytes = vs[k].lag == -3 ? red_bytes : vs[k].lag == -4 ? red_bytes : round_bytes;
       printf("{\"exp\": \"laglab\", \"layout\": \"%s\", \"n\": %d, \"tiles\": %d, \"variant\": "
              "\"%s\", \"us_median\": %.2f, \"us_min\": %.2f, \"bytes\": %.0f, \"frac\": %.4f, "
-             "\"poll_timeouts\": %u, \"lagged_bits_equal\": %s}\n",
+             "\"poll_timeouts\": %u, \"lagged_bits_equal\": %s, \"slots\": %d}\n",
              L.name, L.n, T, vs[k].name.c_str(), us, (double)t[0], bytes,
-             bytes / (us * 1e-6) / 8e12, herr, same ? "true" : "false");
+             bytes / (us * 1e-6) / 8e12, herr, same ? "true" : "false", slots);
       fflush(stdout);
     }
     FA(fa_plan_destroy(plan));

@@ -4,6 +4,8 @@ separate FETCH_SIZE / WRITE_SIZE passes of tools/gpu_round_pmc.sh):
     python tools/round_prof.py round K        # reduce + broadcast launch (FA_F_BCAST)
     python tools/round_prof.py bcast K        # the broadcast launch alone (FA_F_BCAST_ONLY)
     python tools/round_prof.py tgpu K         # the torch-GPU-order reduce (tgpu_kernel<0>)
+    python tools/round_prof.py tgpu32 K       # ... at N = 32 (the S = 2 launch, riders in it)
+    python tools/round_prof.py cpu32 K        # the default order at N = 32 (same clients)
     python tools/round_prof.py sf32 K         # FedDCT sweep layouts' reduce alone (joint
     python tools/round_prof.py resnet110sl K  #   main + proxy bucket, rotated past the MALL)
 """
@@ -52,7 +54,7 @@ def main():
         return sweep(mode, k, dev)
     man = load_manifest("wrn16_8_c10")
     lay = BucketLayout.from_manifest(man)
-    n = 20
+    n = 32 if mode in ("tgpu32", "cpu32") else 20
     cl = make_clients(lay, man, range(n), dev)
     o32, o64 = torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])
     if mode in ("round", "bcast"):
@@ -60,16 +62,21 @@ def main():
                          flags=_lib.FA_PLAN_GAPS_ARE_PADDING)
         red = Reducer(lay, cl, o32, o64, plan=plan,
                       flags=_lib.FA_F_BCAST if mode.startswith("round") else _lib.FA_F_BCAST_ONLY)
-    elif mode == "tgpu":
+    elif mode in ("tgpu", "tgpu32"):
         plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
                          order=_lib.FA_ORDER_TORCH_GPU, n=n)
+        red = Reducer(lay, cl, o32, o64, plan=plan)
+    elif mode == "cpu32":
+        plan = _lib.Plan(lay.segs32, lay.f32_numel, lay.segs64, lay.i64_numel,
+                         flags=_lib.FA_PLAN_GAPS_ARE_PADDING)
         red = Reducer(lay, cl, o32, o64, plan=plan)
     else:
         raise SystemExit(f"unknown mode {mode!r}")
     for _ in range(k):
         red()
     torch.cuda.synchronize()
-    print(f"{mode}: {k} launches, B = {lay.state_bytes()} bytes per client, n = {n}")
+    print(f"{mode}: {k} launches, B = {lay.state_bytes()} bytes per client, n = {n}, "
+          f"algorithmic bytes {lay.algorithmic_bytes(n)}")
 
 
 if __name__ == "__main__":
