@@ -425,11 +425,20 @@ __device__ __forceinline__ void tgpu_wide(KArgs& a, int64_t start, int count, fl
 // ((a0 + a1) + a2) + a3 and, for S = 2, part 0 + part 1.  4 S rows per pass
 // keep the accumulator index static.  The S = 2 launch runs its S = 1 tiles
 // through it too (tgpu_kernel<1>).
+// FA_TGPU_LOOP_DEPTH: rows in flight ahead of the add (1: row b + 1's loads
+// before row b's adds).  2 and 3 (same 130 VGPRs, three workgroups per CU)
+// measured within +-0.4 % of 1 at N = 32 / 48 / 64 (r06,
+// profiles/r06_ab_lib_tgpu_runs.jsonl): the launch is not short of loads in
+// flight.
+#ifndef FA_TGPU_LOOP_DEPTH
+#define FA_TGPU_LOOP_DEPTH 1
+#endif
 template <int U, int S, bool FULL>
 __device__ __forceinline__ void tgpu_wide_loop(KArgs& a, int64_t start, int count, float fac,
                                                bool sum_only) {
   static_assert(S == 1 || S == 2, "row split of the wide loop");
   constexpr int R = 4 * S;
+  constexpr int D = FA_TGPU_LOOP_DEPTH;
   const f4 z = {0.f, 0.f, 0.f, 0.f};
   f4 acc[R][U];
   uint32_t vi[U];
@@ -442,27 +451,31 @@ __device__ __forceinline__ void tgpu_wide_loop(KArgs& a, int64_t start, int coun
     for (int k = 0; k < R; ++k) acc[k][u] = z;
   }
   const int n = a.n;
-  f4 cur[U], nxt[U];
-  {
-    const float* p = sptr32(a, 0) + start;
+  f4 row[D + 1][U];   // row[0]: the row being added; row[d]: d rows ahead
 #pragma unroll
-    for (int u = 0; u < U; ++u) cur[u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
+  for (int d = 0; d < D; ++d) {
+    if (d < n) {
+      const float* p = sptr32(a, d) + start;
+#pragma unroll
+      for (int u = 0; u < U; ++u) row[d][u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
+    }
   }
   for (int b0 = 0; b0 < n; b0 += R) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int b = b0 + k;
       if (b < n) {
-        if (b + 1 < n) {
-          const float* p = sptr32(a, b + 1) + start;
+        if (b + D < n) {
+          const float* p = sptr32(a, b + D) + start;
 #pragma unroll
-          for (int u = 0; u < U; ++u) nxt[u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
+          for (int u = 0; u < U; ++u) row[D][u] = (FULL || ok[u]) ? ldg4<true>(p, vi[u]) : z;
         }
         const int ai = (k % S) * 4 + ((k / S) & 3);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          acc[ai][u] += cur[u];
-          cur[u] = nxt[u];
+          acc[ai][u] += row[0][u];
+#pragma unroll
+          for (int d = 0; d < D; ++d) row[d][u] = row[d + 1][u];
         }
       }
     }
@@ -1552,7 +1565,10 @@ int tgpu_slots(int dev, int batch) {
 // that changes.  The default reduce's 8-client kernels capped the same way
 // ran 20-25 % slower (r05_ab_lib_occupancy_cap.jsonl).  0 when the device
 // cannot say.
-constexpr int kTgpuS2Resident = 3;
+#ifndef FA_TGPU_S2_RESIDENT
+#define FA_TGPU_S2_RESIDENT 3
+#endif
+constexpr int kTgpuS2Resident = FA_TGPU_S2_RESIDENT;
 size_t tgpu_s2_lds(int dev) {
   static std::mutex mu;
   static std::map<int, size_t> cache;
@@ -1578,14 +1594,15 @@ size_t tgpu_s2_lds(int dev) {
 // vs 167.3.
 int tgpu_batch_for(int n) { return n < 16 ? 8 : 16; }
 
-// The S = 1 group's tail round (r04; the default plan's split_tail, §4.3 of
-// DESIGN.md): its scalar and inner tiles first; and when its T tiles spill
+// The tail round of launch group gi (the S = 1 group, r04; the default
+// plan's split_tail, §4.3 of DESIGN.md):
+// its scalar and inner tiles first; and when its T tiles spill
 // 0 < r <= 0.44 slots past k - 1 full rounds, the last slots - r wide tiles
 // are halved (64-element lines), so the table fills exactly k rounds with a
 // last round of half tiles instead of r tiles running alone.  cfg2 at N = 20: ~5,400 tiles on
 // 768 slots = 7.03 rounds.  Per-column arithmetic: the bits never change.
-void tgpu_split_tail(std::vector<Tile>* t, std::vector<float>* fac, int lo[6], int slots) {
-  const int64_t T = lo[1] - lo[0];
+void tgpu_split_tail(std::vector<Tile>* t, std::vector<float>* fac, int lo[6], int gi, int slots) {
+  const int64_t T = lo[gi + 1] - lo[gi];
   const int64_t k = slots > 0 ? (T + slots - 1) / slots : 0;
   const int64_t r = T - (k - 1) * slots;
   // m: the wide tiles to halve (0: none; the group is still reordered so
@@ -1594,13 +1611,15 @@ void tgpu_split_tail(std::vector<Tile>* t, std::vector<float>* fac, int lo[6], i
   const int64_t m = (k > 1 && r > 0 && r * 100 <= kTailMaxPct * (int64_t)slots) ? slots - r : 0;
   std::vector<Tile> nw, wd;
   std::vector<float> fnw, fwd;
-  for (int64_t i = lo[0]; i < lo[1]; ++i) {
+  for (int64_t i = lo[gi]; i < lo[gi + 1]; ++i) {
     const bool w = ((*t)[i].kind & 0xFF) == K_F32_TGPU_W;
     (w ? wd : nw).push_back((*t)[i]);
     (w ? fwd : fnw).push_back((*fac)[i]);
   }
-  std::vector<Tile> g = nw;
-  std::vector<float> f = fnw;
+  std::vector<Tile> g(t->begin(), t->begin() + lo[gi]);
+  std::vector<float> f(fac->begin(), fac->begin() + lo[gi]);
+  g.insert(g.end(), nw.begin(), nw.end());
+  f.insert(f.end(), fnw.begin(), fnw.end());
   const size_t first = (int64_t)wd.size() < m ? wd.size() : wd.size() - (size_t)m;
   for (size_t j = 0; j < wd.size(); ++j) {
     const Tile& x = wd[j];
@@ -1615,12 +1634,12 @@ void tgpu_split_tail(std::vector<Tile>* t, std::vector<float>* fac, int lo[6], i
     f.push_back(fwd[j]);
     f.push_back(fwd[j]);
   }
-  const int add = (int)(g.size() - (size_t)T);
-  g.insert(g.end(), t->begin() + lo[1], t->end());
-  f.insert(f.end(), fac->begin() + lo[1], fac->end());
+  const int add = (int)((int64_t)g.size() - lo[gi] - T);
+  g.insert(g.end(), t->begin() + lo[gi + 1], t->end());
+  f.insert(f.end(), fac->begin() + lo[gi + 1], fac->end());
   t->swap(g);
   fac->swap(f);
-  for (int i = 1; i < 6; ++i) lo[i] += add;
+  for (int i = gi + 1; i < 6; ++i) lo[i] += add;
 }
 }  // namespace
 
@@ -1652,12 +1671,21 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
   // bit) share one run cut into 2048-element tiles across key boundaries, as
   // the default plan's vector runs are: no partial tile per key (cfg2: 5432
   // -> ~5381 tiles).  Gaps join a run only when declared padding.
+  // r06: runs of every row split S (the order depends on (N, S) only, as for
+  // S = 1; S <= 2 in 2048-element W tiles, S >= 4 in 1024-element V tiles),
+  // and adjacent one-element keys of one kind packed a wave each into one
+  // tile: wrn16_8 C10 at N = 32 / 48 / 64 then fills 7 rounds of the S = 2
+  // launch's 768 slots (5,372 / 5,372 / 5,370 tiles) where per-key tiles
+  // spilled past them (5,417 / 5,417 / 5,432)
   int64_t run_s = -1, run_e = -1;
+  int run_ls = 0;
   float run_f = 0.f;
   auto flush = [&]() {
     if (run_s < 0) return;
-    for (int64_t c = run_s; c < run_e; c += 8 * kBlock) {
-      t.push_back(Tile{c, (int32_t)std::min<int64_t>(8 * kBlock, run_e - c), K_F32_TGPU_W});
+    const int64_t te = run_ls <= 1 ? 8 * kBlock : 4 * kBlock;
+    const int kind = (run_ls <= 1 ? K_F32_TGPU_W : K_F32_TGPU_V) | (run_ls << 8);
+    for (int64_t c = run_s; c < run_e; c += te) {
+      t.push_back(Tile{c, (int32_t)std::min<int64_t>(te, run_e - c), kind});
       fac.push_back(run_f);
     }
     run_s = run_e = -1;
@@ -1678,7 +1706,13 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
       if (g.numel == 1) {
         flush();
         const int vec = n >= 128 ? 1 << 16 : 0;  // input-vectorised (tgpu_inner_vec)
-        t.push_back(Tile{g.offset, 1, (pass ? K_I64_TGPU_IN : K_F32_TGPU_IN) | (ls << 8) | vec});
+        const int kind = (pass ? K_I64_TGPU_IN : K_F32_TGPU_IN) | (ls << 8) | vec;
+        if (!t.empty() && t.back().kind == kind && fac.back() == f &&
+            t.back().start + t.back().count == g.offset && t.back().count < kBlock / 64) {
+          t.back().count++;   // one wave per element (tgpu_kernel's inner form)
+          continue;
+        }
+        t.push_back(Tile{g.offset, 1, kind});
         fac.push_back(f);
         continue;
       }
@@ -1699,16 +1733,18 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
       const int64_t body = (g.numel - head) / 4 * 4;
       // S = 1: 2048-element tiles, the default reduce's load shape (r02:
       // 151.9 us on cfg2 with the 1024-element form); S = 2 too since r05
-      // (tgpu_wide_loop), per key
+      // (tgpu_wide_loop); a key whose body is not 16-B aligned keeps its own
+      // tiles
       const bool wide = S <= 2;
-      if (S == 1 && head == 0 && body > 0) {
-        const bool extend = run_s >= 0 && run_f == f &&
+      if (head == 0 && body > 0) {
+        const bool extend = run_s >= 0 && run_f == f && run_ls == ls &&
                             (run_e == g.offset ||
                              ((flags & FA_PLAN_GAPS_ARE_PADDING) && run_e <= g.offset));
         if (!extend) flush();
         if (run_s < 0) {
           run_s = g.offset;
           run_f = f;
+          run_ls = ls;
         }
         run_e = g.offset + body;
         if (body < g.numel) {
@@ -1777,8 +1813,12 @@ int fa_plan_create_order(const fa_seg* seg32, int nseg32, int64_t f32_numel, con
     for (int g = 0; g < 5; ++g) lo[g + 1] += lo[g];
     if (!(flags & FA_PLAN_TUNE_NO_BALANCE)) {
       int dev = 0;
-      if (hipGetDevice(&dev) == hipSuccess)
-        tgpu_split_tail(&t, &fac, lo, tgpu_slots(dev, tgpu_batch_for(n)));
+      if (hipGetDevice(&dev) == hipSuccess) {
+        tgpu_split_tail(&t, &fac, lo, 0, tgpu_slots(dev, tgpu_batch_for(n)));
+        // r06: the same halving on the S = 2 launch measured neutral at
+        // N = 32 / 64 / 100, -2.7 % at N = 48, +0.5 % on C100 N = 128
+        // (profiles/r06_ab_lib_tgpu_runs.jsonl, variant "nobal"): not applied
+      }
     }
     order_groups_tmp.assign(lo, lo + 6);
   }
