@@ -1388,13 +1388,16 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
             ncomm = Comm.from_process_group(group)
         except Exception as e:  # noqa: BLE001
             extra["native_comm_error"] = repr(e)
+    try:
+        extra["multi_env"] = multi_env(ncomm, world)
+    except Exception as e:  # noqa: BLE001
+        extra["multi_env"] = {"error": repr(e)}
     if ncomm is not None:
         from feddct_amd import comm as Cm
         from feddct_amd.comm import (FA_XCHG_RS_GATHER, NativeAggregator,
                                      NativeBlockedAggregator, NativeChainedAggregator,
                                      NativeShardedAggregator, NativeStripedAggregator,
                                      multi_select)
-        extra["multi_env"] = multi_env(ncomm, world)
         # the DEFAULT entry first (r06: the exact form and chunk count the
         # cost model picks for these counts on this layout, result on the
         # last rank — the model's root; the form is in the name)
@@ -1545,7 +1548,8 @@ def multi_env(ncomm, world):
     from feddct_amd import comm as Cm
     env = {k: v for k, v in sorted(os.environ.items())
            if k.startswith(("RCCL_", "NCCL_", "HSA_", "HIP_", "GPU_MAX_HW_QUEUES"))}
-    n, r, d = ncomm.info()
+    # no native communicator (a gloo rehearsal, --same-device): the rest only
+    n, r, d = ncomm.info() if ncomm is not None else (None, None, None)
     ndev = torch.cuda.device_count()
     peer = [[1 if i == j else int(torch.cuda.can_device_access_peer(i, j)) for j in range(ndev)]
             for i in range(ndev)]

@@ -110,3 +110,7 @@ def test_multi_env_fields(monkeypatch):
     assert len(e["peer_access"]) == n and all(len(row) == n for row in e["peer_access"])
     mc = e["model_constants"]
     assert mc["link_GBps"] > 0 and mc["hbm_GBps"] > 0 and mc["group_us"] >= 0
+    # a rehearsal without a native communicator (gloo, --same-device) still
+    # reports the environment and the peer matrix
+    g = bench.multi_env(None, 2)
+    assert g["comm_count"] is None and g["world"] == 2 and g["env"]["NCCL_DEBUG"] == "WARN"
