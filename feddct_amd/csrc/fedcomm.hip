@@ -2060,7 +2060,12 @@ int select_form(const Geo& base, unsigned mflags, int* mode, int* nchunks, doubl
     *mode = first_wide_block(1, base.counts.data(), nullptr, nullptr) < 0 ? FA_MODE_BLOCKED
                                                                          : FA_MODE_CHAINED;
     *nchunks = 1;
-    if (us) *us = -1.0;
+    // fa_round_model's one-rank cost: one kernel reading n_total buckets and
+    // writing one
+    if (us)
+      *us = FA_MODEL_KERNEL_US + us_hbm((double)(base.n_total + 1) *
+                                        (4.0 * (double)base.f32_numel +
+                                         8.0 * (double)base.i64_numel));
     return FA_OK;
   }
   int root = -1;

@@ -281,3 +281,6 @@ def test_one_rank_model_is_the_plain_reduction():
     for mode in ("blocked", "chained", "striped"):
         m = C.round_model(MODES[mode], layout, [20], nchunks=4, root=0)
         assert m["model_us"] == pytest.approx(want) and m["groups"] == 0
+    # the one-rank choice carries that same time (the bench's default_choice)
+    form, k, us = C.multi_select([20], layout=layout, detail=True)
+    assert form == "blocked" and k == 1 and us == pytest.approx(want)
