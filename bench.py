@@ -1555,9 +1555,8 @@ def multi_env(ncomm, world):
             for i in range(ndev)]
     return {"env": env, "comm_count": n, "comm_rank": r, "comm_device": d, "world": world,
             "visible_devices": ndev, "peer_access": peer,
-            "model_constants": {"link_GBps": Cm.MODEL_LINK_GBPS, "hbm_GBps": Cm.MODEL_HBM_GBPS,
-                                "group_us": Cm.MODEL_GROUP_US,
-                                "kernel_us": Cm.MODEL_KERNEL_US}}
+            # in effect in this process (FA_MODEL_* environment overrides)
+            "model_constants": Cm.model_constants()}
 
 
 def build_line(args, world, nbytes_rank, bytes_per_client, t_step, t_kernel, extra):

@@ -43,7 +43,7 @@ COMM_EXPORTS = ["fa_comm_unique_id", "fa_comm_init_rank", "fa_comm_init", "fa_co
                 "fa_multi_plan_mode", "fa_multi_plan_destroy", "fa_reduce_multi",
                 "fa_mean_f32_multi_ex", "fa_stripe_plan_create_ex", "fa_multi_select_layout",
                 "fa_multi_plan_chunks", "fa_round_model", "fa_comm_set_profile",
-                "fa_round_plan_profile"]
+                "fa_round_plan_profile", "fa_model_constants"]
 
 FA_XCHG_REDUCE, FA_XCHG_RS_GATHER = 0, 1
 FA_MODE_SHARDED, FA_MODE_STRIPED, FA_MODE_CHAINED, FA_MODE_BLOCKED = 0, 1, 2, 3
@@ -146,6 +146,7 @@ def _load():
                            ctypes.c_uint, _I, _I, ctypes.POINTER(FaRoundCost)],
         "fa_comm_set_profile": [_P, _I],
         "fa_round_plan_profile": [_P, ctypes.POINTER(FaRoundProfile)],
+        "fa_model_constants": [ctypes.POINTER(ctypes.c_double)] * 4,
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -192,6 +193,15 @@ def multi_select(counts: Sequence[int], exact: bool = True, layout: Optional[Buc
     if detail:
         return MODE_NAMES[m.value], k.value, us.value
     return MODE_NAMES[m.value]
+
+
+def model_constants() -> dict:
+    """The cost model's constants in effect in this process (fa_model_constants:
+    the fedagg_comm.h defaults unless FA_MODEL_LINK_GBPS / FA_MODEL_HBM_GBPS /
+    FA_MODEL_GROUP_US / FA_MODEL_KERNEL_US were set when the model first ran)."""
+    v = [ctypes.c_double() for _ in range(4)]
+    _lib.check(lib().fa_model_constants(*[ctypes.byref(x) for x in v]), "fa_model_constants")
+    return dict(zip(("link_GBps", "hbm_GBps", "group_us", "kernel_us"), (x.value for x in v)))
 
 
 def round_model(mode: int, layout: BucketLayout, counts: Sequence[int], nchunks: int = 0,

@@ -1826,8 +1826,29 @@ int run_round(fa_round_plan* const* plans, int nlocal, const fa_shard_io* io, in
 // rank's schedule replayed in virtual time under the executor's stream rules
 // (execute above): per rank the communication stream (tc) and the caller's
 // stream (tu).  tests/roundmodel.py restates it and checks it against this.
-inline double us_link(double bytes) { return bytes / (FA_MODEL_LINK_GBPS * 1e3); }
-inline double us_hbm(double bytes) { return bytes / (FA_MODEL_HBM_GBPS * 1e3); }
+// The model's constants: fedagg_comm.h's FA_MODEL_* unless the process
+// environment sets a positive FA_MODEL_LINK_GBPS / FA_MODEL_HBM_GBPS /
+// FA_MODEL_GROUP_US / FA_MODEL_KERNEL_US (read once), so numbers measured on
+// a multi-GPU node re-rank the forms without a rebuild.
+struct ModelConst {
+  double link_gbps, hbm_gbps, group_us, kernel_us;
+};
+double env_or(const char* name, double dflt, bool allow_zero) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  char* end = nullptr;
+  const double x = std::strtod(v, &end);
+  return (end && *end == '\0' && (x > 0.0 || (allow_zero && x == 0.0))) ? x : dflt;
+}
+const ModelConst& mc() {
+  static const ModelConst c{env_or("FA_MODEL_LINK_GBPS", FA_MODEL_LINK_GBPS, false),
+                            env_or("FA_MODEL_HBM_GBPS", FA_MODEL_HBM_GBPS, false),
+                            env_or("FA_MODEL_GROUP_US", FA_MODEL_GROUP_US, true),
+                            env_or("FA_MODEL_KERNEL_US", FA_MODEL_KERNEL_US, true)};
+  return c;
+}
+inline double us_link(double bytes) { return bytes / (mc().link_gbps * 1e3); }
+inline double us_hbm(double bytes) { return bytes / (mc().hbm_gbps * 1e3); }
 
 int popc(unsigned v) { return __builtin_popcount(v); }
 
@@ -1982,7 +2003,7 @@ int model_schedules(const std::vector<std::vector<fa_xfer>>& sch, int n_total, i
       if (comm) {
         double link = gcoll;
         for (int q = 0; q < W; ++q) link = std::max(link, std::max(go[q], gi[q]));
-        tc[r] = start + FA_MODEL_GROUP_US + std::max(us_link(link), us_hbm(ghbm));
+        tc[r] = start + mc().group_us + std::max(us_link(link), us_hbm(ghbm));
         hbm[r] += ghbm;
       }
       // the kernels
@@ -1990,7 +2011,7 @@ int model_schedules(const std::vector<std::vector<fa_xfer>>& sch, int n_total, i
         const fa_xfer& x = o[i];
         if (is_comm(x.op)) continue;
         const double kb = kernel_bytes(x, n_total, V);
-        const double dur = FA_MODEL_KERNEL_US + us_hbm(kb);
+        const double dur = mc().kernel_us + us_hbm(kb);
         hbm[r] += kb;
         if (on_comm_stream(x)) {
           if (needs_compute(x)) tc[r] = std::max(tc[r], tu[r]);
@@ -2063,7 +2084,7 @@ int select_form(const Geo& base, unsigned mflags, int* mode, int* nchunks, doubl
     // fa_round_model's one-rank cost: one kernel reading n_total buckets and
     // writing one
     if (us)
-      *us = FA_MODEL_KERNEL_US + us_hbm((double)(base.n_total + 1) *
+      *us = mc().kernel_us + us_hbm((double)(base.n_total + 1) *
                                         (4.0 * (double)base.f32_numel +
                                          8.0 * (double)base.i64_numel));
     return FA_OK;
@@ -2458,6 +2479,16 @@ int fa_describe_round(int mode, int nranks, int rank, const int* counts, const f
 }
 
 
+int fa_model_constants(double* link_gbps, double* hbm_gbps, double* group_us,
+                       double* kernel_us) {
+  const ModelConst& c = mc();
+  if (link_gbps) *link_gbps = c.link_gbps;
+  if (hbm_gbps) *hbm_gbps = c.hbm_gbps;
+  if (group_us) *group_us = c.group_us;
+  if (kernel_us) *kernel_us = c.kernel_us;
+  return FA_OK;
+}
+
 int fa_round_model(int mode, int nranks, const int* counts, const fa_seg* seg32, int nseg32,
                    int64_t f32_numel, const fa_seg* seg64, int nseg64, int64_t i64_numel,
                    int nchunks, int exchange, unsigned flags, int root, int weighted,
@@ -2481,7 +2512,7 @@ int fa_round_model(int mode, int nranks, const int* counts, const fa_seg* seg32,
     // reading n_total buckets and writing one
     fa_round_cost c{};
     c.hbm_bytes_max = (double)(g.n_total + 1) * (4.0 * (double)f32_numel + 8.0 * (double)i64_numel);
-    c.model_us = FA_MODEL_KERNEL_US + us_hbm(c.hbm_bytes_max);
+    c.model_us = mc().kernel_us + us_hbm(c.hbm_bytes_max);
     c.steps = 1;
     *out = c;
     return FA_OK;

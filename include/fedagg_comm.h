@@ -414,6 +414,14 @@ int fa_describe_round(int mode, int nranks, int rank, const int *counts,
 #define FA_MODEL_HBM_GBPS 6500.0   /* GB/s: measured float4 copy ceiling       */
 #define FA_MODEL_GROUP_US 15.0     /* one RCCL group: launch + completion      */
 #define FA_MODEL_KERNEL_US 3.0     /* one kernel: launch gap + ramp / drain    */
+/* The constants in effect: the defaults above unless the process
+ * environment held a positive FA_MODEL_LINK_GBPS / FA_MODEL_HBM_GBPS (a
+ * non-negative FA_MODEL_GROUP_US / FA_MODEL_KERNEL_US) when the model first
+ * ran — read once per process — so rates measured on a multi-GPU node
+ * re-rank the forms fa_multi_select_layout / fa_multi_plan_create pick
+ * without a rebuild.  NULL outputs are skipped; always FA_OK. */
+int fa_model_constants(double *link_gbps, double *hbm_gbps, double *group_us,
+                       double *kernel_us);
 typedef struct fa_round_cost {
   double model_us;
   double link_bytes_max;

@@ -284,3 +284,37 @@ def test_one_rank_model_is_the_plain_reduction():
     # the one-rank choice carries that same time (the bench's default_choice)
     form, k, us = C.multi_select([20], layout=layout, detail=True)
     assert form == "blocked" and k == 1 and us == pytest.approx(want)
+
+
+def test_model_constants_from_the_environment():
+    """The cost model's constants can be overridden per process
+    (FA_MODEL_LINK_GBPS ...; fa_model_constants reports them), so rates
+    measured on a multi-GPU node re-rank the forms without a rebuild: a
+    faster link makes cfg5's exchange cheaper, a slower one dearer.  Run in
+    child processes: the library reads the environment once."""
+    import json
+    import subprocess
+    import sys
+    code = ("import json, sys; sys.path.insert(0, %r); from feddct_amd import comm as C; "
+            "from feddct_amd.layout import BucketLayout; from feddct_amd.workload import "
+            "load_manifest, joint_manifest; "
+            "m = [load_manifest('wrnsl16_8_sf4_c100_main'), load_manifest('wrnsl16_8_sf4_c100_proxy')]; "
+            "lay = BucketLayout.from_manifest(joint_manifest(m)); "
+            "print(json.dumps([C.model_constants(), C.multi_select([3] * 8, layout=lay, detail=True)]))"
+            % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    out = {}
+    for tag, env in (("default", {}), ("fast", {"FA_MODEL_LINK_GBPS": "200"}),
+                     ("slow", {"FA_MODEL_LINK_GBPS": "20", "FA_MODEL_GROUP_US": "0"}),
+                     ("bad", {"FA_MODEL_LINK_GBPS": "-3"})):
+        e = {k: v for k, v in os.environ.items() if not k.startswith("FA_MODEL_")}
+        e.update(env)
+        r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[tag] = json.loads(r.stdout.strip().splitlines()[-1])
+    d, f, s, b = (out[k] for k in ("default", "fast", "slow", "bad"))
+    assert d[0] == {"link_GBps": C.MODEL_LINK_GBPS, "hbm_GBps": C.MODEL_HBM_GBPS,
+                    "group_us": C.MODEL_GROUP_US, "kernel_us": C.MODEL_KERNEL_US}
+    assert f[0]["link_GBps"] == 200.0 and s[0]["link_GBps"] == 20.0 and s[0]["group_us"] == 0.0
+    assert b[0] == d[0]          # a non-positive rate is ignored
+    assert f[1][2] < d[1][2] < s[1][2]
