@@ -1518,6 +1518,9 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
         extra["headline_not_verified_exact"] = True
     extra["modes"] = report
     extra["selected_mode"] = best
+    mc = model_check(report)
+    if mc:
+        extra["model_check"] = mc
     # the opt-in re-associated round beside the exact headline: its time and
     # its distance from the reference's bits
     e1 = [n for n in report if n.startswith("e1/") and "ms_per_step" in report[n]]
@@ -1539,6 +1542,24 @@ def multi_gpu(args, world, rank, dev, group, layout, manifest, clients, out32, o
         except Exception as e:  # noqa: BLE001
             extra["cfg5_feddct_c100_n24_sharded"] = {"error": repr(e)}
     return best_t, t_kernel, ncomm
+
+def model_check(report):
+    """The cost model against the run: for every mode
+    with a modelled time, measured / modelled; whether the model's fastest
+    form is the measured fastest, and the measured time of the model's pick
+    over the measured best (1.0: the model chose right).  None when fewer than
+    two modes carry both numbers."""
+    rows = {n: (r["ms_per_step"] * 1e3, r["model_us"]) for n, r in report.items()
+            if "model_us" in r and "ms_per_step" in r and r["model_us"] > 0
+            and not n.startswith("default=")}
+    if len(rows) < 2:
+        return None
+    ratio = {n: round(t / m, 3) for n, (t, m) in rows.items()}
+    pick = min(rows, key=lambda n: rows[n][1])
+    best = min(rows, key=lambda n: rows[n][0])
+    return {"measured_over_model": ratio, "model_pick": pick, "measured_best": best,
+            "agree": pick == best, "pick_over_best": round(rows[pick][0] / rows[best][0], 3)}
+
 
 def multi_env(ncomm, world):
     """What the first real multi-GPU run needs to be read (VERDICT r05 next

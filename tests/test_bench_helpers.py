@@ -114,3 +114,21 @@ def test_multi_env_fields(monkeypatch):
     # reports the environment and the peer matrix
     g = bench.multi_env(None, 2)
     assert g["comm_count"] is None and g["world"] == 2 and g["env"]["NCCL_DEBUG"] == "WARN"
+
+
+def test_model_check():
+    """The N>1 line's model check: measured over modelled per form, the
+    model's pick against the measured best (the default entry's own line is
+    left out: it duplicates its form)."""
+    rep = {"blocked/native": {"ms_per_step": 1.0, "model_us": 800.0},
+           "chained/native/c4": {"ms_per_step": 2.0, "model_us": 1500.0},
+           "striped/native/c1": {"ms_per_step": 0.9, "model_us": 900.0},
+           "default=blocked/native": {"ms_per_step": 0.5, "model_us": 800.0},
+           "e1/torch.distributed": {"ms_per_step": 0.1},
+           "broken": {"error": "x"}}
+    mc = bench.model_check(rep)
+    assert mc["model_pick"] == "blocked/native" and mc["measured_best"] == "striped/native/c1"
+    assert mc["agree"] is False and mc["pick_over_best"] == round(1.0 / 0.9, 3)
+    assert mc["measured_over_model"]["chained/native/c4"] == round(2000 / 1500, 3)
+    assert "default=blocked/native" not in mc["measured_over_model"]
+    assert bench.model_check({"a": {"ms_per_step": 1.0, "model_us": 5.0}}) is None
