@@ -2034,19 +2034,29 @@ struct Launch {
 // for the round count — keep the batch form).  Not the 1024-float table, not
 // 8..16 clients, not the short launches (resnet110sl N = 25 at two rounds:
 // +0.9 %; sf32 N = 3 at 2.5: +0.8 %).
+// r06: unweighted calls of 64..128 clients too, now on the 2048-float table
+// (select_launch): same process against the 1024-float table's batch form
+// (profiles/r06_ab_lib_n64.jsonl) C10 N = 64 / 100 / 128 -3.5 / -3.1 / -3.2 %,
+// C100 N = 64 / 100 -3.0 / -2.5 %, bits equal; the 2048-float table in the
+// batch form alone -1.8 / -3.0 / -3.3 / -1.8 / -2.0 %.  Weighted calls from
+// 64 keep the batch form (r05: the loop +0.4 / +2.4 % at 80 / 128).
 int pipe_rule(const fa_plan* plan, const Launch& L, int n, bool weighted) {
   (void)plan;
-  (void)weighted;
   if (n > kInline || L.vec_u != 2 || L.slots <= 0 || L.nt < 3 * L.slots) return 0;
-  return (n >= 2 && n <= 7) || (n >= 17 && n <= 63) ? 1 : 0;
+  return (n >= 2 && n <= 7) || (n >= 17 && n <= 63) || (!weighted && n >= 64) ? 1 : 0;
 }
 
 Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) {
   Launch L{plan->d_tiles, plan->nt_dev, plan->ns_dev, plan->d_sidx, plan->vec_u, 0, 0};
   bool alt = false;
   (void)flags;
-  // 1024-float tiles for unweighted N >= 64 (tools/tune.py sweep)
-  if (plan->d_tiles_alt && !weighted && n >= 64) {
+  // 1024-float tiles for unweighted calls past the inline pointers (r02's
+  // tools/tune.py sweep took them from N = 64; r06: 64..128 run faster on the
+  // 2048-float table with the client loop, see pipe_rule)
+#ifndef FA_ALT_MIN_N
+#define FA_ALT_MIN_N (kInline + 1)
+#endif
+  if (plan->d_tiles_alt && !weighted && n >= FA_ALT_MIN_N) {
     L.tiles = plan->d_tiles_alt;
     L.nt = plan->nt_alt_dev;
     L.ns = plan->ns_alt_dev;

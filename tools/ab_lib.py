@@ -53,7 +53,11 @@ CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
          # r05: the N <= 3 table (every column in the vector runs)
          ("sf32w", "wrnsl16_8_sf32_c100", 3, 6), ("c10_n3", "wrn16_8_c10", 3, 2),
          ("r110_n2", "resnet110sl_sf4_c100", 2, 6), ("r110_n3", "resnet110sl_sf4_c100", 3, 6),
-         ("sf16_n3", "wrnsl16_8_sf16_c100", 3, 6)]
+         ("sf16_n3", "wrnsl16_8_sf16_c100", 3, 6),
+         # r06: the default order from 64 clients (the 1024-float table)
+         ("c10_n128", "wrn16_8_c10", 128, 1), ("c100_n64", "wrn16_8_c100", 64, 1),
+         ("c100_n100", "wrn16_8_c100", 100, 1), ("c10_n200", "wrn16_8_c10", 200, 1),
+         ("c10_n256", "wrn16_8_c10", 256, 1)]
 
 
 def load(path):
