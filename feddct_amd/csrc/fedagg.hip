@@ -2036,10 +2036,11 @@ struct Launch {
 // +0.9 %; sf32 N = 3 at 2.5: +0.8 %).
 // r06: unweighted calls of 64..128 clients too, now on the 2048-float table
 // (select_launch): same process against the 1024-float table's batch form
-// (profiles/r06_ab_lib_n64.jsonl) C10 N = 64 / 100 / 128 -3.5 / -3.1 / -3.2 %,
-// C100 N = 64 / 100 -3.0 / -2.5 %, bits equal; the 2048-float table in the
-// batch form alone -1.8 / -3.0 / -3.3 / -1.8 / -2.0 %.  Weighted calls from
-// 64 keep the batch form (r05: the loop +0.4 / +2.4 % at 80 / 128).
+// (profiles/r06_ab_lib_n64.jsonl, two boxes) C10 N = 64 / 100 / 128 -3.5 /
+// -3.1 / -3.2 % and -3.1 / -2.5 / -2.6 %, C100 N = 64 / 100 -3.0 / -2.5 % and
+// -0.3 / -2.2 %, bits equal; the 2048-float table in the batch form alone
+// -1.8 / -3.0 / -3.3 / -1.8 / -2.0 %.  Weighted calls from 64 keep the batch
+// form (r05: the loop +0.4 / +2.4 % at 80 / 128).
 int pipe_rule(const fa_plan* plan, const Launch& L, int n, bool weighted) {
   (void)plan;
   if (n > kInline || L.vec_u != 2 || L.slots <= 0 || L.nt < 3 * L.slots) return 0;
@@ -2052,7 +2053,8 @@ Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) 
   (void)flags;
   // 1024-float tiles for unweighted calls past the inline pointers (r02's
   // tools/tune.py sweep took them from N = 64; r06: 64..128 run faster on the
-  // 2048-float table with the client loop, see pipe_rule)
+  // 2048-float table with the client loop, see pipe_rule; past 128 the
+  // 2048-float table measured +3.7 % at N = 200, -1.4 % at 256: kept)
 #ifndef FA_ALT_MIN_N
 #define FA_ALT_MIN_N (kInline + 1)
 #endif
