@@ -1592,7 +1592,13 @@ size_t tgpu_s2_lds(int dev) {
 // measured r04 (tools/tgpu_speed.py, profiles/r04_tgpu_batch.jsonl) cfg3
 // N = 5 40.8 vs 45.8 us, but cfg2 N = 20 146.7 vs 140.9, cfg5 N = 24 173.9
 // vs 167.3.
-int tgpu_batch_for(int n) { return n < 16 ? 8 : 16; }
+// r06: from 10 clients the 16-row form (three workgroups per CU) since the
+// client loop: same process (profiles/r06_ab_lib_tgpu_batch.jsonl) N = 10 / 12
+// -1.7 / -2.5 %, N = 2 / 5 / sf32 (N = 3) +1.3 / +3.8 / +1.6 %.
+#ifndef FA_TGPU_B16_MIN
+#define FA_TGPU_B16_MIN 10
+#endif
+int tgpu_batch_for(int n) { return n < FA_TGPU_B16_MIN ? 8 : 16; }
 
 // The tail round of launch group gi (the S = 1 group, r04; the default
 // plan's split_tail, §4.3 of DESIGN.md):

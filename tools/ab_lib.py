@@ -57,7 +57,10 @@ CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
          # r06: the default order from 64 clients (the 1024-float table)
          ("c10_n128", "wrn16_8_c10", 128, 1), ("c100_n64", "wrn16_8_c100", 64, 1),
          ("c100_n100", "wrn16_8_c100", 100, 1), ("c10_n200", "wrn16_8_c10", 200, 1),
-         ("c10_n256", "wrn16_8_c10", 256, 1)]
+         ("c10_n256", "wrn16_8_c10", 256, 1),
+         # r06: the torch-GPU order's row batch below 16 clients
+         ("c10_n8_tgpu", "wrn16_8_c10", 8, 1), ("c10_n9_tgpu", "wrn16_8_c10", 9, 1),
+         ("c10_n14_tgpu", "wrn16_8_c10", 14, 1)]
 
 
 def load(path):
