@@ -999,9 +999,16 @@ int build_tiles(const std::vector<fa_seg>& s32, const std::vector<fa_seg>& s64, 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // Clients per load batch of the reduce kernel a call runs (launch_reduce).
+// r06: the 16-client kernels (three workgroups per CU) from 12 clients, with
+// the client loop (pipe_rule): same process (profiles/r06_ab_lib_mid_n.jsonl)
+// N = 12 / 14 / 16 -1.8 / -2.7 / -0.3 %, weighted N = 12 -1.4 / -1.5 % (C10 /
+// C100); at N = 10 +1.0 %, so below 12 the 8-client kernels stay.
+#ifndef FA_B16_MIN
+#define FA_B16_MIN 12
+#endif
 int pick_batch(int n, int vec_u, unsigned pflags) {
   const int b = (pflags & FA_PLAN_TUNE_BATCH8)    ? 8
-                : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (n < 16 ? 8 : 16);
+                : (pflags & FA_PLAN_TUNE_BATCH16) ? 16 : (n < FA_B16_MIN ? 8 : 16);
   return (vec_u == 4 && b == 16) ? 8 : b;  // no 16-client kernels at U = 4
 }
 
@@ -2038,9 +2045,10 @@ struct Launch {
 // 2048-float tiles of launches of three or more rounds of resident
 // workgroups (partial tiles — tensor ends, the halved tail of a table re-cut
 // for the round count — keep the batch form).  Not the 1024-float table, not
-// 8..16 clients, not the short launches (resnet110sl N = 25 at two rounds:
-// +0.9 %; sf32 N = 3 at 2.5: +0.8 %).
-// r06: unweighted calls of 64..128 clients too, now on the 2048-float table
+// 8..16 clients (r05: on the 8-client kernels), not the short launches
+// (resnet110sl N = 25 at two rounds: +0.9 %; sf32 N = 3 at 2.5: +0.8 %).
+// r06: 12..16 clients on the 16-client kernels (pick_batch, FA_B16_MIN);
+// unweighted calls of 64..128 clients too, now on the 2048-float table
 // (select_launch): same process against the 1024-float table's batch form
 // (profiles/r06_ab_lib_n64.jsonl, two boxes) C10 N = 64 / 100 / 128 -3.5 /
 // -3.1 / -3.2 % and -3.1 / -2.5 / -2.6 %, C100 N = 64 / 100 -3.0 / -2.5 % and
@@ -2050,7 +2058,11 @@ struct Launch {
 int pipe_rule(const fa_plan* plan, const Launch& L, int n, bool weighted) {
   (void)plan;
   if (n > kInline || L.vec_u != 2 || L.slots <= 0 || L.nt < 3 * L.slots) return 0;
-  return (n >= 2 && n <= 7) || (n >= 17 && n <= 63) || (!weighted && n >= 64) ? 1 : 0;
+#ifndef FA_PIPE_MID_LO
+#define FA_PIPE_MID_LO FA_B16_MIN
+#endif
+  return (n >= 2 && n <= 7) || (n >= FA_PIPE_MID_LO && n <= 63) || (!weighted && n >= 64) ? 1
+                                                                                            : 0;
 }
 
 Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) {

@@ -361,7 +361,8 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
 // longer sit between one client's data arriving and the next client's loads
 // leaving.  Its own kernel instances (PIPE), full tiles only; the launch
 // rule (fedagg.hip pipe_rule) and the measurements behind it are in DESIGN
-// §4.1: 1.0-1.7 % faster for 2..7 and 17..63 clients, mean or weighted, in
+// §4.1: 1.0-1.7 % faster for 2..7 and 17..63 clients (r06: 12..63, and
+// unweighted 64..128), mean or weighted, in
 // launches of three or more rounds (cfg2, cfg3, cfg4, cfg5), slower for
 // 8..12 and 64..128 clients and on short launches.  Partial tiles keep the
 // batch form: an instance that took them too compiled into a truly two-deep

@@ -69,6 +69,9 @@ CASES = [("one_tensor_1024", 20, False), ("one_tensor_1280", 16, False),
          ("wrnsl16_8_sf32_c100_joint", 3, False), ("wrnsl16_8_sf2_c100_joint", 48, True)]
 
 
+B16 = 12
+
+
 @pytest.mark.parametrize("name,n,weighted", CASES)
 def test_balanced_table_same_bits(lib, name, n, weighted):
     from feddct_amd.workload import make_clients
@@ -91,12 +94,13 @@ def test_balanced_table_same_bits(lib, name, n, weighted):
     nt_b, slots = pb.launch_shape(n, weighted)
     nt_p, slots_p = pp.launch_shape(n, weighted)   # the default batch's slots
     assert slots > 0 and slots_p > 0 and slots % 256 == 0
-    s8 = pp.launch_shape(5, weighted)[1] if n >= 16 else slots_p
+    # the 16-client kernels from B16 clients (r06: 12; fedagg.hip pick_batch)
+    s8 = pp.launch_shape(5, weighted)[1] if n >= B16 else slots_p
     k = -(-nt_p // slots_p)
     r = nt_p - (k - 1) * slots_p
-    if k > 1 and 100 * r <= 44 * slots_p and (n < 16 or nt_p > s8):
+    if k > 1 and 100 * r <= 44 * slots_p and (n < B16 or nt_p > s8):
         assert (nt_b, slots) == (k * slots_p, slots_p)   # tail split: exactly k rounds
-    elif n < 16 or nt_p > s8 or (nt_p <= slots_p and nt_p >= 0.97 * slots_p):
+    elif n < B16 or nt_p > s8 or (nt_p <= slots_p and nt_p >= 0.97 * slots_p):
         assert (nt_b, slots) == (nt_p, slots_p)    # plain table, default batch
     elif nt_p <= slots_p:
         assert nt_p < nt_b <= slots_p and slots == slots_p   # one round, re-cut to fill it
