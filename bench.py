@@ -633,8 +633,13 @@ def other_configs(dev, steps=100, warmup=20):
                 prefixes = ("0.", "1.") if len(names) > 1 else ("",)
                 man = joint_manifest(mans, prefixes) if len(names) > 1 else mans[0]
                 lay = BucketLayout.from_manifest(man)
-                cl = make_clients(lay, list(zip(mans, prefixes)), range(n), dev)
-                o32, o64 = torch.zeros_like(cl[0][0]), torch.zeros_like(cl[0][1])
+                # placed as the drop-in places a round (aggregate.py: a new
+                # slab sized for the N clients + the global, slab.expecting)
+                slab.release()
+                with slab.expecting(n + 1):
+                    cl = make_clients(lay, list(zip(mans, prefixes)), range(n), dev)
+                    o32 = slab.carve(cl[0][0].numel(), torch.float32, dev)
+                o64 = torch.zeros_like(cl[0][1])
                 reds.append((names, prefixes, lay, n, Reducer(lay, cl, o32, o64, weights=w),
                              o32, o64))
             sets.append(reds)
