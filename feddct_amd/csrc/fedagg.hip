@@ -2057,6 +2057,17 @@ struct Launch {
 // form (r05: the loop +0.4 / +2.4 % at 80 / 128).
 int pipe_rule(const fa_plan* plan, const Launch& L, int n, bool weighted) {
   (void)plan;
+  // r06: unweighted calls of 256 clients and more (the DEEP cascade) on the
+  // 2048-float table, the loop reading the device pointer table through
+  // scalar loads (PIPE = 2): same process against the 1024-float table's
+  // batch form (profiles/r06_ab_lib_tab_loop.jsonl) N = 256 / 300 -1.9 /
+  // -3.8 %; at 129..255 (not deep) +0.2 / +3.5 % at 150 / 200, so those keep
+  // the 1024-float table.  Bits equal.
+  if (n > kInline)
+    return (!weighted && n >= 256 && L.vec_u == 2 && L.batch == 16 && L.slots > 0 &&
+            L.nt >= 3 * L.slots)
+               ? 2
+               : 0;
   if (n > kInline || L.vec_u != 2 || L.slots <= 0 || L.nt < 3 * L.slots) return 0;
 #ifndef FA_PIPE_MID_LO
 #define FA_PIPE_MID_LO FA_B16_MIN
@@ -2065,18 +2076,16 @@ int pipe_rule(const fa_plan* plan, const Launch& L, int n, bool weighted) {
                                                                                             : 0;
 }
 
+
 Launch select_launch(const fa_plan* plan, int n, bool weighted, unsigned flags) {
   Launch L{plan->d_tiles, plan->nt_dev, plan->ns_dev, plan->d_sidx, plan->vec_u, 0, 0};
   bool alt = false;
   (void)flags;
-  // 1024-float tiles for unweighted calls past the inline pointers (r02's
-  // tools/tune.py sweep took them from N = 64; r06: 64..128 run faster on the
-  // 2048-float table with the client loop, see pipe_rule; past 128 the
-  // 2048-float table measured +3.7 % at N = 200, -1.4 % at 256: kept)
-#ifndef FA_ALT_MIN_N
-#define FA_ALT_MIN_N (kInline + 1)
-#endif
-  if (plan->d_tiles_alt && !weighted && n >= FA_ALT_MIN_N) {
+  // 1024-float tiles for unweighted calls of 129..255 clients (r02's
+  // tools/tune.py sweep took them from N = 64; r06: 64..128 and from 256 run
+  // faster on the 2048-float table with the client loop, see pipe_rule; the
+  // 2048-float table at N = 200 +3.7 % in the batch form, +3.5 % with the loop)
+  if (plan->d_tiles_alt && !weighted && n > kInline && n < 256) {
     L.tiles = plan->d_tiles_alt;
     L.nt = plan->nt_alt_dev;
     L.ns = plan->ns_alt_dev;

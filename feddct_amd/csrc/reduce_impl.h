@@ -370,18 +370,23 @@ __device__ __forceinline__ void batch_tail(KArgs& a, Acc<U, DEEP>& A, int b0, in
 // did a hand-written two-register-set form (4 %): two clients per wave in
 // flight spread the chip's reads over twice as many places, as the issue-all
 // batch form did in r04 (profiles/r05_ab_lib_pipe2_*.jsonl).
-template <int U, bool DEEP, bool WEIGHTED, int POL>
+template <int U, bool DEEP, bool WEIGHTED, int POL, bool TABP = false>
+__device__ __forceinline__ const float* pipe_ptr(KArgs& a, int i) {
+  if constexpr (TABP) return ((const FA_CONST f32p*)a.tab32)[i];
+  else return a.c32[i];
+}
+template <int U, bool DEEP, bool WEIGHTED, int POL, bool TABP = false>
 __device__ __forceinline__ void pipe2_clients(KArgs& a, Acc<U, DEEP>& A, int n, int64_t start,
                                               const uint32_t (&vl)[U], int lp, int mask) {
   f4 cur[U], nxt[U];
   {
-    const float* p = a.c32[0] + start;
+    const float* p = pipe_ptr<U, DEEP, WEIGHTED, POL, TABP>(a, 0) + start;
 #pragma unroll
     for (int u = 0; u < U; ++u) cur[u] = ldg4<(POL & 1) != 0>(p, vl[u]);
   }
   for (int b = 0; b < n; ++b) {
     if (b + 1 < n) {
-      const float* p = a.c32[b + 1] + start;
+      const float* p = pipe_ptr<U, DEEP, WEIGHTED, POL, TABP>(a, b + 1) + start;
 #pragma unroll
       for (int u = 0; u < U; ++u) nxt[u] = ldg4<(POL & 1) != 0>(p, vl[u]);
     }
@@ -442,12 +447,20 @@ __device__ __forceinline__ void tile_vec(KArgs& a, int64_t start,
     }
   }
   int b0 = 0;
-  if constexpr (PIPE != 0 && FULL && !CHAIN && !TAB) {
+  if constexpr (PIPE == 1 && FULL && !CHAIN && !TAB) {
     // pipe2_clients reads the inline kernarg arrays: safe on its own for any
     // launch, the host rule (pipe_rule) aside — beyond kInline clients the
     // batches below take the tile
     if (n <= kInline) {
       pipe2_clients<U, DEEP, WEIGHTED, POL>(a, A, n, start, vi, lp, mask);
+      b0 = n;
+    }
+  }
+  if constexpr (PIPE == 2 && FULL && !CHAIN && !WEIGHTED) {
+    // r06: the device pointer table through the constant address space
+    // (scalar loads): the unweighted calls of 256 clients and more (DEEP)
+    if (n > kInline) {
+      pipe2_clients<U, DEEP, WEIGHTED, POL, true>(a, A, n, start, vi, lp, mask);
       b0 = n;
     }
   }
@@ -713,12 +726,15 @@ hipError_t launch_chain_ub(const ReduceArgs& a, int ntiles, bool deep, bool w, h
            : launch_one<U, B, false, false, 3, true>(a, ntiles, st);
 }
 // The reduce: nt loads, sc1 result stores (POL 5, st_out).  pipe (fedagg.hip
-// pipe_rule; not deep, U = 2 only): the PIPE instances.
+// pipe_rule; U = 2 only): 1 the PIPE instances over the inline pointers (not
+// deep), 2 (r06) the unweighted DEEP instance over the pointer table.
 template <int U, int B>
 hipError_t launch_u(const ReduceArgs& a, int ntiles, bool deep, bool w, int pipe,
                     hipStream_t st) {
   if constexpr (U == 2) {
-    if (pipe && !deep)
+    if constexpr (B == 16)
+      if (pipe == 2 && deep && !w) return launch_one<U, B, true, false, 5, false, 2>(a, ntiles, st);
+    if (pipe == 1 && !deep)
       return w ? launch_one<U, B, false, true, 5, false, 1>(a, ntiles, st)
                : launch_one<U, B, false, false, 5, false, 1>(a, ntiles, st);
   } else {

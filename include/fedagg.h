@@ -175,8 +175,9 @@ int fa_plan_create_from_tiles(const fa_tile_desc *tiles, int ntiles,
  * fa_plan_launch_form: the kernel that call runs — its vector tile width
  * (floats), clients per load batch, and whether its full tiles take the
  * client loop (pipe = 1: the next client's loads before the current
- * client's adds) or the batches (0).  Torch-GPU-order plans
- * report zeros. */
+ * client's adds; 2: the same loop reading the device pointer
+ * table, unweighted calls of 256 clients and more, r06) or the batches (0).
+ * Torch-GPU-order plans report zeros. */
 int fa_plan_balance_host(const fa_tile_desc *vec, int nvec, int tile_elems,
                          int nscalar, int slots, fa_tile_desc *out, int cap);
 int fa_plan_launch_shape(const fa_plan *plan, int n, int weighted, int *ntiles,

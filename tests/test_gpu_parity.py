@@ -359,15 +359,16 @@ def test_ragged_table_batch_form(lib, n, weighted):
 
 
 @pytest.mark.parametrize("weighted", [False, True])
-@pytest.mark.parametrize("n", [2, 5, 7, 8, 11, 12, 16, 17, 20, 33, 63, 64, 100, 128])
+@pytest.mark.parametrize("n", [2, 5, 7, 8, 11, 12, 16, 17, 20, 33, 63, 64, 100, 128, 200, 256, 300])
 def test_client_loop_instances_on_a_long_launch(lib, n, weighted):
     """The client loop (reduce_impl.h pipe2_clients: the next client's loads
     before the current client's adds; the PIPE kernel instances) driven on
     purpose: a layout whose launch runs >= 3 rounds of resident
     workgroups (pipe_rule), default plan flags, and the choice asserted
     through fa_plan_launch_form — 2..7 and 12..63 clients take the loop on
-    their full tiles (12..16 since r06), and unweighted 64..128 (r06), the
-    rest the batches.  Client data adversarial
+    their full tiles (12..16 since r06), and unweighted 64..128 (r06) and
+    from 256 over the device pointer table (pipe = 2, r06), the rest the
+    batches.  Client data adversarial
     (2^-20 .. 2^20 magnitudes, generated on the device); the oracle checks
     every small tensor whole and windows of the long one — its head, middle
     and its end (the last partial tile and the ILP-4 tail columns), each
@@ -382,6 +383,8 @@ def test_client_loop_instances_on_a_long_launch(lib, n, weighted):
     layout = BucketLayout.from_manifest(man)
     plan = lib.Plan(layout.segs32, layout.f32_numel, flags=lib.FA_PLAN_GAPS_ARE_PADDING)
     want_pipe = 1 if (2 <= n <= 7 or 12 <= n <= 63 or (not weighted and 64 <= n <= 128)) else 0
+    if not weighted and n >= 256:
+        want_pipe = 2          # the loop over the device pointer table (r06)
     assert plan.launch_form(n, weighted)[2] == want_pipe, (n, weighted, plan.launch_form(n, weighted))
     F = max(layout.f32_numel, 64)
     g = torch.Generator(device=DEV)
