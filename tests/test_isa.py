@@ -199,7 +199,8 @@ def test_reduce_family_is_the_shipped_set(tmp_path):
     shipped variants — U x B in {1x8, 1x16, 2x8, 2x16, 4x8}, deep x weighted,
     POL 5 for the reduce and POL 3 for chain segments: 36 instances; plus the
     client-loop instances (PIPE 1: U = 2, B = 8 / 16, mean and weighted, not
-    deep, POL 5): 40."""
+    deep, POL 5): 40; r06: the loop over the device pointer table (PIPE 2:
+    U = 2, B = 16, deep, mean): 41."""
     names = set()
     for co in _code_objects(LIBS[0], tmp_path):
         names |= {k for k in _kernels(co) if "reduce_kernel" in k}
@@ -213,4 +214,5 @@ def test_reduce_family_is_the_shipped_set(tmp_path):
             for u, b in ((1, 8), (1, 16), (2, 8), (2, 16), (4, 8))
             for d in (0, 1) for w in (0, 1) for c in (0, 1) if not (c and (u, b) == (1, 16))}
     want |= {(2, b, 0, w, 5, 0, 1) for b in (8, 16) for w in (0, 1)}
+    want |= {(2, 16, 1, 0, 5, 0, 2)}
     assert got == want, (sorted(got - want), sorted(want - got))
