@@ -2054,7 +2054,8 @@ struct Launch {
 // -3.1 / -3.2 % and -3.1 / -2.5 / -2.6 %, C100 N = 64 / 100 -3.0 / -2.5 % and
 // -0.3 / -2.2 %, bits equal; the 2048-float table in the batch form alone
 // -1.8 / -3.0 / -3.3 / -1.8 / -2.0 %.  Weighted calls from 64 keep the batch
-// form (r05: the loop +0.4 / +2.4 % at 80 / 128).
+// form (r05: the loop +0.4 / +2.4 % at 80 / 128; r06 again: -0.7 / +0.3 /
+// +1.2 / +3.2 % at 64 / 80 / 100 / 128, profiles/r06_ab_lib_w64_loop.jsonl).
 int pipe_rule(const fa_plan* plan, const Launch& L, int n, bool weighted) {
   (void)plan;
   // r06: unweighted calls of 256 clients and more (the DEEP cascade) on the

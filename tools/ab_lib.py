@@ -63,7 +63,9 @@ CASES = [("cfg2", "wrn16_8_c10", 20, 1), ("cfg4w", "wrn16_8_c100", 20, 1),
          ("c10_n14_tgpu", "wrn16_8_c10", 14, 1), ("c10_n14", "wrn16_8_c10", 14, 1),
          ("c100_n12w", "wrn16_8_c100", 12, 1), ("c10_n11", "wrn16_8_c10", 11, 1),
          ("c10_n13", "wrn16_8_c10", 13, 1), ("c10_n16w", "wrn16_8_c10", 16, 1),
-         ("c10_n150", "wrn16_8_c10", 150, 1), ("c10_n300", "wrn16_8_c10", 300, 1)]
+         ("c10_n150", "wrn16_8_c10", 150, 1), ("c10_n300", "wrn16_8_c10", 300, 1),
+         ("c10_n64w", "wrn16_8_c10", 64, 1), ("c10_n100w", "wrn16_8_c10", 100, 1),
+         ("c100_n64w", "wrn16_8_c100", 64, 1)]
 
 
 def load(path):
