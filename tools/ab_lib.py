@@ -129,10 +129,23 @@ def fill(lib, lay, parts, c, dev):
     return f32, i64
 
 
+def parse_case(name):
+    """A case not in CASES named like c10_n40, c100_n24w, c10_n40_tgpu: the
+    wrn16_8 layout of that class count, that many clients (one set)."""
+    import re
+    m = re.fullmatch(r"c(10|100)_n(\d+)(w?)(_tgpu)?", name)
+    return (name, f"wrn16_8_c{m.group(1)}", int(m.group(2)), 1) if m else None
+
+
 def main():
     paths = sys.argv[1:3]
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 7
     which = sys.argv[4].split(",") if len(sys.argv) > 4 else [c[0] for c in CASES]
+    known = {c[0] for c in CASES}
+    extra = [parse_case(w) for w in which if w not in known]
+    if None in extra:
+        raise SystemExit(f"unknown case in {which}")
+    CASES.extend(extra)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     libs = [load(p) for p in paths]
